@@ -1,0 +1,152 @@
+/*
+ * lazydb_gpu.h — C ABI of the MI355X log-scan engine (liblazydb_gpu.so).
+ *
+ * The engine replaces the per-entry body of LazyDB's log-file replay:
+ *   reference  logfile/log_file.go:116-145   (*LogFile).ReadLogEntry(offset)
+ *              logfile/log_entry.go:81-121    decodeHeader / getEntryCrc
+ *              logfile/log_entry.go:48-78     EncodeEntry (only its size is used at replay)
+ *              index.go:84-95                 the replay loop that calls ReadLogEntry until EOF
+ * One call scans a whole log-file image and returns, in file order, exactly the
+ * (fid, offset, entrySize, key/value extents, status) tuples the replay loop
+ * would have produced, plus how and where the loop stopped.
+ *
+ * No torch / HIP types appear in these signatures: device pointers are plain
+ * pointers, the HIP stream is passed as `void*` (a hipStream_t, NULL = default).
+ * Every function returns an ldb_status (0 = LDB_OK) and never aborts the process.
+ */
+#ifndef LAZYDB_GPU_H
+#define LAZYDB_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDB_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------
+ * Normal terminations of the replay loop (index.go:86-88 `break`) are > 0;
+ * conditions the reference treats as fatal (index.go:90 log.Fatalf, or a Go
+ * runtime panic) are < 0.  LDB_OK (0) is returned by API calls that succeed. */
+typedef enum ldb_status {
+  LDB_OK = 0,
+  LDB_EOF_WINDOW = 1,    /* 38-byte header read hit EOF  -> io.EOF (log_file.go:117-122;
+                            iocontroller/fileio.go:35-37 short ReadAt, iocontroller/mmap.go:46-52) */
+  LDB_EOF_SENTINEL = 2,  /* crc==0 && kSize==0 && vSize==0 -> ErrLogEndOfFile (log_file.go:124-126) */
+  LDB_EOF_KV = 3,        /* key+value read hit EOF -> io.EOF (log_file.go:130-139) */
+  LDB_ERR_CRC = -1,      /* stored crc != recomputed -> ErrInvalidCrc (log_file.go:141-143) */
+  LDB_ERR_MALFORMED = -2,/* the reference would panic (slice bounds in decodeHeader / getEntryCrc
+                            with a negative header size) or get a non-EOF read error */
+  LDB_ERR_CAPACITY = -3, /* output array too small (n_entries still reports the full count) */
+  LDB_ERR_ARG = -4,      /* bad argument */
+  LDB_ERR_HIP = -5,      /* HIP runtime error */
+  LDB_ERR_NOMEM = -6     /* device workspace allocation failed */
+} ldb_status;
+
+/* IOController kind of the LogFile being scanned (logfile/log_file.go:35-41).
+ * It selects the end-of-file bound rule of the reference:
+ *   FileIO: bound = file size, a read of [o, o+n) fails iff o+n >  bound  (os.File.ReadAt)
+ *   Mmap  : bound = mapping length (= MaxLogFileSize), fails iff o+n >= bound (mmap.go:48) */
+typedef enum ldb_io_type { LDB_IO_FILEIO = 0, LDB_IO_MMAP = 1 } ldb_io_type;
+
+/* ---- output tuples -------------------------------------------------------
+ * LDB_TUPLE_INDEX (16 B): what index.go:15-26 needs to build Value{fid, offset, entrySize}
+ * and to slice the key out of the file image:
+ *   key       = image[offset + hdr_size, + k_size)
+ *   value     = image[offset + hdr_size + k_size, + v_size)
+ *   next      = offset + hdr_size + k_size + v_size       (index.go:94 offset += entSize)
+ *   entrySize = enc_hdr_size + k_size + v_size            (index.go:20 len(EncodeEntry(entry)))
+ * `pos` packs: bits [0,40) offset, [40,46) hdr_size, [46,52) enc_hdr_size, [52,60) stat.
+ * (fid is the same for every tuple of a call and is returned in ldb_scan_result.) */
+typedef struct ldb_index_tuple {
+  uint64_t pos;
+  uint32_t k_size;
+  uint32_t v_size;
+} ldb_index_tuple;
+
+#define LDB_POS_OFFSET(p)  ((p) & 0xFFFFFFFFFFull)
+#define LDB_POS_HDR(p)     ((uint32_t)(((p) >> 40) & 0x3F))
+#define LDB_POS_ENCHDR(p)  ((uint32_t)(((p) >> 46) & 0x3F))
+#define LDB_POS_STAT(p)    ((uint32_t)(((p) >> 52) & 0xFF))
+
+/* LDB_TUPLE_ENTRY (48 B): every field of logfile.LogEntry (log_entry.go:35-45) except the
+ * key/value bytes, so a host-side ReadLogEntry(offset) can be answered without re-decoding. */
+typedef struct ldb_entry {
+  uint64_t offset;
+  int64_t expired_at;
+  uint64_t tx_id;
+  uint32_t crc;
+  uint32_t k_size;
+  uint32_t v_size;
+  uint16_t tx_stat;
+  uint8_t stat;
+  uint8_t hdr_size;
+  uint8_t enc_hdr_size;
+  uint8_t pad_[3];
+  uint32_t fid;
+} ldb_entry;
+
+typedef enum ldb_tuple_kind { LDB_TUPLE_INDEX = 0, LDB_TUPLE_ENTRY = 1 } ldb_tuple_kind;
+
+/* Result of one file scan. Tuples [0, n_entries) were produced in file order. */
+typedef struct ldb_scan_result {
+  int32_t status;        /* how the replay loop stopped: LDB_EOF_* (normal) or LDB_ERR_CRC / _MALFORMED;
+                            LDB_ERR_CAPACITY if cap < n_entries (then only cap tuples were written) */
+  uint32_t fid;
+  uint64_t n_entries;    /* entries accepted before the stop */
+  uint64_t end_off;      /* offset at which ReadLogEntry returned `status`; for EOF statuses this is the
+                            append position index.go:97-99 stores into LogFile.Offset */
+  uint32_t n_repairs;    /* diagnostics: speculative-walk repairs performed (0 on well-formed logs) */
+  uint32_t n_regions;    /* diagnostics: parallel regions the image was cut into */
+} ldb_scan_result;
+
+/* ---- context ---------------------------------------------------------------
+ * One context per (thread, device). Holds the device's CRC tables and a
+ * growable scan workspace. Not safe for concurrent calls; use one context per
+ * caller thread (index.go:103-108 replays the 5 value types from 5 goroutines). */
+typedef struct ldb_ctx ldb_ctx;
+
+int ldb_abi_version(void);
+const char* ldb_status_str(int status);
+
+int ldb_ctx_create(int device, ldb_ctx** out);
+int ldb_ctx_destroy(ldb_ctx* ctx);
+/* Pre-size the workspace for images up to max_len bytes, so later scans do no allocation. */
+int ldb_ctx_reserve(ldb_ctx* ctx, uint64_t max_len);
+/* Device bytes of workspace a scan of `len` bytes needs. */
+uint64_t ldb_workspace_bytes(uint64_t len);
+
+/* Device-resident scan (the hot path).  d_image: `len` bytes in device memory, len = bound
+ * (FileIO: the file size; Mmap: the mapping length).  d_out: device array of `cap` tuples of
+ * `tuple_kind`.  d_result: device ldb_scan_result written at the end of the stream work.
+ * Asynchronous with respect to the host: enqueues work on `stream` and returns. */
+int ldb_scan_file_dev(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, uint32_t fid, int io_type,
+                      int tuple_kind, void* d_out, uint64_t cap, ldb_scan_result* d_result, void* stream);
+
+/* Host-memory scan: copies the image to HBM, scans, copies tuples and result back.
+ * Synchronous. This is what a cgo caller holding an mmap'd file uses. */
+int ldb_scan_file(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type,
+                  int tuple_kind, void* h_out, uint64_t cap, ldb_scan_result* h_result);
+
+/* Batch of device-resident files scanned back to back on one stream (one device).
+ * Multi-GPU callers give each device its own context and file subset. */
+int ldb_scan_files_dev(ldb_ctx* ctx, int n_files, const uint8_t* const* d_images, const uint64_t* lens,
+                       const uint32_t* fids, int io_type, int tuple_kind, void* const* d_outs,
+                       const uint64_t* caps, ldb_scan_result* d_results, void* stream);
+
+/* Serial single-lane GPU walker: same results as ldb_scan_file_dev, one entry at a time.
+ * Exists as an independent second implementation for tests; not a fast path. */
+int ldb_scan_file_dev_serial(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, uint32_t fid, int io_type,
+                             int tuple_kind, void* d_out, uint64_t cap, ldb_scan_result* d_result,
+                             void* stream);
+
+/* Timing hook for bench.py: average device time (ms) of the main decode+CRC kernel over the
+ * launches since the last reset, measured with HIP events on the scan stream. */
+int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LAZYDB_GPU_H */

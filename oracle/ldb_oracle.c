@@ -1,0 +1,358 @@
+/*
+ * ldb_oracle.c — CPU restatement of LazyDB's log codec + replay scan.
+ * TEST INFRASTRUCTURE ONLY (see ldb_oracle.h). Every function cites the
+ * reference file:line it restates (paths relative to kakosute/lazydb @ v1).
+ */
+#define _GNU_SOURCE
+#include "ldb_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+/* ------------------------------------------------------------------ CRC-32/IEEE
+ * hash/crc32 IEEE: reflected polynomial 0xEDB88320, crc32.Update(crc, tab, p)
+ * = ~reg(~crc, p). Slicing-by-8 (the same algorithm class as Go's amd64
+ * fallback path for short inputs). */
+static uint32_t crc_tab[8][256];
+static int crc_ready = 0;
+
+static void crc_init_tables(void) {
+  if (crc_ready) return;
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    crc_tab[0][i] = c;
+  }
+  for (int j = 1; j < 8; ++j)
+    for (int i = 0; i < 256; ++i) crc_tab[j][i] = (crc_tab[j - 1][i] >> 8) ^ crc_tab[0][crc_tab[j - 1][i] & 0xff];
+  crc_ready = 1;
+}
+
+uint32_t ldbo_crc32_reg(uint32_t c, const uint8_t* p, size_t n) {
+  crc_init_tables();
+  while (n && ((uintptr_t)p & 7)) {
+    c = crc_tab[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+    --n;
+  }
+  while (n >= 8) {
+    uint32_t a, b;
+    memcpy(&a, p, 4);
+    memcpy(&b, p + 4, 4);
+    a ^= c;
+    c = crc_tab[7][a & 0xff] ^ crc_tab[6][(a >> 8) & 0xff] ^ crc_tab[5][(a >> 16) & 0xff] ^ crc_tab[4][a >> 24] ^
+        crc_tab[3][b & 0xff] ^ crc_tab[2][(b >> 8) & 0xff] ^ crc_tab[1][(b >> 16) & 0xff] ^ crc_tab[0][b >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = crc_tab[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+  return c;
+}
+
+uint32_t ldbo_crc32_update(uint32_t crc, const uint8_t* p, size_t n) { return ~ldbo_crc32_reg(~crc, p, n); }
+
+/* ------------------------------------------------------------------ varints
+ * encoding/binary (Go 1.18) varint.go: Uvarint returns (0, 0) if the buffer is
+ * too short, (0, -(i+1)) on 64-bit overflow (the 11th byte, or a 10th byte > 1). */
+int ldbo_uvarint(const uint8_t* buf, size_t len, uint64_t* out) {
+  uint64_t x = 0;
+  unsigned s = 0;
+  for (size_t i = 0; i < len; ++i) {
+    if (i == 10) { *out = 0; return -(int)(i + 1); }
+    uint8_t b = buf[i];
+    if (b < 0x80) {
+      if (i == 9 && b > 1) { *out = 0; return -(int)(i + 1); }
+      *out = x | ((uint64_t)b << s);
+      return (int)(i + 1);
+    }
+    x |= (uint64_t)(b & 0x7f) << s;
+    s += 7;
+  }
+  *out = 0;
+  return 0;
+}
+
+int ldbo_varint(const uint8_t* buf, size_t len, int64_t* out) {
+  uint64_t ux;
+  int n = ldbo_uvarint(buf, len, &ux);
+  int64_t x = (int64_t)(ux >> 1);
+  if (ux & 1) x = ~x;
+  *out = x;
+  return n;
+}
+
+int ldbo_put_varint(uint8_t* buf, int64_t x) {
+  uint64_t ux = (uint64_t)x << 1;
+  if (x < 0) ux = ~ux;
+  int i = 0;
+  while (ux >= 0x80) {
+    buf[i++] = (uint8_t)ux | 0x80;
+    ux >>= 7;
+  }
+  buf[i++] = (uint8_t)ux;
+  return i;
+}
+
+int ldbo_varint_len(int64_t x) {
+  uint8_t tmp[10];
+  return ldbo_put_varint(tmp, x);
+}
+
+/* ------------------------------------------------------------------ codec */
+/* logfile/log_entry.go:48-78 EncodeEntry */
+size_t ldbo_encode_entry(uint8_t stat, int64_t expired_at, uint64_t tx_id, uint16_t tx_stat, const uint8_t* key,
+                         uint32_t klen, const uint8_t* val, uint32_t vlen, uint8_t* out) {
+  size_t off = 5;
+  out[4] = stat;                                             /* :54 */
+  off += ldbo_put_varint(out + off, expired_at);             /* :57 */
+  off += ldbo_put_varint(out + off, (int64_t)tx_id);         /* :59 */
+  off += ldbo_put_varint(out + off, (int64_t)tx_stat);       /* :61 */
+  off += ldbo_put_varint(out + off, (int64_t)klen);          /* :63 */
+  off += ldbo_put_varint(out + off, (int64_t)vlen);          /* :65 */
+  if (klen) memcpy(out + off, key, klen);                    /* :72 */
+  if (vlen) memcpy(out + off + klen, val, vlen);             /* :73 */
+  size_t size = off + klen + vlen;                           /* :68 */
+  uint32_t crc = ldbo_crc32_update(0, out + 4, size - 4);    /* :75 ChecksumIEEE(newBuf[4:]) */
+  out[0] = (uint8_t)crc;                                     /* :76 LittleEndian.PutUint32 */
+  out[1] = (uint8_t)(crc >> 8);
+  out[2] = (uint8_t)(crc >> 16);
+  out[3] = (uint8_t)(crc >> 24);
+  return size;
+}
+
+/* logfile/log_entry.go:81-107 decodeHeader on the 38-byte window of log_file.go:117.
+ * Go evaluates buf[offset:] before each Varint: a negative offset panics. */
+int ldbo_decode_header(const uint8_t* win, ldbo_header* h) {
+  memset(h, 0, sizeof(*h));
+  h->crc = (uint32_t)win[0] | ((uint32_t)win[1] << 8) | ((uint32_t)win[2] << 16) | ((uint32_t)win[3] << 24); /* :86 */
+  h->stat = win[4];                                                                                          /* :87 */
+  int off = 5;
+  int64_t v[5];
+  for (int f = 0; f < 5; ++f) {
+    if (off < 0) return LDB_ERR_MALFORMED; /* buf[offset:] with offset < 0 */
+    int n = ldbo_varint(win + off, (size_t)(LDBO_MAX_HEADER - off), &v[f]);
+    off += n;
+  }
+  h->expired_at = v[0];           /* :91 */
+  h->tx_id = (uint64_t)v[1];      /* :94 */
+  h->tx_stat = (uint16_t)v[2];    /* :97 */
+  h->k_size = (uint32_t)v[3];     /* :100 */
+  h->v_size = (uint32_t)v[4];     /* :103 */
+  h->size = off;                  /* :106 */
+  /* the header EncodeEntry would re-emit (index.go:20 uses its length) */
+  h->enc_size = 5 + ldbo_varint_len(h->expired_at) + ldbo_varint_len((int64_t)h->tx_id) +
+                ldbo_varint_len((int64_t)h->tx_stat) + ldbo_varint_len((int64_t)h->k_size) +
+                ldbo_varint_len((int64_t)h->v_size);
+  return LDB_OK;
+}
+
+/* IOController read-bound rules (iocontroller/fileio.go:35-37 via os.File.ReadAt;
+ * iocontroller/mmap.go:46-52). Returns 1 if Read(b, off) with len(b)=n fails with EOF. */
+static int read_eof(uint64_t len, int io_type, int64_t off, uint64_t n) {
+  if (io_type == LDB_IO_MMAP) {
+    if (off < 0 || (uint64_t)off >= len || (uint64_t)off + n >= len) return 1; /* mmap.go:48 */
+    return 0;
+  }
+  return (uint64_t)off + n > len; /* ReadAt short read -> io.EOF */
+}
+
+/* logfile/log_file.go:116-145 ReadLogEntry */
+int ldbo_read_log_entry(const uint8_t* img, uint64_t len, int io_type, uint64_t off, ldbo_header* h,
+                        uint64_t* entry_size) {
+  /* :117-122 headerBuf := make([]byte, MaxHeaderSize); Read(headerBuf, offset) */
+  if (read_eof(len, io_type, (int64_t)off, LDBO_MAX_HEADER)) return LDB_EOF_WINDOW;
+  /* :123 decodeHeader */
+  if (ldbo_decode_header(img + off, h) != LDB_OK) return LDB_ERR_MALFORMED;
+  /* :124-126 zero sentinel */
+  if (h->crc == 0 && h->k_size == 0 && h->v_size == 0) return LDB_EOF_SENTINEL;
+  int64_t size = h->size;
+  uint64_t kv = (uint64_t)h->k_size + (uint64_t)h->v_size;
+  /* :130-139 read k+v at offset+size */
+  if (h->k_size > 0 || h->v_size > 0) {
+    int64_t at = (int64_t)off + size;
+    if (io_type == LDB_IO_FILEIO && at < 0) return LDB_ERR_MALFORMED; /* ReadAt: "negative offset" (not io.EOF) */
+    if (read_eof(len, io_type, at, kv)) return LDB_EOF_KV;
+  }
+  /* :141-143 getEntryCrc(headerBuf[:size], le) (log_entry.go:110-121) */
+  if (size < 0) return LDB_ERR_MALFORMED; /* headerBuf[:size] panics */
+  uint32_t crc = 0;
+  if (size > 4) crc = ldbo_crc32_update(0, img + off + 4, (size_t)(size - 4) + kv); /* buf[4:] ++ Key ++ Value */
+  if (crc != h->crc) return LDB_ERR_CRC;
+  *entry_size = (uint64_t)(size + (int64_t)kv); /* :128 entrySize = size + kSize + vSize */
+  return LDB_OK;
+}
+
+static void emit(void* out, int tuple_kind, uint64_t idx, uint64_t off, const ldbo_header* h, uint32_t fid) {
+  if (tuple_kind == LDB_TUPLE_ENTRY) {
+    ldb_entry* e = (ldb_entry*)out + idx;
+    memset(e, 0, sizeof(*e));
+    e->offset = off;
+    e->expired_at = h->expired_at;
+    e->tx_id = h->tx_id;
+    e->crc = h->crc;
+    e->k_size = h->k_size;
+    e->v_size = h->v_size;
+    e->tx_stat = h->tx_stat;
+    e->stat = h->stat;
+    e->hdr_size = (uint8_t)h->size;
+    e->enc_hdr_size = (uint8_t)h->enc_size;
+    e->fid = fid;
+  } else {
+    ldb_index_tuple* t = (ldb_index_tuple*)out + idx;
+    t->pos = (off & 0xFFFFFFFFFFull) | ((uint64_t)(h->size & 0x3F) << 40) | ((uint64_t)(h->enc_size & 0x3F) << 46) |
+             ((uint64_t)h->stat << 52);
+    t->k_size = h->k_size;
+    t->v_size = h->v_size;
+  }
+}
+
+/* index.go:84-95: offset := 0; for { ReadLogEntry(offset); EOF -> break; err -> fatal; offset += entSize } */
+int ldbo_scan(const uint8_t* img, uint64_t len, int io_type, uint32_t fid, int tuple_kind, void* out, uint64_t cap,
+              ldb_scan_result* res) {
+  uint64_t off = 0, n = 0;
+  int st;
+  for (;;) {
+    ldbo_header h;
+    uint64_t es = 0;
+    st = ldbo_read_log_entry(img, len, io_type, off, &h, &es);
+    if (st != LDB_OK) break;
+    if (out && n < cap) emit(out, tuple_kind, n, off, &h, fid);
+    ++n;
+    off += es;
+  }
+  memset(res, 0, sizeof(*res));
+  res->status = (out && n > cap) ? LDB_ERR_CAPACITY : st;
+  res->fid = fid;
+  res->n_entries = n;
+  res->end_off = off;
+  return LDB_OK;
+}
+
+/* The per-entry work of the reference replay, restated with the same system calls
+ * and allocations: log_file.go:117 make+Read(38), :132 make+Read(k+v),
+ * :141 getEntryCrc, index.go:20 EncodeEntry (a second allocation + CRC pass). */
+static int faithful_read(int fd, uint64_t len, int io_type, int64_t off, uint8_t* buf, uint64_t n) {
+  if (read_eof(len, io_type, off, n)) return LDB_EOF_WINDOW;
+  uint64_t got = 0;
+  while (got < n) {
+    ssize_t r = pread(fd, buf + got, n - got, off + (int64_t)got);
+    if (r <= 0) return LDB_EOF_WINDOW;
+    got += (uint64_t)r;
+  }
+  return LDB_OK;
+}
+
+int ldbo_scan_faithful(int fd, uint64_t len, int io_type, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                       ldb_scan_result* res) {
+  uint64_t off = 0, n = 0;
+  int st = LDB_OK;
+  for (;;) {
+    uint8_t* hdr = (uint8_t*)malloc(LDBO_MAX_HEADER);
+    if (faithful_read(fd, len, io_type, (int64_t)off, hdr, LDBO_MAX_HEADER) != LDB_OK) {
+      free(hdr);
+      st = LDB_EOF_WINDOW;
+      break;
+    }
+    ldbo_header h;
+    if (ldbo_decode_header(hdr, &h) != LDB_OK) { free(hdr); st = LDB_ERR_MALFORMED; break; }
+    if (h.crc == 0 && h.k_size == 0 && h.v_size == 0) { free(hdr); st = LDB_EOF_SENTINEL; break; }
+    uint64_t kv = (uint64_t)h.k_size + h.v_size;
+    uint8_t* kvb = NULL;
+    if (kv) {
+      int64_t at = (int64_t)off + h.size;
+      if (io_type == LDB_IO_FILEIO && at < 0) { free(hdr); st = LDB_ERR_MALFORMED; break; }
+      if (read_eof(len, io_type, at, kv)) { free(hdr); st = LDB_EOF_KV; break; }
+      kvb = (uint8_t*)malloc(kv);
+      if (faithful_read(fd, len, io_type, at, kvb, kv) != LDB_OK) { free(hdr); free(kvb); st = LDB_EOF_KV; break; }
+    }
+    if (h.size < 0) { free(hdr); free(kvb); st = LDB_ERR_MALFORMED; break; }
+    uint32_t crc = 0;
+    if (h.size > 4) {
+      crc = ldbo_crc32_update(0, hdr + 4, (size_t)h.size - 4);
+      crc = ldbo_crc32_update(crc, kvb, h.k_size);
+      crc = ldbo_crc32_update(crc, kvb ? kvb + h.k_size : NULL, h.v_size);
+    }
+    if (crc != h.crc) { free(hdr); free(kvb); st = LDB_ERR_CRC; break; }
+    /* index.go:15-26 buildStrIndex: SDelete -> Delete(key); else size from EncodeEntry */
+    if (h.stat != 1) {
+      uint8_t* enc = (uint8_t*)malloc(LDBO_MAX_HEADER + kv);
+      size_t es = ldbo_encode_entry(h.stat, h.expired_at, h.tx_id, h.tx_stat, kvb, h.k_size,
+                                    kvb ? kvb + h.k_size : NULL, h.v_size, enc);
+      if ((int)es - (int)kv != h.enc_size) { free(enc); free(hdr); free(kvb); st = LDB_ERR_MALFORMED; break; }
+      free(enc);
+    }
+    if (out && n < cap) emit(out, LDB_TUPLE_INDEX, n, off, &h, fid);
+    ++n;
+    off += (uint64_t)(h.size + (int64_t)kv);
+    free(hdr);
+    free(kvb);
+  }
+  memset(res, 0, sizeof(*res));
+  res->status = st;
+  res->fid = fid;
+  res->n_entries = n;
+  res->end_off = off;
+  return LDB_OK;
+}
+
+/* ------------------------------------------------------------------ generator */
+uint64_t ldbo_splitmix64(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static const char kAlphabet[] = "0123456789abcdefghijklmnopqrstuvwxyz"; /* bench/db_bench_test.go:21-27 */
+
+uint64_t ldbo_gen_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint32_t ksize, uint32_t vsize,
+                      int value_mode, double zipf_s, uint32_t zipf_max, uint64_t max_entries, uint64_t* end_off) {
+  uint64_t st = seed;
+  double* cdf = NULL;
+  if (value_mode == 1) {
+    cdf = (double*)malloc(sizeof(double) * zipf_max);
+    double acc = 0;
+    for (uint32_t r = 1; r <= zipf_max; ++r) {
+      acc += pow((double)r, -zipf_s);
+      cdf[r - 1] = acc;
+    }
+    for (uint32_t r = 0; r < zipf_max; ++r) cdf[r] /= acc;
+  }
+  uint32_t vmax = value_mode == 1 ? 16u * zipf_max : vsize;
+  uint8_t* key = (uint8_t*)malloc(ksize + 32);
+  uint8_t* val = (uint8_t*)malloc(vmax + 8);
+  uint64_t off = 0, n = 0;
+  for (; n < max_entries; ++n) {
+    uint32_t vl = vsize;
+    if (value_mode == 1) {
+      double u = (double)(ldbo_splitmix64(&st) >> 11) * (1.0 / 9007199254740992.0);
+      uint32_t lo = 0, hi = zipf_max - 1;
+      while (lo < hi) {
+        uint32_t mid = (lo + hi) / 2;
+        if (cdf[mid] < u) lo = mid + 1; else hi = mid;
+      }
+      vl = 16u * (lo + 1);
+    }
+    /* key "key-" + zero-padded decimal n, exactly ksize bytes */
+    char num[32];
+    int nd = 0;
+    uint64_t t = n;
+    do { num[nd++] = (char)('0' + t % 10); t /= 10; } while (t);
+    memset(key, '0', ksize);
+    if (ksize >= 4) memcpy(key, "key-", 4);
+    for (int i = 0; i < nd && (uint32_t)i < ksize - 4; ++i) key[ksize - 1 - i] = (uint8_t)num[i];
+    for (uint32_t i = 0; i < vl; i += 8) {
+      uint64_t r = ldbo_splitmix64(&st);
+      for (int b = 0; b < 8 && i + b < vl; ++b) { val[i + b] = (uint8_t)kAlphabet[(r & 0xff) % 36]; r >>= 8; }
+    }
+    uint64_t need = 5 + ldbo_varint_len(0) * 3 + ldbo_varint_len(ksize) + ldbo_varint_len(vl) + ksize + vl;
+    if (off + need > cap_bytes) break; /* db.go:485 rollover: the entry goes to the next file */
+    off += ldbo_encode_entry(0, 0, 0, 0, key, ksize, val, vl, img + off);
+  }
+  free(key);
+  free(val);
+  free(cdf);
+  if (end_off) *end_off = off;
+  return n;
+}

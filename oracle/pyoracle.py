@@ -1,0 +1,181 @@
+"""Pure-Python restatement of LazyDB's log codec and replay scan.
+
+TEST INFRASTRUCTURE ONLY: an independent second oracle (CRC from zlib, varints
+written from the Go spec) used to cross-check oracle/ldb_oracle.c and to write
+the small golden fixtures under tests/golden/.  Only tests/, smoke() and
+bench.py's cpu_baseline may use anything under oracle/.
+
+Parity pinning: the Go reference cannot be built or run here (no Go
+toolchain; mmap/mmap.go:24 `msync` vs mmap/mmap_linux.go:75 `mSync`).  This
+module reproduces the reference's literal vectors in
+logfile/log_entry_test.go:18-32, 57-69, 93-104 (see tests/test_oracle_golden.py).
+"""
+from __future__ import annotations
+
+import struct
+import zlib
+from dataclasses import dataclass
+
+MAX_HEADER = 38  # logfile/log_entry.go:32
+
+FILEIO, MMAP = 0, 1  # logfile/log_file.go:35-41
+
+OK, EOF_WINDOW, EOF_SENTINEL, EOF_KV = 0, 1, 2, 3
+ERR_CRC, ERR_MALFORMED = -1, -2
+
+
+def uvarint(buf: bytes) -> tuple[int, int]:
+    """encoding/binary.Uvarint (Go 1.18)."""
+    x = 0
+    s = 0
+    for i, b in enumerate(buf):
+        if i == 10:
+            return 0, -(i + 1)
+        if b < 0x80:
+            if i == 9 and b > 1:
+                return 0, -(i + 1)
+            return x | (b << s), i + 1
+        x |= (b & 0x7F) << s
+        s += 7
+    return 0, 0
+
+
+def varint(buf: bytes) -> tuple[int, int]:
+    """encoding/binary.Varint: zigzag over Uvarint."""
+    ux, n = uvarint(buf)
+    x = ux >> 1
+    if ux & 1:
+        x = ~x
+    # int64(ux >> 1) is always non-negative before the complement
+    return x, n
+
+
+def put_varint(x: int) -> bytes:
+    """encoding/binary.PutVarint for an int64 x."""
+    x &= (1 << 64) - 1
+    sx = x - (1 << 64) if x >> 63 else x
+    ux = (x << 1) & ((1 << 64) - 1)
+    if sx < 0:
+        ux = (~ux) & ((1 << 64) - 1)
+    out = bytearray()
+    while ux >= 0x80:
+        out.append((ux & 0x7F) | 0x80)
+        ux >>= 7
+    out.append(ux)
+    return bytes(out)
+
+
+def _i64(x: int) -> int:
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >> 63 else x
+
+
+@dataclass
+class Entry:
+    """logfile.LogEntry (log_entry.go:35-45)."""
+
+    crc: int = 0
+    expired_at: int = 0
+    stat: int = 0
+    tx_id: int = 0
+    tx_stat: int = 0
+    k_size: int = 0
+    v_size: int = 0
+    key: bytes = b""
+    value: bytes = b""
+
+
+def encode_entry(e: Entry) -> bytes:
+    """logfile.EncodeEntry (log_entry.go:48-78)."""
+    hdr = bytearray(5)
+    hdr[4] = e.stat & 0xFF
+    hdr += put_varint(e.expired_at)
+    hdr += put_varint(_i64(e.tx_id))
+    hdr += put_varint(e.tx_stat & 0xFFFF)
+    hdr += put_varint(len(e.key))
+    hdr += put_varint(len(e.value))
+    buf = bytes(hdr) + e.key + e.value
+    crc = zlib.crc32(buf[4:]) & 0xFFFFFFFF
+    return struct.pack("<I", crc) + buf[4:]
+
+
+def decode_header(win: bytes):
+    """logfile.decodeHeader (log_entry.go:81-107). Returns (Entry, size) or None if Go panics."""
+    if len(win) <= 4:
+        return None, 0
+    e = Entry()
+    e.crc = struct.unpack_from("<I", win, 0)[0]
+    e.stat = win[4]
+    off = 5
+    vals = []
+    for _ in range(5):
+        if off < 0:
+            return "panic", 0
+        v, n = varint(win[off:])
+        vals.append(v)
+        off += n
+    e.expired_at = _i64(vals[0])
+    e.tx_id = vals[1] & ((1 << 64) - 1)
+    e.tx_stat = vals[2] & 0xFFFF
+    e.k_size = vals[3] & 0xFFFFFFFF
+    e.v_size = vals[4] & 0xFFFFFFFF
+    return e, off
+
+
+def enc_header_size(e: Entry) -> int:
+    return 5 + len(put_varint(e.expired_at)) + len(put_varint(_i64(e.tx_id))) + len(put_varint(e.tx_stat)) + \
+        len(put_varint(e.k_size)) + len(put_varint(e.v_size))
+
+
+def _read_eof(length: int, io_type: int, off: int, n: int) -> bool:
+    if io_type == MMAP:  # iocontroller/mmap.go:48
+        return off < 0 or off >= length or off + n >= length
+    return off + n > length  # os.File.ReadAt short read -> io.EOF
+
+
+def read_log_entry(img: bytes, io_type: int, off: int):
+    """(*LogFile).ReadLogEntry (log_file.go:116-145): (status, Entry|None, size, hdr_size)."""
+    length = len(img)
+    if _read_eof(length, io_type, off, MAX_HEADER):
+        return EOF_WINDOW, None, 0, 0
+    e, size = decode_header(img[off:off + MAX_HEADER])
+    if e == "panic":
+        return ERR_MALFORMED, None, 0, 0
+    if e.crc == 0 and e.k_size == 0 and e.v_size == 0:
+        return EOF_SENTINEL, None, 0, 0
+    kv = e.k_size + e.v_size
+    if e.k_size > 0 or e.v_size > 0:
+        at = off + size
+        if io_type == FILEIO and at < 0:
+            return ERR_MALFORMED, None, 0, 0
+        if _read_eof(length, io_type, at, kv):
+            return EOF_KV, None, 0, 0
+        e.key = bytes(img[at:at + e.k_size])
+        e.value = bytes(img[at + e.k_size:at + kv])
+    if size < 0:
+        return ERR_MALFORMED, None, 0, 0
+    crc = 0
+    if size > 4:
+        crc = zlib.crc32(bytes(img[off + 4:off + size]))
+        crc = zlib.crc32(e.key, crc)
+        crc = zlib.crc32(e.value, crc)
+    if crc != e.crc:
+        return ERR_CRC, None, 0, 0
+    return OK, e, size + kv, size
+
+
+def scan(img: bytes, io_type: int = FILEIO, fid: int = 0):
+    """The replay loop of index.go:84-95. Returns (status, end_off, tuples) with
+    tuples = [(offset, hdr_size, enc_hdr_size, stat, k_size, v_size)]."""
+    off = 0
+    out = []
+    while True:
+        st, e, es, h = read_log_entry(img, io_type, off)
+        if st != OK:
+            return st, off, out
+        out.append((off, h, enc_header_size(e), e.stat, e.k_size, e.v_size))
+        off += es
+
+
+def pack_pos(off: int, h: int, eh: int, stat: int) -> int:
+    return (off & 0xFFFFFFFFFF) | ((h & 0x3F) << 40) | ((eh & 0x3F) << 46) | ((stat & 0xFF) << 52)
