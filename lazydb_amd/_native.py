@@ -1,0 +1,86 @@
+"""ctypes binding of liblazydb_gpu.so (the C ABI in include/lazydb_gpu.h).
+
+The library is the product: hand-written gfx950 kernels behind a C ABI. There is
+no CPU fallback — if the library is missing or no GPU is visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "liblazydb_gpu.so")
+
+LDB_OK = 0
+EOF_WINDOW, EOF_SENTINEL, EOF_KV = 1, 2, 3
+ERR_CRC, ERR_MALFORMED, ERR_CAPACITY, ERR_ARG, ERR_HIP, ERR_NOMEM = -1, -2, -3, -4, -5, -6
+FILEIO, MMAP = 0, 1
+TUPLE_INDEX, TUPLE_ENTRY = 0, 1
+
+INDEX_TUPLE = np.dtype([("pos", "<u8"), ("k_size", "<u4"), ("v_size", "<u4")])
+ENTRY_TUPLE = np.dtype([("offset", "<u8"), ("expired_at", "<i8"), ("tx_id", "<u8"), ("crc", "<u4"),
+                        ("k_size", "<u4"), ("v_size", "<u4"), ("tx_stat", "<u2"), ("stat", "u1"),
+                        ("hdr_size", "u1"), ("enc_hdr_size", "u1"), ("pad_", "u1", (3,)), ("fid", "<u4")])
+
+
+class ScanResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("fid", C.c_uint32), ("n_entries", C.c_uint64), ("end_off", C.c_uint64),
+                ("n_repairs", C.c_uint32), ("n_regions", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+RESULT_BYTES = C.sizeof(ScanResult)
+assert RESULT_BYTES == 32
+
+_lib = None
+
+
+class LdbError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LdbError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        L = C.CDLL(LIB_PATH)
+        vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+        L.ldb_abi_version.restype = i32
+        L.ldb_status_str.argtypes = [i32]
+        L.ldb_status_str.restype = C.c_char_p
+        L.ldb_ctx_create.argtypes = [i32, C.POINTER(vp)]
+        L.ldb_ctx_destroy.argtypes = [vp]
+        L.ldb_ctx_reserve.argtypes = [vp, u64]
+        L.ldb_workspace_bytes.argtypes = [u64]
+        L.ldb_workspace_bytes.restype = u64
+        L.ldb_scan_file_dev.argtypes = [vp, vp, u64, u32, i32, i32, vp, u64, vp, vp]
+        L.ldb_scan_file_dev_serial.argtypes = [vp, vp, u64, u32, i32, i32, vp, u64, vp, vp]
+        L.ldb_scan_file.argtypes = [vp, vp, u64, u32, i32, i32, vp, u64, C.POINTER(ScanResult)]
+        L.ldb_scan_files_dev.argtypes = [vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]
+        L.ldb_kernel_timing.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)]
+        for fn in ("ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve", "ldb_scan_file_dev",
+                   "ldb_scan_file_dev_serial", "ldb_scan_file", "ldb_scan_files_dev", "ldb_kernel_timing"):
+            getattr(L, fn).restype = i32
+        if L.ldb_abi_version() != 1:
+            raise LdbError("liblazydb_gpu ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
+           "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
+           "ldb_scan_file_dev_serial", "ldb_kernel_timing")
+
+
+def status_str(s: int) -> str:
+    return lib().ldb_status_str(s).decode()
+
+
+def check(rc: int, what: str):
+    if rc != LDB_OK:
+        raise LdbError(f"{what}: {status_str(rc)} ({rc})")

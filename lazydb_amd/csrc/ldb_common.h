@@ -1,0 +1,196 @@
+// ldb_common.h — host/device codec primitives of the MI355X log-scan engine.
+//
+// Restates, for gfx950 kernels and the host runtime, the entry format and the
+// per-entry decision procedure of the reference:
+//   logfile/log_entry.go:81-107  decodeHeader (Go encoding/binary.Varint semantics)
+//   logfile/log_entry.go:110-121 getEntryCrc  (CRC-32/IEEE over [off+4, off+entrySize))
+//   logfile/log_file.go:116-145  ReadLogEntry (EOF rules, sentinel, kv read, crc check)
+//   iocontroller/fileio.go:35-37, iocontroller/mmap.go:46-52  (read-bound rules)
+// Everything here is integer/byte arithmetic; no floating point.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/lazydb_gpu.h"
+
+#if defined(__HIPCC__)
+#define LDB_HD __host__ __device__ __forceinline__
+#else
+#define LDB_HD inline
+#endif
+
+namespace ldb {
+
+constexpr int kMaxHeader = 38;            // logfile/log_entry.go:32
+constexpr uint32_t kPoly = 0xEDB88320u;   // CRC-32/IEEE, reflected
+constexpr uint32_t kNone32 = 0xFFFFFFFFu;
+constexpr uint64_t kNone64 = ~0ull;
+
+// Internal "continue" status of a region/lane walk (not terminated).
+constexpr int kCont = 0;
+
+// ---------------------------------------------------------------- varints
+// encoding/binary.Uvarint (Go 1.18): (0, 0) when the buffer ends first, (0, -(i+1)) on
+// overflow (an 11th byte, or a 10th byte > 1).  `avail` = bytes left in the 38-byte window.
+template <class Fetch>
+LDB_HD int go_uvarint(Fetch fetch, int at, int avail, uint64_t* out) {
+  uint64_t x = 0;
+  unsigned s = 0;
+  for (int i = 0; i < avail; ++i) {
+    if (i == 10) { *out = 0; return -(i + 1); }
+    const uint32_t b = fetch(at + i);
+    if (b < 0x80u) {
+      if (i == 9 && b > 1u) { *out = 0; return -(i + 1); }
+      *out = x | ((uint64_t)b << s);
+      return i + 1;
+    }
+    x |= (uint64_t)(b & 0x7fu) << s;
+    s += 7;
+  }
+  *out = 0;
+  return 0;
+}
+
+LDB_HD int64_t zigzag(uint64_t ux) {
+  int64_t x = (int64_t)(ux >> 1);
+  return (ux & 1) ? ~x : x;
+}
+
+// len(binary.PutVarint(x)) — what EncodeEntry emits (log_entry.go:57-66).
+LDB_HD int varint_len(int64_t x) {
+  uint64_t ux = (uint64_t)x << 1;
+  if (x < 0) ux = ~ux;
+  int n = 1;
+  while (ux >= 0x80u) { ux >>= 7; ++n; }
+  return n;
+}
+
+// Decoded header: the scalar fields of logfile.LogEntry (log_entry.go:35-45).
+struct Header {
+  uint32_t crc;
+  uint32_t k_size;
+  uint32_t v_size;
+  uint32_t stat;       // uint8 Status
+  int64_t expired_at;
+  uint64_t tx_id;
+  uint32_t tx_stat;    // uint16 TxStatus
+  int32_t size;        // decodeHeader's returned offset; may be negative for malformed varints
+  int32_t enc_size;    // header length EncodeEntry would re-emit (index.go:20 uses it)
+  uint32_t raw_tx_stat_ok;  // decoded TxStat varint was canonical and in [0, 2] (plausibility only)
+  uint32_t canonical;       // every varint minimal and non-empty (plausibility only)
+};
+
+// logfile.decodeHeader over the 38-byte window at `fetch(0..37)`.
+// Returns false where Go would panic (buf[offset:] with offset < 0).
+template <class Fetch>
+LDB_HD bool decode_header(Fetch fetch, Header* h) {
+  h->crc = fetch(0) | (fetch(1) << 8) | (fetch(2) << 16) | (fetch(3) << 24);  // :86
+  h->stat = fetch(4);                                                         // :87
+  int off = 5;
+  uint64_t v[5];
+  uint32_t canon = 1;
+  for (int f = 0; f < 5; ++f) {
+    if (off < 0) return false;
+    const int n = go_uvarint(fetch, off, kMaxHeader - off, &v[f]);
+    // minimal encoding: n > 0 and (n == 1 or the last byte != 0)
+    if (n <= 0 || (n > 1 && fetch(off + n - 1) == 0)) canon = 0;
+    off += n;
+  }
+  const int64_t ea = zigzag(v[0]), tx = zigzag(v[1]), ts = zigzag(v[2]), ks = zigzag(v[3]), vs = zigzag(v[4]);
+  h->expired_at = ea;                 // :91
+  h->tx_id = (uint64_t)tx;            // :94
+  h->tx_stat = (uint32_t)(uint16_t)ts;// :97
+  h->k_size = (uint32_t)ks;           // :100
+  h->v_size = (uint32_t)vs;           // :103
+  h->size = off;                      // :106
+  h->raw_tx_stat_ok = (ts >= 0 && ts <= 2) ? 1u : 0u;
+  h->canonical = canon && ks >= 0 && vs >= 0 && ks <= 0xFFFFFFFFll && vs <= 0xFFFFFFFFll;
+  h->enc_size = 5 + varint_len(ea) + varint_len(tx) + varint_len((int64_t)h->tx_stat) +
+                varint_len((int64_t)h->k_size) + varint_len((int64_t)h->v_size);
+  return true;
+}
+
+// IOController.Read(b, off) with len(b) = n fails with io.EOF?
+//   FileIO: os.File.ReadAt short read  <=>  off + n > len      (fileio.go:35-37)
+//   Mmap  : off < 0 || off >= len || off + n >= len            (mmap.go:48)
+LDB_HD bool read_eof(uint64_t len, int io_type, int64_t off, uint64_t n) {
+  if (io_type == LDB_IO_MMAP) return off < 0 || (uint64_t)off >= len || (uint64_t)off + n >= len;
+  return (uint64_t)off + n > len;
+}
+
+// Outcome of ReadLogEntry(off) up to (not including) the CRC comparison.
+struct EntryInfo {
+  int status;          // kCont = decoded and readable (CRC still to check), else LDB_EOF_* / LDB_ERR_MALFORMED
+  Header h;
+  uint64_t size;       // entrySize = size + kSize + vSize (valid when status == kCont)
+  // CRC span [off + 4, off + size) exists iff h.size > 4; otherwise getEntryCrc returns 0 (log_entry.go:111)
+};
+
+// log_file.go:116-140: window read, decodeHeader, sentinel, k+v read.
+// `fetch(i)` returns image byte off+i for i in [0, 38) and is only called after the window check.
+template <class Fetch>
+LDB_HD EntryInfo classify_entry(Fetch fetch, uint64_t len, int io_type, uint64_t off) {
+  EntryInfo r;
+  r.size = 0;
+  if (read_eof(len, io_type, (int64_t)off, kMaxHeader)) { r.status = LDB_EOF_WINDOW; return r; }  // :117-122
+  if (!decode_header(fetch, &r.h)) { r.status = LDB_ERR_MALFORMED; return r; }                    // :123
+  if (r.h.crc == 0 && r.h.k_size == 0 && r.h.v_size == 0) { r.status = LDB_EOF_SENTINEL; return r; }  // :124-126
+  const uint64_t kv = (uint64_t)r.h.k_size + (uint64_t)r.h.v_size;
+  const int64_t size = r.h.size;
+  if (r.h.k_size > 0 || r.h.v_size > 0) {  // :130-139
+    const int64_t at = (int64_t)off + size;
+    if (io_type == LDB_IO_FILEIO && at < 0) { r.status = LDB_ERR_MALFORMED; return r; }  // ReadAt: negative offset
+    if (read_eof(len, io_type, at, kv)) { r.status = LDB_EOF_KV; return r; }
+  }
+  if (size < 0) { r.status = LDB_ERR_MALFORMED; return r; }  // headerBuf[:size] panics (:141)
+  r.size = (uint64_t)size + kv;
+  r.status = kCont;
+  return r;
+}
+
+// Heuristic used only to pick speculative walk starts (never to decide results):
+// a header LazyDB's writer (db.go:473-523 -> EncodeEntry) could have produced.
+LDB_HD bool plausible_start(const EntryInfo& e) {
+  return e.status == kCont && e.h.stat <= 2 && e.h.raw_tx_stat_ok && e.h.canonical && e.h.expired_at >= 0 &&
+         e.h.size == e.h.enc_size && e.h.size >= 10 && e.h.crc != 0;
+}
+
+LDB_HD uint64_t pack_pos(uint64_t off, const Header& h) {
+  return (off & 0xFFFFFFFFFFull) | ((uint64_t)(h.size & 0x3F) << 40) | ((uint64_t)(h.enc_size & 0x3F) << 46) |
+         ((uint64_t)(h.stat & 0xFF) << 52);
+}
+
+// ---------------------------------------------------------------- GF(2) CRC algebra
+// Reflected CRC register update over zero bytes is multiplication by x^(8n) mod P.
+// multmodp(a, b) = a*b mod P in the reflected bit order (bit 31 = x^0), as zlib's crc32_combine.
+LDB_HD uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
+  }
+  return p;
+}
+
+// x^(8n) mod P (reflected); host side, used to build the shift tables.
+inline uint32_t x8n_modp(uint64_t n) {
+  uint32_t p = 1u << 31;      // x^0
+  uint32_t sq = 1u << 23;     // x^8
+  while (n) {
+    if (n & 1) p = multmodp(sq, p);
+    sq = multmodp(sq, sq);
+    n >>= 1;
+  }
+  return p;
+}
+
+// Byte-at-a-time register step (8-bit table T0).
+LDB_HD uint32_t crc_byte(const uint32_t* t0, uint32_t reg, uint32_t byte) {
+  return t0[(reg ^ byte) & 0xFFu] ^ (reg >> 8);
+}
+
+}  // namespace ldb

@@ -1,0 +1,174 @@
+// ldb_pipeline.h — cross-region stitching of the per-region summaries (host+device).
+//
+// After every region ran region_process speculatively, the chain of
+// ReadLogEntry positions (index.go:84-95) is verified region to region:
+//   link    : a region's exit must be the start of the region it lands in, and every region it
+//             jumps over must contain no entry start of its own;
+//   repair  : walk the true chain from the first broken link, re-running regions with the
+//             entering position forced, until it merges back into a verified region;
+//   combine : entries that cross region boundaries are CRC-verified by folding the regions'
+//             raw pieces with GF(2) shifts;
+//   final   : the scan stops at the first terminal along the chain; tuples before it are kept.
+#pragma once
+
+#include "ldb_wave.h"
+
+namespace ldb {
+
+struct Pipe {
+  const uint8_t* img;
+  uint64_t len;
+  int io;
+  uint32_t fid;
+  uint64_t nreg;
+  const uint32_t* gtab;     // kTabWords table block (global copy)
+  const uint32_t* xw;       // x^(8n) mod P for n = 0..kW
+  // SoA region summaries
+  uint64_t* start;
+  uint64_t* exitp;
+  uint64_t* soff;
+  int32_t* status;
+  uint32_t* count;
+  uint32_t* rpre;
+  uint32_t* rout;
+  uint32_t* scrc;
+  uint32_t* sflag;
+  ldb_index_tuple* scratch;   // nreg * kRegionCap
+  // control
+  int64_t* fail_src;          // regions whose outgoing link failed (-1: region 0 does not start at 0)
+  uint32_t* ctr;              // [0] fail count, [1] overflow, [2] repairs, [3] first terminal region (min)
+  uint64_t* tpos;             // [0] min terminal position, [1] its status (packed with position)
+  uint64_t* blk;              // per 1024-region block: [0] count sum
+  uint64_t* blk_prefix;
+  void* out;
+  uint64_t cap;
+  int kind;
+  ldb_scan_result* result;
+};
+
+constexpr int kBlkRegions = 1024;
+
+LDB_HD void store_region(const Pipe& p, uint64_t r, const RegionSum& s) {
+  p.start[r] = s.start;
+  p.exitp[r] = s.exitp;
+  p.soff[r] = s.soff;
+  p.status[r] = s.status;
+  p.count[r] = s.count;
+  p.rpre[r] = s.rpre;
+  p.rout[r] = s.rout;
+  p.scrc[r] = s.scrc;
+  p.sflag[r] = s.sflag;
+}
+
+LDB_HD uint32_t region_len(const Pipe& p, uint64_t r) {
+  const uint64_t R0 = r * (uint64_t)kW;
+  return (uint32_t)((p.len - R0) < (uint64_t)kW ? (p.len - R0) : (uint64_t)kW);
+}
+
+// Link check of region r. Returns true when r's outgoing link is broken (or r == 0 does not
+// start at offset 0, reported by the caller as source -1).
+LDB_HD bool link_broken(const Pipe& p, uint64_t r) {
+  if (p.start[r] == kNone64 || p.status[r] != kCont) return false;
+  const uint64_t x = p.exitp[r];
+  if (x >= p.len) return false;  // chain ends exactly at the file end (tail terminal)
+  const uint64_t m = x / kW;
+  for (uint64_t k = r + 1; k < m; ++k)
+    if (p.start[k] != kNone64) return true;
+  return p.start[m] != x;
+}
+
+// ---------------------------------------------------------------- CRC helpers (global memory)
+LDB_HD uint32_t g_shift(const Pipe& p, uint32_t reg, uint64_t n) {
+  // n <= kW uses the table; larger n folds whole regions
+  while (n > (uint64_t)kW) { reg = multmodp(p.xw[kW], reg); n -= kW; }
+  return n ? multmodp(p.xw[n], reg) : reg;
+}
+
+// CRC-32 register over image bytes [a, b) from register `reg` (byte at a time; rare paths only).
+LDB_HD uint32_t g_crc_bytes(const Pipe& p, uint32_t reg, uint64_t a, uint64_t b) {
+  const uint32_t* t8 = p.gtab + kT8Off;
+  for (uint64_t i = a; i < b; ++i) reg = crc_byte(t8, reg, p.img[i]);
+  return reg;
+}
+
+// Verify the straddle-out entry of region r (its CRC span crosses into later regions).
+// Returns true when it matches its stored crc.
+LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
+  const uint32_t fl = p.sflag[r];
+  if (fl & kNoCrc) return true;
+  const uint64_t o = p.soff[r];
+  const uint64_t end = p.exitp[r];
+  const uint64_t lo = o + 4;
+  uint32_t reg;
+  uint64_t k;
+  if (fl & kSkip) {
+    // span starts within 3 bytes of (or after) the region end: compute its first piece directly
+    // up to the end of region r+1, then fold the rest.
+    const uint64_t e1 = (r + 2) * (uint64_t)kW;
+    const uint64_t b = end < e1 ? end : e1;
+    reg = g_crc_bytes(p, 0xFFFFFFFFu, lo, b);
+    if (end <= e1) return reg == ~p.scrc[r];
+    k = r + 2;
+  } else {
+    reg = p.rout[r];
+    k = r + 1;
+  }
+  const uint64_t m = end / kW;  // region holding the entry's end (may be == nreg when end == len)
+  for (; k < m; ++k) reg = multmodp(p.xw[kW], reg) ^ p.rpre[k];
+  if (m < p.nreg) {
+    const uint64_t n = end - m * (uint64_t)kW;
+    if (n) reg = multmodp(p.xw[n], reg) ^ p.rpre[m];
+  }
+  return reg == ~p.scrc[r];
+}
+
+LDB_HD uint64_t pack_term(uint64_t pos, int32_t status) {
+  // smallest position wins; status in the low 4 bits (statuses -2..3 -> 0..5)
+  return (pos << 4) | (uint64_t)(status + 2);
+}
+LDB_HD uint64_t term_pos(uint64_t t) { return t >> 4; }
+LDB_HD int32_t term_status(uint64_t t) { return (int32_t)(t & 15) - 2; }
+
+}  // namespace ldb
+
+namespace ldb {
+
+// Repair walk. Wave-uniform control flow: every lane of the one repairing
+// wavefront evaluates the same loads. `rd` reads summaries coherently, `first_term(lo, hi)`
+// returns the first region in (lo, hi] whose (verified) walk stopped with a terminal status
+// or -1, and `run(r, enter)` re-processes region r with its entering position forced and
+// returns its new summary.  Returns the number of regions re-processed.
+template <class Rd, class FirstTerm, class Run>
+LDB_HD uint32_t repair(const Pipe& p, uint32_t nfail, Rd rd, FirstTerm first_term, Run run) {
+  int64_t done = -2;
+  uint32_t repairs = 0;
+  for (;;) {
+    int64_t src = INT64_MAX;
+    for (uint32_t i = 0; i < nfail; ++i) {
+      const int64_t s = p.fail_src[i];
+      if (s > done && s < src) src = s;
+    }
+    if (src == INT64_MAX) break;
+    if (first_term(done, src) >= 0) break;  // a verified region before src already ends the scan
+    uint64_t x = src < 0 ? 0 : rd.exitp((uint64_t)src);
+    int64_t cur = src;
+    bool stop = false;
+    for (;;) {
+      if (x >= p.len) { stop = true; break; }
+      const uint64_t m = x / kW;
+      for (int64_t k = cur + 1; k < (int64_t)m; ++k) {
+        if (rd.start((uint64_t)k) != kNone64) { run((uint64_t)k, kForceNone); ++repairs; }
+      }
+      if (rd.start(m) == x) { done = (int64_t)m - 1; break; }
+      const RegionSum s = run(m, (uint32_t)(x - m * (uint64_t)kW));
+      ++repairs;
+      if (s.status != kCont) { stop = true; break; }
+      cur = (int64_t)m;
+      x = s.exitp;
+    }
+    if (stop) break;
+  }
+  return repairs;
+}
+
+}  // namespace ldb

@@ -1,0 +1,756 @@
+// ldb_scan.hip — gfx950 kernels + C ABI of the LazyDB log-scan engine (liblazydb_gpu.so).
+//
+// Pipeline per file (all on one HIP stream, no host round trip):
+//   k_scan_main  : one wavefront per 5 KiB region, LDS-DMA ring staging, speculative
+//                  decode + CRC-32 per region (region_process, ldb_wave.h)   <- the hot kernel
+//   k_link       : verify region-to-region links of the ReadLogEntry chain
+//   k_repair     : one wavefront re-walks the true chain from each broken link (rare)
+//   k_combine    : CRC-verify entries crossing region boundaries; terminal reduction
+//   k_final      : stop position, status and entry count (index.go:84-95 semantics)
+//   k_compact    : copy the per-region tuples into the caller's dense array
+//   k_serial     : single-lane reference walker (ldb_scan_file_dev_serial, overflow fallback)
+// Reference semantics: logfile/log_file.go:116-145, logfile/log_entry.go:48-121, index.go:55-110.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "ldb_pipeline.h"
+
+using namespace ldb;
+
+#define LDB_HIP(x)                                                 \
+  do {                                                             \
+    hipError_t e_ = (x);                                           \
+    if (e_ != hipSuccess) return LDB_ERR_HIP;                      \
+  } while (0)
+
+namespace {
+
+constexpr int kWPB = 4;     // wavefronts per workgroup in k_scan_main
+constexpr int kNB = 3;      // LDS ring depth per wavefront
+constexpr int kG = kW / 1024 + 1;  // LDS-DMA instructions per region (5 x 1 KiB + the halo)
+
+// ---------------------------------------------------------------- wave policy (SIMT)
+struct GpuWave {
+  int lane;
+  __device__ static void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  template <class F> __device__ void each(F f) { f(lane); sync(); }
+  template <class P> __device__ uint64_t ballot(P p) { return __ballot(p(lane) ? 1 : 0); }
+  template <class P> __device__ int first(P p) {
+    const uint64_t b = __ballot(p(lane) ? 1 : 0);
+    return b ? __builtin_ctzll(b) : -1;
+  }
+  template <class P> __device__ int last(P p) {
+    const uint64_t b = __ballot(p(lane) ? 1 : 0);
+    return b ? 63 - __builtin_clzll(b) : -1;
+  }
+  template <class V> __device__ uint32_t sum(V v) {
+    uint32_t x = v(lane);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+  }
+  template <class V> __device__ void excl_prefix(V v, uint32_t* out) {
+    const uint32_t mine = v(lane);
+    uint32_t x = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    out[lane] = x - mine;
+    sync();
+  }
+  template <class F> __device__ void single(F f) {
+    if (lane == 0) f();
+    sync();
+  }
+};
+
+// LDS image of one wavefront's working state
+struct alignas(16) WaveLds {
+  WaveSh sh;
+  RegionSum rs;
+};
+
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Stage region r ([R0, R0 + kW + kHalo) clipped to len) into a buffer by LDS-DMA: kG wave instructions.
+__device__ __forceinline__ void stage_dma(const uint8_t* img, uint64_t len, uint64_t r, uint32_t buf_lds, int lane) {
+  const uint64_t R0 = r * (uint64_t)kW;
+#pragma unroll
+  for (int k = 0; k < kG - 1; ++k) {
+    const uint64_t off = R0 + (uint64_t)k * 1024 + (uint64_t)lane * 16;
+    // Keep the instruction count wave-uniform for vmcnt accounting: lanes past the end of the
+    // file reload the region's first chunk (harmless bytes that are never used).
+    glds16(img + (off < len ? off : R0), buf_lds + kPre + k * 1024);
+  }
+  // halo: 64 bytes past the region end, lanes 0..3 only (always active -> always issued)
+  if (lane < kHalo / 16) {
+    const uint64_t off = R0 + (uint64_t)(kG - 1) * 1024 + (uint64_t)lane * 16;
+    glds16(img + (off < len ? off : R0), buf_lds + kPre + (kG - 1) * 1024);
+  }
+}
+
+__device__ __forceinline__ void store_tuple(ldb_index_tuple* dst, uint64_t pos, uint32_t k, uint32_t v) {
+  uint4 t;
+  t.x = (uint32_t)pos;
+  t.y = (uint32_t)(pos >> 32);
+  t.z = k;
+  t.w = v;
+  *reinterpret_cast<uint4*>(dst) = t;
+}
+
+__device__ __forceinline__ void write_region(const Pipe& p, uint64_t r, const RegionSum& s) { store_region(p, r, s); }
+
+// ---------------------------------------------------------------- k_scan_main
+__global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* wbase = smem + kTabBytes + wave * (sizeof(WaveLds) + kNB * kBuf);
+  WaveLds* wl = reinterpret_cast<WaveLds*>(wbase);
+  uint8_t* ring = wbase + sizeof(WaveLds);
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)smem + (uint32_t)(ring - smem);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWPB + wave, nw = (uint64_t)gridDim.x * kWPB;
+  const uint64_t count = gw < p.nreg ? (p.nreg - gw + nw - 1) / nw : 0;
+  GpuWave wp{lane};
+  for (int b = 0; b < kNB - 1; ++b)
+    if ((uint64_t)b < count) stage_dma(p.img, p.len, gw + (uint64_t)b * nw, ring_lds + b * kBuf, lane);
+  for (uint64_t i = 0; i < count; ++i) {
+    // prefetch region i+kNB-1 into the slot freed by region i-1, then wait for region i:
+    // at least (issued-after) DMA batches remain in flight, whatever stores were issued between.
+    const uint64_t pf = i + kNB - 1;
+    if (pf < count) {
+      stage_dma(p.img, p.len, gw + pf * nw, ring_lds + (uint32_t)(pf % kNB) * kBuf, lane);
+      wait_vm<(kNB - 1) * kG>();
+    } else if (pf == count && kNB >= 3) {
+      wait_vm<(kNB - 2) * kG>();
+    } else {
+      wait_vm<0>();
+    }
+    GpuWave::sync();
+    const uint64_t r = gw + i * nw;
+    View v;
+    v.buf = ring + (uint32_t)(i % kNB) * kBuf;
+    v.tab = tab;
+    v.R0 = r * (uint64_t)kW;
+    v.rlen = region_len(p, r);
+    v.len = p.len;
+    v.io = p.io;
+    ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
+    region_process(wp, v, wl->sh, kForceSpec, &wl->rs,
+                   [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); });
+    if (lane == 0) write_region(p, r, wl->rs);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    GpuWave::sync();
+  }
+}
+
+// ---------------------------------------------------------------- k_link
+__global__ void k_link(Pipe p) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= p.nreg) return;
+  bool bad = link_broken(p, r);
+  if (bad) {
+    const uint32_t i = atomicAdd(&p.ctr[0], 1u);
+    p.fail_src[i] = (int64_t)r;
+  }
+  if (r == 0 && p.start[0] != 0) {
+    const uint32_t i = atomicAdd(&p.ctr[0], 1u);
+    p.fail_src[i] = -1;
+  }
+}
+
+// ---------------------------------------------------------------- k_repair (one wavefront)
+struct CohRd {
+  const Pipe* p;
+  __device__ uint64_t start(uint64_t r) const {
+    return __hip_atomic_load(&p->start[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ uint64_t exitp(uint64_t r) const {
+    return __hip_atomic_load(&p->exitp[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
+__global__ __launch_bounds__(64) void k_repair(Pipe p) {
+  const uint32_t nfail = p.ctr[0];
+  if (nfail == 0) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
+  WaveLds* wl = reinterpret_cast<WaveLds*>(smem + kTabBytes);
+  uint8_t* buf = smem + kTabBytes + sizeof(WaveLds);
+  __syncthreads();
+  const int lane = threadIdx.x;
+  GpuWave wp{lane};
+  CohRd rd{&p};
+  auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
+    for (int64_t b = lo + 1; b <= hi; b += 64) {
+      const int64_t r = b + lane;
+      bool t = false;
+      if (r >= 0 && r <= hi && (uint64_t)r < p.nreg) {
+        const int32_t st = __hip_atomic_load(&p.status[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = st != kCont && rd.start((uint64_t)r) != kNone64;
+      }
+      const uint64_t m = __ballot(t ? 1 : 0);
+      if (m) return b + __builtin_ctzll(m);
+    }
+    return -1;
+  };
+  auto run = [&](uint64_t r, uint32_t enter) -> RegionSum {
+    const uint64_t R0 = r * (uint64_t)kW;
+    // synchronous staging through registers
+    for (int k = lane; k < (kW + kHalo) / 16; k += 64) {
+      const uint64_t off = R0 + (uint64_t)k * 16;
+      uint4 d = make_uint4(0, 0, 0, 0);
+      if (off < p.len) d = *reinterpret_cast<const uint4*>(p.img + off);
+      *reinterpret_cast<uint4*>(buf + kPre + k * 16) = d;
+    }
+    GpuWave::sync();
+    View v;
+    v.buf = buf;
+    v.tab = tab;
+    v.R0 = R0;
+    v.rlen = region_len(p, r);
+    v.len = p.len;
+    v.io = p.io;
+    ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
+    region_process(wp, v, wl->sh, enter, &wl->rs,
+                   [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); });
+    const RegionSum s = wl->rs;
+    if (lane == 0) {
+      write_region(p, r, s);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    GpuWave::sync();
+    return s;
+  };
+  const uint32_t n = repair(p, nfail, rd, first_term, run);
+  if (lane == 0) p.ctr[2] = n;
+}
+
+// ---------------------------------------------------------------- k_combine
+__global__ __launch_bounds__(256) void k_combine(Pipe p) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint64_t s_sum[256];
+  uint64_t cnt = 0;
+  if (r < p.nreg) {
+    const int32_t st = p.status[r];
+    const uint64_t start = p.start[r];
+    cnt = p.count[r];
+    if (st == kOverflow) {
+      atomicOr(&p.ctr[1], 1u);
+    } else if (start != kNone64) {
+      if (st != kCont) {
+        atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.exitp[r], st));
+      } else {
+        const uint64_t x = p.exitp[r];
+        if (x >= p.len) atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.len, LDB_EOF_WINDOW));
+        if ((p.sflag[r] & kStraddle) && !combine_region(p, r))
+          atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.soff[r], LDB_ERR_CRC));
+      }
+    }
+  }
+  s_sum[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int o = 128; o; o >>= 1) {
+    if (threadIdx.x < o) s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&p.blk[(r / kBlkRegions)], (unsigned long long)s_sum[0]);
+}
+
+// ---------------------------------------------------------------- k_final (1 block)
+// blk_prefix[b] = exclusive prefix of effective counts; blk_prefix[nblk] = regT; result filled.
+__global__ __launch_bounds__(1024) void k_final(Pipe p) {
+  __shared__ uint64_t s_part[1024];
+  __shared__ uint64_t s_regT, s_base;
+  const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
+  const uint64_t T = p.tpos[0];
+  uint64_t tp = term_pos(T);
+  int32_t ts = term_status(T);
+  if (T == ~0ull) { tp = p.len; ts = LDB_ERR_MALFORMED; }  // unreachable: the chain always stops
+  const uint64_t regT = tp / kW;
+  if (threadIdx.x == 0) {
+    s_regT = regT;
+    uint64_t acc = 0;
+    for (uint64_t b = 0; b < nblk; ++b) {
+      p.blk_prefix[b] = acc;
+      if ((b + 1) * kBlkRegions <= regT) acc += p.blk[b];
+    }
+    s_base = acc;  // sum of all blocks fully before regT's block
+  }
+  __syncthreads();
+  // partial sum inside regT's block (regions before regT) + regT's effective count
+  const uint64_t b0 = (regT / kBlkRegions) * kBlkRegions;
+  uint64_t part = 0;
+  for (uint64_t r = b0 + threadIdx.x; r < regT && r < p.nreg; r += blockDim.x) part += p.count[r];
+  s_part[threadIdx.x] = part;
+  __syncthreads();
+  for (int o = 512; o; o >>= 1) {
+    if (threadIdx.x < o) s_part[threadIdx.x] += s_part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    uint64_t eff = 0;
+    if (regT < p.nreg) {
+      eff = p.count[regT];
+      // the terminal is this region's straddle-out entry failing its CRC
+      if (p.status[regT] == kCont && (p.sflag[regT] & kStraddle) && p.soff[regT] == tp && eff > 0) eff -= 1;
+    }
+    const uint64_t n = s_base + s_part[0] + eff;
+    ldb_scan_result res;
+    res.status = ts;
+    res.fid = p.fid;
+    res.n_entries = n;
+    res.end_off = tp;
+    res.n_repairs = p.ctr[2];
+    res.n_regions = (uint32_t)p.nreg;
+    if (n > p.cap) res.status = LDB_ERR_CAPACITY;
+    if (p.ctr[1]) res.status = kOverflow;  // k_serial redoes the scan
+    *p.result = res;
+    p.blk_prefix[nblk] = regT;
+  }
+}
+
+// ---------------------------------------------------------------- k_compact
+// One workgroup per 1024-region block; each wavefront copies whole regions.
+__device__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out) {
+  struct G {
+    const uint8_t* q;
+    __device__ uint32_t operator()(int i) const { return q[i]; }
+  };
+  Header h;
+  decode_header(G{p.img + off}, &h);
+  ldb_entry e;
+  e.offset = off;
+  e.expired_at = h.expired_at;
+  e.tx_id = h.tx_id;
+  e.crc = h.crc;
+  e.k_size = h.k_size;
+  e.v_size = h.v_size;
+  e.tx_stat = (uint16_t)h.tx_stat;
+  e.stat = (uint8_t)h.stat;
+  e.hdr_size = (uint8_t)h.size;
+  e.enc_hdr_size = (uint8_t)h.enc_size;
+  e.pad_[0] = e.pad_[1] = e.pad_[2] = 0;
+  e.fid = p.fid;
+  *out = e;
+}
+
+__global__ __launch_bounds__(1024) void k_compact(Pipe p) {
+  __shared__ uint32_t s_cnt[kBlkRegions];
+  __shared__ uint64_t s_off[kBlkRegions];
+  const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
+  const uint64_t regT = p.blk_prefix[nblk];
+  const uint64_t b = blockIdx.x;
+  const uint64_t r0 = b * kBlkRegions;
+  if (r0 > regT || p.ctr[1]) return;
+  const uint64_t r = r0 + threadIdx.x;
+  uint32_t c = 0;
+  if (r < p.nreg && r <= regT) {
+    c = p.count[r];
+    if (r == regT && p.status[r] == kCont && (p.sflag[r] & kStraddle) && p.soff[r] == term_pos(p.tpos[0]) && c > 0)
+      c -= 1;
+  }
+  s_cnt[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t acc = p.blk_prefix[b];
+    for (int i = 0; i < kBlkRegions; ++i) { s_off[i] = acc; acc += s_cnt[i]; }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = wave; i < kBlkRegions; i += 16) {
+    const uint32_t n = s_cnt[i];
+    const uint64_t base = s_off[i];
+    const ldb_index_tuple* src = p.scratch + (r0 + i) * (uint64_t)kRegionCap;
+    for (uint32_t j = lane; j < n; j += 64) {
+      const uint64_t dst = base + j;
+      if (dst >= p.cap) break;
+      const ldb_index_tuple t = src[j];
+      if (p.kind == LDB_TUPLE_ENTRY) {
+        decode_entry_global(p, t.pos & 0xFFFFFFFFFFull, reinterpret_cast<ldb_entry*>(p.out) + dst);
+      } else {
+        reinterpret_cast<ldb_index_tuple*>(p.out)[dst] = t;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- k_serial
+// One lane walks the chain exactly like index.go:84-95 (global memory, byte-wise CRC).
+__global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
+  if (threadIdx.x != 0) return;
+  if (only_on_overflow && !p.ctr[1]) return;
+  const uint32_t* t8 = p.gtab + kT8Off;
+  struct G {
+    const uint8_t* q;
+    __device__ uint32_t operator()(int i) const { return q[i]; }
+  };
+  uint64_t off = 0, n = 0;
+  int st;
+  for (;;) {
+    EntryInfo e;
+    if (read_eof(p.len, p.io, (int64_t)off, kMaxHeader)) {
+      e.status = LDB_EOF_WINDOW;
+    } else {
+      e = classify_entry(G{p.img + off}, p.len, p.io, off);
+    }
+    if (e.status != kCont) { st = e.status; break; }
+    uint32_t crc = 0;
+    if (e.h.size > 4) crc = ~g_crc_bytes(p, 0xFFFFFFFFu, off + 4, off + e.size);
+    if (crc != e.h.crc) { st = LDB_ERR_CRC; break; }
+    if (n < p.cap) {
+      if (p.kind == LDB_TUPLE_ENTRY) {
+        decode_entry_global(p, off, reinterpret_cast<ldb_entry*>(p.out) + n);
+      } else {
+        ldb_index_tuple t;
+        t.pos = pack_pos(off, e.h);
+        t.k_size = e.h.k_size;
+        t.v_size = e.h.v_size;
+        reinterpret_cast<ldb_index_tuple*>(p.out)[n] = t;
+      }
+    }
+    ++n;
+    off += e.size;
+  }
+  ldb_scan_result res;
+  res.status = n > p.cap ? LDB_ERR_CAPACITY : st;
+  res.fid = p.fid;
+  res.n_entries = n;
+  res.end_off = off;
+  res.n_repairs = 0;
+  res.n_regions = (uint32_t)p.nreg;
+  *p.result = res;
+}
+
+size_t main_lds_bytes() { return kTabBytes + kWPB * (sizeof(WaveLds) + kNB * kBuf); }
+size_t repair_lds_bytes() { return kTabBytes + sizeof(WaveLds) + kBuf; }
+
+}  // namespace
+
+// ==================================================================== host runtime
+struct ldb_ctx {
+  int device = 0;
+  int n_cu = 256;
+  uint32_t* d_tab = nullptr;   // kTabWords
+  uint32_t* d_xw = nullptr;    // kW + 1
+  uint8_t* ws = nullptr;       // workspace
+  uint64_t ws_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  bool timing = false;
+  double t_main = 0, t_total = 0;
+  uint64_t t_n = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+};
+
+namespace {
+
+struct WsLayout {
+  uint64_t nreg, nblk;
+  uint64_t o_start, o_exitp, o_soff, o_status, o_count, o_rpre, o_rout, o_scrc, o_sflag, o_scratch, o_fail, o_ctr,
+      o_tpos, o_blk, o_blkp, total;
+};
+
+WsLayout layout(uint64_t len) {
+  WsLayout L;
+  L.nreg = (len + kW - 1) / kW;
+  if (L.nreg == 0) L.nreg = 1;
+  L.nblk = (L.nreg + kBlkRegions - 1) / kBlkRegions;
+  uint64_t o = 0;
+  auto take = [&](uint64_t bytes) {
+    const uint64_t at = o;
+    o += (bytes + 255) & ~255ull;
+    return at;
+  };
+  // control words first (one memset covers ctr, tpos, blk)
+  L.o_ctr = take(16);
+  L.o_tpos = take(16);
+  L.o_blk = take(8 * L.nblk);
+  L.o_blkp = take(8 * (L.nblk + 1));
+  L.o_start = take(8 * L.nreg);
+  L.o_exitp = take(8 * L.nreg);
+  L.o_soff = take(8 * L.nreg);
+  L.o_status = take(4 * L.nreg);
+  L.o_count = take(4 * L.nreg);
+  L.o_rpre = take(4 * L.nreg);
+  L.o_rout = take(4 * L.nreg);
+  L.o_scrc = take(4 * L.nreg);
+  L.o_sflag = take(4 * L.nreg);
+  L.o_fail = take(8 * (L.nreg + 1));
+  L.o_scratch = take(sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg);
+  L.total = o;
+  return L;
+}
+
+int ensure_ws(ldb_ctx* c, uint64_t bytes) {
+  if (c->ws_bytes >= bytes) return LDB_OK;
+  if (c->ws) (void)hipFree(c->ws);
+  c->ws = nullptr;
+  c->ws_bytes = 0;
+  if (hipMalloc(&c->ws, bytes) != hipSuccess) return LDB_ERR_NOMEM;
+  c->ws_bytes = bytes;
+  return LDB_OK;
+}
+
+Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, uint32_t fid, int io, int kind,
+               void* out, uint64_t cap, ldb_scan_result* res) {
+  Pipe p;
+  uint8_t* w = c->ws;
+  p.img = img;
+  p.len = len;
+  p.io = io;
+  p.fid = fid;
+  p.nreg = L.nreg;
+  p.gtab = c->d_tab;
+  p.xw = c->d_xw;
+  p.start = reinterpret_cast<uint64_t*>(w + L.o_start);
+  p.exitp = reinterpret_cast<uint64_t*>(w + L.o_exitp);
+  p.soff = reinterpret_cast<uint64_t*>(w + L.o_soff);
+  p.status = reinterpret_cast<int32_t*>(w + L.o_status);
+  p.count = reinterpret_cast<uint32_t*>(w + L.o_count);
+  p.rpre = reinterpret_cast<uint32_t*>(w + L.o_rpre);
+  p.rout = reinterpret_cast<uint32_t*>(w + L.o_rout);
+  p.scrc = reinterpret_cast<uint32_t*>(w + L.o_scrc);
+  p.sflag = reinterpret_cast<uint32_t*>(w + L.o_sflag);
+  p.scratch = reinterpret_cast<ldb_index_tuple*>(w + L.o_scratch);
+  p.fail_src = reinterpret_cast<int64_t*>(w + L.o_fail);
+  p.ctr = reinterpret_cast<uint32_t*>(w + L.o_ctr);
+  p.tpos = reinterpret_cast<uint64_t*>(w + L.o_tpos);
+  p.blk = reinterpret_cast<uint64_t*>(w + L.o_blk);
+  p.blk_prefix = reinterpret_cast<uint64_t*>(w + L.o_blkp);
+  p.out = out;
+  p.cap = cap;
+  p.kind = kind;
+  p.result = res;
+  return p;
+}
+
+int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, int io, int kind, void* d_out,
+                 uint64_t cap, ldb_scan_result* d_res, hipStream_t s, bool serial) {
+  if (!c || !d_res || (io != LDB_IO_FILEIO && io != LDB_IO_MMAP) ||
+      (kind != LDB_TUPLE_INDEX && kind != LDB_TUPLE_ENTRY) || (cap && !d_out))
+    return LDB_ERR_ARG;
+  if (len && !d_img) return LDB_ERR_ARG;
+  if (((uintptr_t)d_img & 15) != 0) return LDB_ERR_ARG;
+  if (len >= (1ull << 40)) return LDB_ERR_ARG;  // tuple offsets are 40-bit
+  const WsLayout L = layout(len);
+  int rc = ensure_ws(c, L.total);
+  if (rc != LDB_OK) return rc;
+  const Pipe p = make_pipe(c, L, d_img, len, fid, io, kind, d_out, cap, d_res);
+  // control words: ctr = 0, tpos = ~0, blk = 0
+  LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 16, s));
+  LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
+  LDB_HIP(hipMemsetAsync(c->ws + L.o_blk, 0, 8 * L.nblk, s));
+  if (serial || len < (uint64_t)kMaxHeader) {
+    hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 0);
+    return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+  }
+  const bool tm = c->timing;
+  if (tm) LDB_HIP(hipEventRecord(c->ev0, s));
+  const int grid = (int)std::min<uint64_t>((L.nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * 2);
+  hipLaunchKernelGGL(k_scan_main, dim3(grid), dim3(64 * kWPB), main_lds_bytes(), s, p);
+  if (tm) LDB_HIP(hipEventRecord(c->ev1, s));
+  const int g256 = (int)((L.nreg + 255) / 256);
+  hipLaunchKernelGGL(k_link, dim3(g256), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_repair, dim3(1), dim3(64), repair_lds_bytes(), s, p);
+  hipLaunchKernelGGL(k_combine, dim3(g256), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_final, dim3(1), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_compact, dim3((unsigned)L.nblk), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 1);
+  if (tm) {
+    LDB_HIP(hipEventRecord(c->ev2, s));
+    // accumulate when the events complete (synchronously here: timing mode is for benchmarks)
+    LDB_HIP(hipEventSynchronize(c->ev2));
+    float a = 0, b = 0;
+    LDB_HIP(hipEventElapsedTime(&a, c->ev0, c->ev1));
+    LDB_HIP(hipEventElapsedTime(&b, c->ev0, c->ev2));
+    c->t_main += a;
+    c->t_total += b;
+    c->t_n += 1;
+  }
+  return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ldb_abi_version(void) { return LDB_ABI_VERSION; }
+
+const char* ldb_status_str(int s) {
+  switch (s) {
+    case LDB_OK: return "ok";
+    case LDB_EOF_WINDOW: return "eof (header window)";
+    case LDB_EOF_SENTINEL: return "end of log entries (zero header)";
+    case LDB_EOF_KV: return "eof (key/value)";
+    case LDB_ERR_CRC: return "invalid crc";
+    case LDB_ERR_MALFORMED: return "malformed entry header";
+    case LDB_ERR_CAPACITY: return "output capacity exceeded";
+    case LDB_ERR_ARG: return "invalid argument";
+    case LDB_ERR_HIP: return "hip runtime error";
+    case LDB_ERR_NOMEM: return "out of device memory";
+    default: return "unknown status";
+  }
+}
+
+uint64_t ldb_workspace_bytes(uint64_t len) { return layout(len).total; }
+
+int ldb_ctx_create(int device, ldb_ctx** out) {
+  if (!out) return LDB_ERR_ARG;
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return LDB_ERR_HIP;
+  ldb_ctx* c = new (std::nothrow) ldb_ctx();
+  if (!c) return LDB_ERR_NOMEM;
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+  std::vector<uint32_t> tab(kTabWords), xw(kW + 1);
+  build_tables(tab.data());
+  for (int n = 0; n <= kW; ++n) xw[n] = x8n_modp((uint64_t)n);
+  if (hipMalloc(&c->d_tab, tab.size() * 4) != hipSuccess || hipMalloc(&c->d_xw, xw.size() * 4) != hipSuccess) {
+    ldb_ctx_destroy(c);
+    return LDB_ERR_NOMEM;
+  }
+  if (hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_xw, xw.data(), xw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    ldb_ctx_destroy(c);
+    return LDB_ERR_HIP;
+  }
+  if (hipFuncSetAttribute((const void*)k_scan_main, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)main_lds_bytes()) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_repair, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)repair_lds_bytes()) != hipSuccess) {
+    ldb_ctx_destroy(c);
+    return LDB_ERR_HIP;
+  }
+  (void)hipEventCreate(&c->ev0);
+  (void)hipEventCreate(&c->ev1);
+  (void)hipEventCreate(&c->ev2);
+  *out = c;
+  return LDB_OK;
+}
+
+int ldb_ctx_destroy(ldb_ctx* c) {
+  if (!c) return LDB_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  if (c->d_tab) (void)hipFree(c->d_tab);
+  if (c->d_xw) (void)hipFree(c->d_xw);
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  delete c;
+  return LDB_OK;
+}
+
+int ldb_ctx_reserve(ldb_ctx* c, uint64_t max_len) {
+  if (!c) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  return ensure_ws(c, layout(max_len).total);
+}
+
+int ldb_scan_file_dev(ldb_ctx* c, const uint8_t* d_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
+                      void* d_out, uint64_t cap, ldb_scan_result* d_result, void* stream) {
+  if (!c) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  return enqueue_scan(c, d_image, len, fid, io_type, tuple_kind, d_out, cap, d_result, (hipStream_t)stream, false);
+}
+
+int ldb_scan_file_dev_serial(ldb_ctx* c, const uint8_t* d_image, uint64_t len, uint32_t fid, int io_type,
+                             int tuple_kind, void* d_out, uint64_t cap, ldb_scan_result* d_result, void* stream) {
+  if (!c) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  return enqueue_scan(c, d_image, len, fid, io_type, tuple_kind, d_out, cap, d_result, (hipStream_t)stream, true);
+}
+
+int ldb_scan_files_dev(ldb_ctx* c, int n_files, const uint8_t* const* d_images, const uint64_t* lens,
+                       const uint32_t* fids, int io_type, int tuple_kind, void* const* d_outs, const uint64_t* caps,
+                       ldb_scan_result* d_results, void* stream) {
+  if (!c || n_files < 0 || (n_files && (!d_images || !lens || !fids || !d_outs || !caps || !d_results)))
+    return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  uint64_t mx = 0;
+  for (int i = 0; i < n_files; ++i) mx = std::max(mx, lens[i]);
+  int rc = ensure_ws(c, layout(mx).total);
+  if (rc != LDB_OK) return rc;
+  for (int i = 0; i < n_files; ++i) {
+    rc = enqueue_scan(c, d_images[i], lens[i], fids[i], io_type, tuple_kind, d_outs[i], caps[i], d_results + i,
+                      (hipStream_t)stream, false);
+    if (rc != LDB_OK) return rc;
+  }
+  return LDB_OK;
+}
+
+int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
+                  void* h_out, uint64_t cap, ldb_scan_result* h_result) {
+  if (!c || !h_result || (len && !h_image) || (cap && !h_out)) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  const size_t tsz = tuple_kind == LDB_TUPLE_ENTRY ? sizeof(ldb_entry) : sizeof(ldb_index_tuple);
+  uint8_t* d_img = nullptr;
+  void* d_out = nullptr;
+  ldb_scan_result* d_res = nullptr;
+  int rc = LDB_OK;
+  hipStream_t s = nullptr;
+  if (hipStreamCreate(&s) != hipSuccess) return LDB_ERR_HIP;
+  if (hipMalloc(&d_img, len ? len : 16) != hipSuccess || hipMalloc(&d_res, sizeof(ldb_scan_result)) != hipSuccess ||
+      (cap && hipMalloc(&d_out, cap * tsz) != hipSuccess)) {
+    rc = LDB_ERR_NOMEM;
+  }
+  if (rc == LDB_OK && len && hipMemcpyAsync(d_img, h_image, len, hipMemcpyHostToDevice, s) != hipSuccess) rc = LDB_ERR_HIP;
+  if (rc == LDB_OK) rc = enqueue_scan(c, d_img, len, fid, io_type, tuple_kind, d_out, cap, d_res, s, false);
+  ldb_scan_result res;
+  if (rc == LDB_OK && hipMemcpyAsync(&res, d_res, sizeof(res), hipMemcpyDeviceToHost, s) != hipSuccess) rc = LDB_ERR_HIP;
+  if (rc == LDB_OK && hipStreamSynchronize(s) != hipSuccess) rc = LDB_ERR_HIP;
+  if (rc == LDB_OK) {
+    const uint64_t n = std::min<uint64_t>(res.n_entries, cap);
+    if (n && hipMemcpy(h_out, d_out, n * tsz, hipMemcpyDeviceToHost) != hipSuccess) rc = LDB_ERR_HIP;
+    *h_result = res;
+  }
+  if (d_img) (void)hipFree(d_img);
+  if (d_out) (void)hipFree(d_out);
+  if (d_res) (void)hipFree(d_res);
+  (void)hipStreamDestroy(s);
+  return rc;
+}
+
+int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n) {
+  if (!c) return LDB_ERR_ARG;
+  if (avg_main_ms) *avg_main_ms = c->t_n ? c->t_main / c->t_n : 0.0;
+  if (avg_total_ms) *avg_total_ms = c->t_n ? c->t_total / c->t_n : 0.0;
+  if (n) *n = c->t_n;
+  if (enable >= 0) {
+    c->timing = enable != 0;
+    c->t_main = c->t_total = 0;
+    c->t_n = 0;
+  }
+  return LDB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,171 @@
+// ldb_emu.cpp — CPU emulation of the gfx950 scan pipeline (TEST HARNESS ONLY).
+//
+// Runs the engine's own phase functions (lazydb_amd/csrc/ldb_engine.h, ldb_wave.h,
+// ldb_pipeline.h) with a sequential 64-lane "wave policy", region after region, then the
+// link / repair / combine / final / compact stages exactly as the kernels in ldb_scan.hip
+// order them. It exists so the algorithm can be checked against the oracle in this
+// GPU-less container; it is not linked into liblazydb_gpu.so and is not a fallback.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../lazydb_amd/csrc/ldb_pipeline.h"
+
+using namespace ldb;
+
+namespace {
+
+struct CpuWave {
+  template <class F> void each(F f) { for (int l = 0; l < kLanes; ++l) f(l); }
+  template <class P> uint64_t ballot(P p) {
+    uint64_t b = 0;
+    for (int l = 0; l < kLanes; ++l)
+      if (p(l)) b |= 1ull << l;
+    return b;
+  }
+  template <class P> int first(P p) {
+    for (int l = 0; l < kLanes; ++l)
+      if (p(l)) return l;
+    return -1;
+  }
+  template <class P> int last(P p) {
+    for (int l = kLanes - 1; l >= 0; --l)
+      if (p(l)) return l;
+    return -1;
+  }
+  template <class V> uint32_t sum(V v) {
+    uint32_t s = 0;
+    for (int l = 0; l < kLanes; ++l) s += v(l);
+    return s;
+  }
+  template <class V> void excl_prefix(V v, uint32_t* out) {
+    uint32_t s = 0;
+    for (int l = 0; l < kLanes; ++l) { out[l] = s; s += v(l); }
+  }
+  template <class F> void single(F f) { f(); }
+};
+
+struct Emu {
+  std::vector<uint32_t> tab, xw;
+  std::vector<uint8_t> buf;
+  WaveSh sh;
+  uint64_t garbage = 0x1234567;
+  Emu() : tab(kTabWords), xw(kW + 1), buf(kBuf) {
+    build_tables(tab.data());
+    for (int n = 0; n <= kW; ++n) xw[n] = x8n_modp((uint64_t)n);
+  }
+  void stage(const Pipe& p, uint64_t r) {
+    const uint64_t R0 = r * (uint64_t)kW;
+    for (int i = 0; i < kBuf; ++i) {
+      const int64_t a = (int64_t)R0 + i - kPre;
+      garbage = garbage * 6364136223846793005ull + 1442695040888963407ull;
+      buf[i] = (a >= 0 && (uint64_t)a < p.len) ? p.img[a] : (uint8_t)(garbage >> 56);
+    }
+  }
+  RegionSum run(const Pipe& p, uint64_t r, uint32_t enter) {
+    stage(p, r);
+    View v;
+    v.buf = buf.data();
+    v.tab = tab.data();
+    v.R0 = r * (uint64_t)kW;
+    v.rlen = region_len(p, r);
+    v.len = p.len;
+    v.io = p.io;
+    RegionSum s;
+    CpuWave wp;
+    ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
+    region_process(wp, v, sh, enter, &s, [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
+      sc[slot].pos = pos;
+      sc[slot].k_size = k;
+      sc[slot].v_size = vv;
+    });
+    store_region(p, r, s);
+    return s;
+  }
+};
+
+struct Rd {
+  const Pipe* p;
+  uint64_t start(uint64_t r) const { return p->start[r]; }
+  uint64_t exitp(uint64_t r) const { return p->exitp[r]; }
+};
+
+}  // namespace
+
+extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                        ldb_scan_result* res, uint32_t* stats) {
+  Emu emu;
+  const uint64_t nreg = std::max<uint64_t>(1, (len + kW - 1) / kW);
+  const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
+  std::vector<uint64_t> start(nreg), exitp(nreg), soff(nreg), blk(nblk, 0), blkp(nblk + 1, 0), tpos(2, ~0ull);
+  std::vector<int32_t> status(nreg);
+  std::vector<uint32_t> count(nreg), rpre(nreg), rout(nreg), scrc(nreg), sflag(nreg), ctr(4, 0);
+  std::vector<ldb_index_tuple> scratch(nreg * (uint64_t)kRegionCap);
+  std::vector<int64_t> fail(nreg + 1);
+  Pipe p;
+  p.img = img; p.len = len; p.io = io; p.fid = fid; p.nreg = nreg;
+  p.gtab = emu.tab.data(); p.xw = emu.xw.data();
+  p.start = start.data(); p.exitp = exitp.data(); p.soff = soff.data(); p.status = status.data();
+  p.count = count.data(); p.rpre = rpre.data(); p.rout = rout.data(); p.scrc = scrc.data(); p.sflag = sflag.data();
+  p.scratch = scratch.data(); p.fail_src = fail.data(); p.ctr = ctr.data(); p.tpos = tpos.data();
+  p.blk = blk.data(); p.blk_prefix = blkp.data(); p.out = out; p.cap = cap; p.kind = LDB_TUPLE_INDEX; p.result = res;
+  if (len < (uint64_t)kMaxHeader) {
+    // the kernels route tiny images to k_serial; mirror it
+    res->status = LDB_EOF_WINDOW; res->fid = fid; res->n_entries = 0; res->end_off = 0; res->n_repairs = 0;
+    res->n_regions = (uint32_t)nreg;
+    return 0;
+  }
+  // k_scan_main
+  for (uint64_t r = 0; r < nreg; ++r) emu.run(p, r, kForceSpec);
+  // k_link
+  for (uint64_t r = 0; r < nreg; ++r) {
+    if (link_broken(p, r)) fail[ctr[0]++] = (int64_t)r;
+    if (r == 0 && start[0] != 0) fail[ctr[0]++] = -1;
+  }
+  const uint32_t nfail = ctr[0];
+  // k_repair
+  if (nfail) {
+    auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
+      for (int64_t r = std::max<int64_t>(lo + 1, 0); r <= hi && (uint64_t)r < nreg; ++r)
+        if (status[r] != kCont && start[r] != kNone64) return r;
+      return -1;
+    };
+    ctr[2] = repair(p, nfail, Rd{&p}, first_term, [&](uint64_t r, uint32_t enter) { return emu.run(p, r, enter); });
+  }
+  // k_combine
+  for (uint64_t r = 0; r < nreg; ++r) {
+    const int32_t st = status[r];
+    if (st == kOverflow) { ctr[1] = 1; continue; }
+    blk[r / kBlkRegions] += count[r];
+    if (start[r] == kNone64) continue;
+    if (st != kCont) {
+      tpos[0] = std::min(tpos[0], pack_term(exitp[r], st));
+    } else {
+      if (exitp[r] >= len) tpos[0] = std::min(tpos[0], pack_term(len, LDB_EOF_WINDOW));
+      if ((sflag[r] & kStraddle) && !combine_region(p, r)) tpos[0] = std::min(tpos[0], pack_term(soff[r], LDB_ERR_CRC));
+    }
+  }
+  if (ctr[1]) return -100;  // overflow: the GPU pipeline re-runs k_serial
+  // k_final + k_compact
+  const uint64_t T = tpos[0];
+  if (T == ~0ull) return -101;
+  const uint64_t tp = term_pos(T);
+  const uint64_t regT = tp / kW;
+  uint64_t n = 0;
+  for (uint64_t r = 0; r < nreg && r <= regT; ++r) {
+    uint64_t c = count[r];
+    if (r == regT && status[r] == kCont && (sflag[r] & kStraddle) && soff[r] == tp && c > 0) c -= 1;
+    for (uint64_t j = 0; j < c; ++j)
+      if (n + j < cap) out[n + j] = scratch[r * (uint64_t)kRegionCap + j];
+    n += c;
+  }
+  res->status = n > cap ? LDB_ERR_CAPACITY : term_status(T);
+  res->fid = fid;
+  res->n_entries = n;
+  res->end_off = tp;
+  res->n_repairs = ctr[2];
+  res->n_regions = (uint32_t)nreg;
+  if (stats) { stats[0] = nfail; stats[1] = ctr[2]; }
+  return 0;
+}

@@ -1,0 +1,111 @@
+"""GPU parity: liblazydb_gpu.so (called through its C ABI) vs the CPU oracle.
+
+Bit-exact: status, end offset, entry count and every tuple field (offsets, header
+sizes, EncodeEntry sizes, stat, key/value sizes; ENTRY kind adds crc, expiredAt,
+txid, txstat, fid).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from lazydb_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def to_dev(img):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(img, dtype=np.uint8)).to("cuda:0")
+
+
+def assert_same(res, tup, ref, rt, kind=0):
+    assert (res.status, res.end_off, res.n_entries) == (ref.status, ref.end_off, ref.n_entries), \
+        (res.as_dict(), (ref.status, ref.end_off, ref.n_entries))
+    if kind == 0:
+        assert np.array_equal(tup["pos"], rt["pos"])
+        assert np.array_equal(tup["k_size"], rt["k_size"]) and np.array_equal(tup["v_size"], rt["v_size"])
+    else:
+        assert tup.tobytes() == rt.tobytes()
+
+
+def test_golden_fixtures_device_api(eng, golden):
+    meta, imgs = golden
+    for m in meta:
+        img = np.frombuffer(imgs[m["name"]], np.uint8)
+        res, tup = eng.scan_dev(to_dev(img) if img.size else to_dev(np.zeros(0, np.uint8)), io_type=m["io_type"])
+        assert (res.status, res.end_off, res.n_entries) == (m["status"], m["end_off"], len(m["tuples"])), m["name"]
+        want = [t[0] | (t[1] << 40) | (t[2] << 46) | (t[3] << 52) for t in m["tuples"]]
+        assert list(tup["pos"]) == want, m["name"]
+        assert list(tup["k_size"]) == [t[4] for t in m["tuples"]], m["name"]
+
+
+def test_golden_fixtures_host_api_and_entry_kind(eng, golden):
+    meta, imgs = golden
+    for m in meta:
+        img = np.frombuffer(imgs[m["name"]], np.uint8)
+        res, tup = eng.scan_host(img, fid=3, io_type=m["io_type"], kind=1)
+        ref, rt = coracle.scan(img, m["io_type"], fid=3, tuple_kind=1)
+        assert_same(res, tup, ref, rt, kind=1)
+
+
+def test_serial_walker_matches(eng, golden):
+    meta, imgs = golden
+    for m in meta[:20]:
+        img = np.frombuffer(imgs[m["name"]], np.uint8)
+        if img.size == 0:
+            continue
+        res, tup = eng.scan_dev(to_dev(img), io_type=m["io_type"], serial=True)
+        assert (res.status, res.end_off, res.n_entries) == (m["status"], m["end_off"], len(m["tuples"])), m["name"]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_mutated_logs(eng, seed):
+    from tests.golden import make_golden as G
+    rng = random.Random(seed)
+    cases = [
+        coracle.gen_log(rng.randrange(100000, 3 << 20), seed, ksize=rng.choice([5, 16, 64]),
+                        vsize=rng.choice([0, 3, 100, 256, 4000]))[0],
+        coracle.gen_log(4 << 20, seed + 100, ksize=64, value_mode=1, zipf_max=4096)[0],
+        np.frombuffer(G.embedded(seed, 200000), np.uint8).copy(),
+        np.frombuffer(G.binary_values(seed, 200000), np.uint8).copy(),
+        np.frombuffer(G.mixed(seed, 300000), np.uint8).copy(),
+    ]
+    for img in cases:
+        m = rng.random()
+        if m < 0.4:
+            for _ in range(rng.randrange(1, 4)):
+                img[rng.randrange(img.size)] ^= rng.randrange(1, 256)
+        elif m < 0.6:
+            img = img[: rng.randrange(img.size)].copy()
+        for io in (0, 1):
+            res, tup = eng.scan_dev(to_dev(img), io_type=io)
+            ref, rt = coracle.scan(img, io)
+            assert_same(res, tup, ref, rt)
+
+
+def test_capacity_reporting(eng):
+    img, n, end = coracle.gen_log(1 << 20, 7, ksize=16, vsize=50)
+    res, tup = eng.scan_dev(to_dev(img), cap=100)
+    assert res.status == -3 and res.n_entries == n and len(tup) == 100
+    ref, rt = coracle.scan(img)
+    assert np.array_equal(tup["pos"], rt["pos"][:100])
+
+
+def test_config2_1gib_full_parity(eng):
+    """BASELINE config 2: one 1 GiB file of 64-B key / 256-B value entries (FileIO bound)."""
+    img, n, end = coracle.gen_log(1 << 30, 1, ksize=64, vsize=256)
+    assert n == 3234162 and end == 1073741784
+    d = to_dev(img)
+    res, tup = eng.scan_dev(d, cap=n + 16)
+    ref, rt = coracle.scan(img)
+    assert_same(res, tup, ref, rt)
+    assert res.status == 2 and res.n_repairs == 0
