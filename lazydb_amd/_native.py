@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "liblazydb_gpu.so")
+LIB_PATH = os.environ.get("LAZYDB_GPU_LIB") or os.path.join(HERE, "_lib", "liblazydb_gpu.so")
 
 LDB_OK = 0
 EOF_WINDOW, EOF_SENTINEL, EOF_KV = 1, 2, 3

@@ -32,13 +32,30 @@ using namespace ldb;
 
 namespace {
 
-constexpr int kWPB = 4;     // wavefronts per workgroup in k_scan_main
-constexpr int kNB = 3;      // LDS ring depth per wavefront
+#ifndef LDB_WPB
+#define LDB_WPB 8
+#endif
+#ifndef LDB_NB
+#define LDB_NB 2
+#endif
+constexpr int kWPB = LDB_WPB;  // wavefronts per workgroup in k_scan_main
+constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
 constexpr int kG = kW / 1024 + 1;  // LDS-DMA instructions per region (5 x 1 KiB + the halo)
 
 // ---------------------------------------------------------------- wave policy (SIMT)
 struct GpuWave {
   int lane;
+#ifdef LDB_STAMPS
+  uint64_t t_last = 0;
+  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ void stamp(int id) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if (t_last) acc[id] += t - t_last;
+    t_last = t;
+  }
+#else
+  __device__ void stamp(int) {}
+#endif
   __device__ static void sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -73,6 +90,12 @@ struct GpuWave {
   template <class F> __device__ void single(F f) {
     if (lane == 0) f();
     sync();
+  }
+  __device__ uint32_t bcast_or(uint32_t x) {
+    uint32_t y = x;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) y |= __shfl_xor(y, o);
+    return y;
   }
 };
 
@@ -122,6 +145,9 @@ __device__ __forceinline__ void store_tuple(ldb_index_tuple* dst, uint64_t pos, 
 
 __device__ __forceinline__ void write_region(const Pipe& p, uint64_t r, const RegionSum& s) { store_region(p, r, s); }
 
+#ifdef LDB_STAMPS
+__device__ uint64_t g_stamps[8];
+#endif
 // ---------------------------------------------------------------- k_scan_main
 __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -152,21 +178,29 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
       wait_vm<0>();
     }
     GpuWave::sync();
+    wp.stamp(6);
     const uint64_t r = gw + i * nw;
     View v;
     v.buf = ring + (uint32_t)(i % kNB) * kBuf;
     v.tab = tab;
+    v.xw = p.xw;
     v.R0 = r * (uint64_t)kW;
     v.rlen = region_len(p, r);
     v.len = p.len;
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    region_process(wp, v, wl->sh, kForceSpec, &wl->rs,
+    LaneKeep kp;
+    region_process(wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LaneKeep& { return kp; },
                    [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); });
     if (lane == 0) write_region(p, r, wl->rs);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
+    wp.stamp(7);
   }
+#ifdef LDB_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&g_stamps[k], (unsigned long long)wp.acc[k]);
+#endif
 }
 
 // ---------------------------------------------------------------- k_link
@@ -233,12 +267,14 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
     View v;
     v.buf = buf;
     v.tab = tab;
+    v.xw = p.xw;
     v.R0 = R0;
     v.rlen = region_len(p, r);
     v.len = p.len;
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    region_process(wp, v, wl->sh, enter, &wl->rs,
+    LaneKeep kp;
+    region_process(wp, v, wl->sh, enter, &wl->rs, [&](int) -> LaneKeep& { return kp; },
                    [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); });
     const RegionSum s = wl->rs;
     if (lane == 0) {
@@ -289,7 +325,7 @@ __global__ __launch_bounds__(256) void k_combine(Pipe p) {
 // blk_prefix[b] = exclusive prefix of effective counts; blk_prefix[nblk] = regT; result filled.
 __global__ __launch_bounds__(1024) void k_final(Pipe p) {
   __shared__ uint64_t s_part[1024];
-  __shared__ uint64_t s_regT, s_base;
+  __shared__ uint64_t s_base;
   const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
   const uint64_t T = p.tpos[0];
   uint64_t tp = term_pos(T);
@@ -297,7 +333,6 @@ __global__ __launch_bounds__(1024) void k_final(Pipe p) {
   if (T == ~0ull) { tp = p.len; ts = LDB_ERR_MALFORMED; }  // unreachable: the chain always stops
   const uint64_t regT = tp / kW;
   if (threadIdx.x == 0) {
-    s_regT = regT;
     uint64_t acc = 0;
     for (uint64_t b = 0; b < nblk; ++b) {
       p.blk_prefix[b] = acc;
@@ -408,7 +443,6 @@ __global__ __launch_bounds__(1024) void k_compact(Pipe p) {
 __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   if (threadIdx.x != 0) return;
   if (only_on_overflow && !p.ctr[1]) return;
-  const uint32_t* t8 = p.gtab + kT8Off;
   struct G {
     const uint8_t* q;
     __device__ uint32_t operator()(int i) const { return q[i]; }
@@ -739,6 +773,17 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
   (void)hipStreamDestroy(s);
   return rc;
 }
+
+#ifdef LDB_STAMPS
+int ldb_debug_stamps(uint64_t* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), 64) != hipSuccess) return LDB_ERR_HIP;
+  if (reset) {
+    uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 64) != hipSuccess) return LDB_ERR_HIP;
+  }
+  return LDB_OK;
+}
+#endif
 
 int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n) {
   if (!c) return LDB_ERR_ARG;

@@ -9,6 +9,8 @@
 #include <cstdint>
 #include <cstring>
 #include <vector>
+#include <cstdio>
+#include <cstdlib>
 
 #include "../../lazydb_amd/csrc/ldb_pipeline.h"
 
@@ -44,6 +46,8 @@ struct CpuWave {
     for (int l = 0; l < kLanes; ++l) { out[l] = s; s += v(l); }
   }
   template <class F> void single(F f) { f(); }
+  uint32_t bcast_or(uint32_t x) { return x; }
+  void stamp(int) {}
 };
 
 struct Emu {
@@ -68,6 +72,7 @@ struct Emu {
     View v;
     v.buf = buf.data();
     v.tab = tab.data();
+    v.xw = xw.data();
     v.R0 = r * (uint64_t)kW;
     v.rlen = region_len(p, r);
     v.len = p.len;
@@ -75,7 +80,8 @@ struct Emu {
     RegionSum s;
     CpuWave wp;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    region_process(wp, v, sh, enter, &s, [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
+    LaneKeep keep[kLanes];
+    region_process(wp, v, sh, enter, &s, [&](int l) -> LaneKeep& { return keep[l]; }, [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
       sc[slot].pos = pos;
       sc[slot].k_size = k;
       sc[slot].v_size = vv;
@@ -120,7 +126,15 @@ extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, 
   for (uint64_t r = 0; r < nreg; ++r) emu.run(p, r, kForceSpec);
   // k_link
   for (uint64_t r = 0; r < nreg; ++r) {
-    if (link_broken(p, r)) fail[ctr[0]++] = (int64_t)r;
+    if (link_broken(p, r)) {
+      fail[ctr[0]++] = (int64_t)r;
+      if (getenv("LDB_EMU_DEBUG")) {
+        const uint64_t m = exitp[r] / kW;
+        fprintf(stderr, "fail r=%llu start=%llu exit=%llu st=%d -> m=%llu start[m]=%llu (rel %lld) st[m]=%d\n",
+                (unsigned long long)r, (unsigned long long)start[r], (unsigned long long)exitp[r], status[r],
+                (unsigned long long)m, (unsigned long long)start[m], (long long)(start[m] - m * kW), status[m]);
+      }
+    }
     if (r == 0 && start[0] != 0) fail[ctr[0]++] = -1;
   }
   const uint32_t nfail = ctr[0];

@@ -214,6 +214,29 @@ def noncanonical() -> bytes:
     return image(out, sum(map(len, out)) + 64)
 
 
+def noncanonical5() -> bytes:
+    """5-byte padded expiredAt / txID varints (re-encoded shorter by EncodeEntry) among normal entries."""
+    rng = random.Random(23)
+    out = []
+    for i in range(300):
+        key, val = alpha(rng, rng.randrange(1, 20)), alpha(rng, rng.randrange(0, 100))
+        if i % 3:
+            out.append(ent(key=key, value=val, expired_at=rng.choice([0, 5, 1676969769])))
+            continue
+        fields = [rng.choice([0, 1, 63, 1000]), rng.choice([0, 7]), 0, len(key), len(val)]
+        hdr = bytearray([0])
+        for j, f in enumerate(fields):
+            enc = bytearray(P.put_varint(f))
+            if j == i % 2 or rng.random() < 0.3:
+                while len(enc) < 5:
+                    enc[-1] |= 0x80
+                    enc.append(0)
+            hdr += enc
+        body = bytes(hdr) + key + val
+        out.append(struct.pack("<I", __import__("zlib").crc32(body)) + body)
+    return image(out, sum(map(len, out)) + 64)
+
+
 def malformed(seed: int) -> list[tuple[str, bytes]]:
     """Random header windows after a valid prefix; keep one image per ReadLogEntry outcome,
     plus an accepted entry whose decoded header size is <= 4 (getEntryCrc returns 0)."""
@@ -260,6 +283,7 @@ def fixtures() -> list[tuple[str, bytes, list[int]]]:
         ("sentinel_mid", sentinel_mid(), [0]),
         ("zero_len_entries", zero_len_entries(), [0]),
         ("noncanonical", noncanonical(), [0]),
+        ("noncanonical5", noncanonical5(), [0, 1]),
         ("all_zero", bytes(10000), [0, 1]),
         ("tiny_37", ent(key=b"k", value=b"v") + bytes(25), [0, 1]),
         ("empty", b"", [0, 1]),

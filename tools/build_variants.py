@@ -1,0 +1,36 @@
+"""Build tuning variants of liblazydb_gpu.so (waves per workgroup, LDS ring depth, stamps).
+
+Usage: python tools/build_variants.py w8n2 w12n1 stamps ...  -> lazydb_amd/_lib/var_<name>.so
+Select one at run time with LAZYDB_GPU_LIB=<path>.
+"""
+import os
+import re
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "lazydb_amd", "csrc", "ldb_scan.hip")
+OUT = os.path.join(ROOT, "lazydb_amd", "_lib")
+
+
+def build(name: str) -> str:
+    defs = []
+    m = re.fullmatch(r"w(\d+)n(\d+)", name)
+    if m:
+        defs = [f"-DLDB_WPB={m.group(1)}", f"-DLDB_NB={m.group(2)}"]
+    elif name == "stamps":
+        defs = ["-DLDB_STAMPS=1"]
+    else:
+        raise SystemExit(f"unknown variant {name}")
+    out = os.path.join(OUT, f"var_{name}.so")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                    "-Wno-unused-function", *defs, "-o", out, SRC], check=True)
+    return out
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    with ThreadPoolExecutor(4) as ex:
+        for p in ex.map(build, sys.argv[1:]):
+            print(p)
