@@ -142,8 +142,10 @@ int ldb_scan_file_dev_serial(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len,
                              int tuple_kind, void* d_out, uint64_t cap, ldb_scan_result* d_result,
                              void* stream);
 
-/* Timing hook for bench.py: average device time (ms) of the main decode+CRC kernel over the
- * launches since the last reset, measured with HIP events on the scan stream. */
+/* Timing hook for bench.py: average device time (ms) of the main decode+CRC kernel and of the
+ * whole pipeline over the launches since the last reset, measured with HIP events recorded on
+ * the scan stream around each launch (no host synchronisation while enabled; the query waits
+ * for the recorded events). enable: 1 on + reset, 0 off + reset, -1 query only. */
 int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n);
 
 #ifdef __cplusplus

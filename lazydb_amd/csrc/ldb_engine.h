@@ -31,6 +31,13 @@
 
 #include "ldb_common.h"
 
+#ifdef LDB_EMU_COUNTERS   // CPU emulator instrumentation only (tests/emu): per-lane event counts
+namespace ldb { extern int g_emu_lane; extern uint32_t g_emu_cnt[8][64]; }
+#define LDB_COUNT(id) (++ldb::g_emu_cnt[id][ldb::g_emu_lane & 63])
+#else
+#define LDB_COUNT(id) ((void)0)
+#endif
+
 namespace ldb {
 
 // ---------------------------------------------------------------- geometry
@@ -50,7 +57,8 @@ constexpr int kTAOff = 0;                 // 2048 + 2048 + 1024
 constexpr int kTBOff = 5120;              // 2048 + 2048 + 1024
 constexpr int kT8Off = 10240;             // 256: byte-at-a-time table (rare paths)
 constexpr int kZSOff = 10496;             // 4 x 256: register shift by kS zero bytes (fold chains)
-constexpr int kTabWords = 11520;
+constexpr int kKOff = 11520;              // kS + 1: K[n] = register after n zero bytes from ~0
+constexpr int kTabWords = 11616;
 constexpr int kTabBytes = kTabWords * 4;
 
 // Force codes for a lane (re)run.
@@ -79,6 +87,7 @@ inline void build_tables(uint32_t* tab) {
   for (uint32_t i = 0; i < 256; ++i) tab[kT8Off + i] = step_bits(i, 8);
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b) tab[kZSOff + q * 256 + b] = step_bits(b << (8 * q), 8 * kS);
+  for (int n = 0; n < kTabWords - kKOff; ++n) tab[kKOff + n] = n <= kS ? step_bits(0xFFFFFFFFu, 8 * n) : 0u;
 }
 
 // ---------------------------------------------------------------- memory views
@@ -137,22 +146,22 @@ LDB_HD uint32_t mask_from(uint32_t nbytes) {  // bytes [nbytes, 4) kept, nbytes 
 // from register `init`: the register is injected (XORed) into the first 4 message bytes, which
 // is exact for |M| >= 4; for |M| < 4 the unconsumed part (init >> 8|M|) is added at the end.
 // init = ~0: CRC-32 span (getEntryCrc); init = 0: raw register (leading zero bytes are free).
-LDB_HD uint32_t crc_segment(const View& v, int64_t lo, int64_t hi, uint32_t init) {
-  const int64_t L = hi - lo;
-  const int64_t n8 = (L + 7) / 8;
-  int64_t c = hi - 8 * n8;
+LDB_HD uint32_t crc_segment(const View& v, int lo, int hi, uint32_t init) {
+  const int L = hi - lo;
+  const int n8 = (L + 7) >> 3;
+  const int c = hi - 8 * n8;
   const uint32_t pad = (uint32_t)(lo - c);  // 0..7 leading bytes outside the segment
   const uint32_t m0 = mask_from(pad), m1 = pad <= 4 ? 0xFFFFFFFFu : mask_from(pad - 4);
   // init bytes land on message bytes [pad, pad+4) of the 12-byte window starting at c
   const uint64_t sh64 = (uint64_t)init << (8 * (pad & 3));
   const uint32_t ilo = (uint32_t)sh64, ihi = (uint32_t)(sh64 >> 32);
   const uint32_t i0 = pad < 4 ? ilo : 0u, i1 = pad < 4 ? ihi : ilo, i2 = pad < 4 ? 0u : ihi;
-  const int64_t a0 = c + kPre;
-  int64_t q = a0 & ~(int64_t)3;
+  const int a0 = c + kPre;
+  int q = a0 & ~3;
   const uint32_t sh = (uint32_t)(a0 & 3);
   uint32_t d0 = lds32(v, q);
   uint32_t reg = 0;
-  for (int64_t k = 0; k < n8; ++k) {
+  for (int k = 0; k < n8; ++k) {
     const uint32_t d1 = lds32(v, q + 4), d2 = lds32(v, q + 8);
     uint32_t w0 = funnel(d1, d0, sh), w1 = funnel(d2, d1, sh);
     if (k == 0) { w0 = (w0 & m0) ^ i0; w1 = (w1 & m1) ^ i1; }
@@ -163,6 +172,63 @@ LDB_HD uint32_t crc_segment(const View& v, int64_t lo, int64_t hi, uint32_t init
   }
   if (L < 4) reg ^= init >> (8 * L);
   return reg;
+}
+
+// 16-byte LDS row (slices start 16-byte aligned in the staging buffer)
+struct alignas(16) Row16 { uint32_t w[4]; };
+
+// Uniform slice pass: raw CRC register (init 0) over slice bytes [B + r0, B + kS) on the slice's
+// natural 8-byte grid, bytes before B + r0 masked to zero (free while the register is 0).
+// Every lane runs the same kS/8 steps whatever its r0 (r0 >= kS: empty, returns 0).
+// A CRC span with init ~0 over the same bytes is this value ^ K[kS - r0] (linearity).
+LDB_HD uint32_t crc_slice_from(const View& v, int B, int r0) {
+  const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
+  uint32_t reg = 0;
+#pragma unroll
+  for (int k = 0; k < kS / 16; ++k) {
+    const Row16 q = row[k];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = r0 - 16 * k - 8 * h;   // bytes of this word before the piece
+      const int c0 = r < 0 ? 0 : (r > 4 ? 4 : r), c1 = r < 4 ? 0 : (r > 8 ? 4 : r - 4);
+      const uint32_t m0 = (uint32_t)(0xFFFFFFFFull << (8 * c0)), m1 = (uint32_t)(0xFFFFFFFFull << (8 * c1));
+      reg = crc_step8(v.tab, reg, q.w[2 * h] & m0, q.w[2 * h + 1] & m1);
+    }
+  }
+  return reg;
+}
+
+// Uniform two-chain slice pass (every lane, same kS/8 steps on the slice's natural 8-byte grid):
+//   chain A keeps bytes [B, B + tA), XORs C into bytes [B + tA, B + tA + 4) and zeroes the rest:
+//     A = shift(raw([B, B+tA)), kS - tA) ^ shift(C, kS - tA)   (the C >> 8L fix covers tA > kS - 4)
+//   chain B keeps bytes [B + uB, B + kS), zeroes the bytes before (free while its register is 0):
+//     Bv = raw([B + uB, B + kS))
+// tA >= kS: A = raw of the whole slice (C must be 0); uB >= kS: Bv = 0.
+LDB_HD void crc_slice2(const View& v, int B, int tA, uint32_t C, int uB, uint32_t* ra, uint32_t* rb) {
+  const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
+  uint32_t a = 0, b = 0;
+#pragma unroll
+  for (int k = 0; k < kS / 16; ++k) {
+    const Row16 q = row[k];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int off = 16 * k + 8 * h;
+      const uint64_t w = ((uint64_t)q.w[2 * h + 1] << 32) | q.w[2 * h];
+      const int t = tA - off;    // bytes of this word chain A keeps
+      const int u = uB - off;    // bytes of this word chain B drops
+      const int tc = t < 0 ? 0 : (t > 8 ? 8 : t), uc = u < 0 ? 0 : (u > 8 ? 8 : u);
+      const uint64_t keepA = tc == 8 ? ~0ull : ~(~0ull << (8 * tc));
+      const uint64_t keepB = uc == 8 ? 0ull : (~0ull << (8 * uc));
+      const uint64_t inj = (t >= 0 && t < 8) ? ((uint64_t)C << (8 * t)) : ((t > -4 && t < 0) ? ((uint64_t)C >> (-8 * t)) : 0ull);
+      const uint64_t wa = (w & keepA) ^ inj, wb = w & keepB;
+      a = crc_step8(v.tab, a, (uint32_t)wa, (uint32_t)(wa >> 32));
+      b = crc_step8(v.tab, b, (uint32_t)wb, (uint32_t)(wb >> 32));
+    }
+  }
+  const int L = kS - tA;
+  if (L > 0 && L < 4) a ^= C >> (8 * L);
+  *ra = a;
+  *rb = b;
 }
 
 // register shift by kS zero bytes (constant-distance GF(2) multiply, 4 table reads)
@@ -191,103 +257,129 @@ LDB_HD uint32_t pext7(uint32_t b) {
   return (b & 0x7Fu) | ((b >> 1) & 0x3F80u) | ((b >> 2) & 0x1FC000u) | ((b >> 3) & 0xFE00000u);
 }
 
-LDB_HD uint32_t vlen32(uint64_t ux) {  // bytes of PutUvarint(ux)
-  uint32_t n = 1;
-  while (ux >= 0x80u) { ux >>= 7; ++n; }
-  return n;
+// bytes of PutUvarint(ux), ux < 2^32
+LDB_HD uint32_t vlen32(uint32_t ux) {
+  const uint32_t bits = ux ? 32u - (uint32_t)__builtin_clz(ux) : 1u;
+  return ((bits + 6u) * 147u) >> 10;   // ceil(bits / 7) for bits in [1, 32]
 }
 
-// ReadLogEntry(off) up to the CRC comparison (classify_entry semantics), fast path for headers
-// whose five varints end within bytes [5, 20) with ts/k/v varints <= 4 bytes and expiredAt/txID
-// varints <= 5 bytes — every header LazyDB's writer emits for sizes < 128 MiB. Anything else
-// (and every status other than kCont) goes through the exact byte-wise decoder.
-LDB_HD EntryInfo classify_at(const View& v, int64_t p) {
-  EntryInfo r;
-  r.size = 0;
+// ReadLogEntry(off) up to the CRC comparison, as the walk needs it.
+struct Hot {
+  int32_t status;     // kCont (decoded and readable) or the ReadLogEntry status at this position
+  uint32_t crc;
+  int32_t hsize;      // decodeHeader's offset (<= 4 only for degenerate headers: no CRC span)
+  uint32_t esize;     // header length EncodeEntry re-emits
+  uint32_t stat;
+  uint32_t k, v;
+  uint32_t plaus;     // plausible_start (speculation only)
+  uint64_t size;      // entrySize = hsize + k + v (status == kCont)
+};
+
+LDB_HD Hot hot_from(const EntryInfo& e) {
+  Hot r;
+  r.status = e.status;
+  r.crc = e.h.crc;
+  r.hsize = e.h.size;
+  r.esize = (uint32_t)e.h.enc_size;
+  r.stat = e.h.stat;
+  r.k = e.h.k_size;
+  r.v = e.h.v_size;
+  r.plaus = plausible_start(e) ? 1u : 0u;
+  r.size = e.size;
+  return r;
+}
+
+LDB_HD uint64_t pack_hot(uint64_t off, const Hot& h) {
+  return (off & 0xFFFFFFFFFFull) | ((uint64_t)(h.hsize & 0x3F) << 40) | ((uint64_t)(h.esize & 0x3F) << 46) |
+         ((uint64_t)(h.stat & 0xFF) << 52);
+}
+
+// Fast decode at region-relative p for headers whose five varints end within bytes [5, 20)
+// with ts/k/v varints <= 4 bytes and expiredAt/txID <= 5 bytes (every header LazyDB's writer
+// emits for sizes < 128 MiB). Everything else, and every status other than kCont, goes through
+// the exact byte-wise decoder (classify_entry, Go semantics).
+LDB_HD Hot classify_at(const View& v, int p) {
   const uint64_t off = v.R0 + (uint64_t)p;
-  if (read_eof(v.len, v.io, (int64_t)off, kMaxHeader)) { r.status = LDB_EOF_WINDOW; return r; }
-  // window bytes [p, p+24) -> w[0..5]
-  const int64_t a = p + kPre;
-  const int64_t q = a & ~(int64_t)3;
-  const uint32_t sh = (uint32_t)(a & 3);
-  uint32_t d[7];
+  if (!read_eof(v.len, v.io, (int64_t)off, kMaxHeader)) {
+    const int a = p + kPre;
+    const int q = a & ~3;
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[7];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) d[i] = lds32(v, q + 4 * i);
-  uint32_t w[6];
+    for (int i = 0; i < 7; ++i) d[i] = lds32(v, q + 4 * i);
+    uint32_t w[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) w[i] = funnel(d[i + 1], d[i], sh);
-  // continuation bits of bytes 4..23, terminators among bytes 5..19
-  const uint32_t M = msb4(w[1]) | (msb4(w[2]) << 4) | (msb4(w[3]) << 8) | (msb4(w[4]) << 12) | (msb4(w[5]) << 16);
-  uint32_t T = (~M) & 0xFFFEu;   // bit i <-> byte 4 + i; keep bytes 5..19
-  uint32_t e[5];
-  uint32_t prev = 0;
-  bool fast = true;
-#pragma unroll
-  for (int f = 0; f < 5; ++f) {
-    if (T == 0) { fast = false; e[f] = 0; continue; }
-    e[f] = __builtin_ctz(T);   // byte index - 4
-    T &= T - 1;
-    const uint32_t n = e[f] - prev;
-    fast = fast && n <= (f < 2 ? 5u : 4u);
-    prev = e[f];
-  }
-  if (fast) {
-    // field f occupies window bytes [4 + e[f-1] + 1, 4 + e[f]]
-    uint32_t val[3], lastb[5], n[5];
-    uint32_t pe = 0;
+    for (int i = 0; i < 6; ++i) w[i] = funnel(d[i + 1], d[i], sh);
+    // terminator bits (bit i <-> window byte 4 + i), bytes 5..19
+    const uint32_t M = msb4(w[1]) | (msb4(w[2]) << 4) | (msb4(w[3]) << 8) | (msb4(w[4]) << 12);
+    uint32_t T = (~M) & 0xFFFEu;
+    uint32_t e[5];
+    uint32_t prev = 0;
+    bool fast = true;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
-      const uint32_t s = 5 + pe;                 // first byte of the field (window index)
-      n[f] = e[f] - pe;
-      // 4 bytes at window index s (s in [5, 19]): dword s>>2 .. +1 of w
-      const uint32_t di = s >> 2, bs = s & 3;
-      const uint32_t lo = di == 1 ? w[1] : di == 2 ? w[2] : di == 3 ? w[3] : w[4];
-      const uint32_t hi = di == 1 ? w[2] : di == 2 ? w[3] : di == 3 ? w[4] : w[5];
-      uint32_t b = funnel(hi, lo, bs);
-      const uint32_t nn = n[f] > 4 ? 4 : n[f];
-      if (n[f] > 4) {  // 5-byte expiredAt / txID: its last byte is window byte 4 + e[f] (9..14)
-        const uint32_t li = 4 + e[f];
-        lastb[f] = ((li >> 2) == 2 ? w[2] : w[3]) >> (8 * (li & 3)) & 0xFFu;
-      } else {
-        lastb[f] = (b >> (8 * (nn - 1))) & 0xFFu;
-      }
-      if (f >= 2) {
-        b &= nn == 4 ? 0xFFFFFFFFu : ((1u << (8 * nn)) - 1);
-        val[f - 2] = pext7(b);
-      }
-      if (f == 0) r.h.expired_at = (b & 1u) ? -1 : 0;   // sign only (zigzag LSB); value unused here
-      pe = e[f];
+      e[f] = T ? (uint32_t)__builtin_ctz(T) : 16u;
+      T &= T - 1;
+      fast = fast && e[f] < 16u && e[f] - prev <= (f < 2 ? 5u : 4u);
+      prev = e[f];
     }
-    bool canon = true;
+    if (fast) {
+      uint32_t val[3];
+      uint32_t pe = 0, sign0 = 0;
+      bool canon = true;
 #pragma unroll
-    for (int f = 0; f < 5; ++f) canon = canon && (n[f] == 1 || lastb[f] != 0);
-    if (canon) {
-      const uint32_t ts_ux = val[0], k_ux = val[1], v_ux = val[2];
-      const int64_t ts = zigzag(ts_ux), ks = zigzag(k_ux), vs = zigzag(v_ux);
-      r.h.crc = w[0];
-      r.h.stat = w[1] & 0xFFu;
-      r.h.tx_id = 0;   // value unused on the fast path (ENTRY tuples re-decode in k_compact)
-      r.h.tx_stat = (uint32_t)(uint16_t)ts;
-      r.h.k_size = (uint32_t)ks;
-      r.h.v_size = (uint32_t)vs;
-      r.h.size = (int32_t)(5 + e[4]);
-      r.h.raw_tx_stat_ok = (ts >= 0 && ts <= 2) ? 1u : 0u;
-      r.h.canonical = ks >= 0 && vs >= 0;
-      r.h.enc_size = (int32_t)(5 + n[0] + n[1] + vlen32((uint64_t)r.h.tx_stat << 1) + vlen32((uint64_t)r.h.k_size << 1) +
-                               vlen32((uint64_t)r.h.v_size << 1));
-      if (r.h.crc == 0 && r.h.k_size == 0 && r.h.v_size == 0) { r.status = LDB_EOF_SENTINEL; return r; }
-      const uint64_t kv = (uint64_t)r.h.k_size + (uint64_t)r.h.v_size;
-      if (kv && read_eof(v.len, v.io, (int64_t)(off + (uint64_t)r.h.size), kv)) { r.status = LDB_EOF_KV; return r; }
-      r.size = (uint64_t)r.h.size + kv;
-      r.status = kCont;
-      return r;
+      for (int f = 0; f < 5; ++f) {
+        const uint32_t st = 5 + pe;               // first byte of the field (window index, 5..19)
+        const uint32_t n = e[f] - pe;
+        const uint32_t di = st >> 2, bs = st & 3;
+        const uint32_t lo = di == 1 ? w[1] : di == 2 ? w[2] : di == 3 ? w[3] : w[4];
+        const uint32_t hi = di == 1 ? w[2] : di == 2 ? w[3] : di == 3 ? w[4] : w[5];
+        uint32_t b = funnel(hi, lo, bs);
+        const uint32_t nn = n > 4 ? 4 : n;
+        uint32_t lastb;
+        if (n > 4) {  // 5-byte expiredAt / txID: its last byte is window byte 4 + e[f]
+          const uint32_t li = 4 + e[f];
+          lastb = (((li >> 2) == 2 ? w[2] : w[3]) >> (8 * (li & 3))) & 0xFFu;
+        } else {
+          lastb = (b >> (8 * (nn - 1))) & 0xFFu;
+        }
+        canon = canon && (n == 1 || lastb != 0);
+        if (f == 0) sign0 = b & 1u;
+        if (f >= 2) {
+          b &= nn == 4 ? 0xFFFFFFFFu : ((1u << (8 * nn)) - 1);
+          val[f - 2] = pext7(b);
+        }
+        pe = e[f];
+      }
+      if (canon) {
+        Hot r;
+        const int32_t ts = (int32_t)(val[0] >> 1) ^ -(int32_t)(val[0] & 1u);
+        const int32_t ks = (int32_t)(val[1] >> 1) ^ -(int32_t)(val[1] & 1u);
+        const int32_t vs = (int32_t)(val[2] >> 1) ^ -(int32_t)(val[2] & 1u);
+        r.crc = w[0];
+        r.stat = w[1] & 0xFFu;
+        r.k = (uint32_t)ks;   // uint32(int64) of a value in (-2^27, 2^27)
+        r.v = (uint32_t)vs;
+        r.hsize = (int32_t)(5 + e[4]);
+        const uint32_t tx_stat = (uint32_t)(uint16_t)ts;
+        // exp + txID occupy window bytes [5, 5 + e[1]); EncodeEntry re-emits them as read
+        r.esize = 5 + e[1] + vlen32(tx_stat << 1) + vlen32(r.k << 1) + vlen32(r.v << 1);
+        const bool sentinel = r.crc == 0 && r.k == 0 && r.v == 0;
+        const uint64_t kv = (uint64_t)r.k + (uint64_t)r.v;
+        r.status = sentinel ? LDB_EOF_SENTINEL
+                            : ((kv && read_eof(v.len, v.io, (int64_t)(off + (uint64_t)r.hsize), kv)) ? LDB_EOF_KV : kCont);
+        r.size = (uint64_t)r.hsize + kv;
+        r.plaus = (r.status == kCont && r.stat <= 2u && ts >= 0 && ts <= 2 && ks >= 0 && vs >= 0 && sign0 == 0 &&
+                   (uint32_t)r.hsize == r.esize && r.crc != 0) ? 1u : 0u;
+        return r;
+      }
     }
   }
-  return classify_slow(v, p);
+  return hot_from(classify_slow(v, p));
 }
 
 // 38 zero bytes at p (p + 38 inside the staged bytes)?
-LDB_HD bool zero_window(const View& v, int64_t p) {
+LDB_HD bool zero_window(const View& v, int p) {
   uint32_t o = 0;
   for (int i = 0; i < kMaxHeader; ++i) o |= vbyte(v, p + i);
   return o == 0;
@@ -300,7 +392,7 @@ struct LaneState {
   int32_t term;      // kCont or the ReadLogEntry status that stopped the walk
   uint32_t tpos;     // region-relative position of that status
   uint64_t x;        // absolute offset after the last entry that started here (term == kCont)
-  uint32_t raw;      // s == kNone32: raw CRC register over the whole slice [B, Eeff); else unused
+  uint32_t raw;      // lane_crc chain A: covered slice: raw register of [B, Eeff); else shift(raw([B,s)) ^ C, E-s)
   uint32_t sflag;    // kStraddle | kSkip | kNoCrc for the last entry (x beyond the slice)
   uint32_t so;       // its region-relative start
   uint32_t scrc;     // its stored crc
@@ -309,100 +401,131 @@ struct LaneState {
 
 // Tuples a lane keeps for emission (registers on the GPU).
 struct LaneKeep {
-  uint64_t pos[kKeep];
-  uint32_t k[kKeep];
-  uint32_t v[kKeep];
+  uint64_t pos0, pos1;
+  uint32_t k0, k1, v0, v1;
+  LDB_HD void put(uint32_t i, uint64_t pos, uint32_t k, uint32_t v) {
+    if (i == 0) { pos0 = pos; k0 = k; v0 = v; }
+    else { pos1 = pos; k1 = k; v1 = v; }
+  }
 };
+static_assert(kKeep == 2, "LaneKeep holds two tuples");
 
 // hasless(w, 3): a byte of w is < 3 (may flag extra bytes above a true hit; prefilter only)
 LDB_HD uint32_t small_bytes(uint32_t w) { return (w - 0x03030303u) & ~w & 0x80808080u; }
 
-// Speculative start search (never decides results; see plausible_start).
-LDB_HD uint32_t find_start(const View& v, int64_t B, int64_t Eeff) {
+// Speculative start search (never decides results; see plausible_start). Returns the start
+// (or kNone32) and its decode in *h (valid when the start is not kNone32).
+LDB_HD uint32_t find_start(const View& v, int B, int Eeff, Hot* h) {
   // first window-EOF position (every later position is one too)
-  int64_t pe = Eeff;
+  int pe = Eeff;
   {
     const int64_t lim = (int64_t)(v.len - v.R0) - kMaxHeader + (v.io == LDB_IO_MMAP ? 0 : 1);
-    if (lim < pe) pe = lim < B ? B : lim;
+    if (lim < (int64_t)pe) pe = lim < (int64_t)B ? B : (int)lim;
   }
-  // stat bytes of positions B..B+79 are bytes B+4..B+83: dwords at B+4+4q (aligned, B % 16 == 0)
+  // stat bytes of positions B..B+79 are bytes B+4..B+83: dwords 1..20 of the rows at B
+  const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
   uint32_t cand[3] = {0, 0, 0};  // bit i <-> position B + i
 #pragma unroll
-  for (int qd = 0; qd < kS / 4; ++qd) {
-    const uint32_t t = small_bytes(lds32(v, kPre + B + 4 + 4 * qd));
-    const uint32_t bits = msb4(t);
-    cand[qd >> 3] |= bits << (4 * (qd & 7));
-  }
-  const int64_t nvalid = pe - B;  // positions [B, pe) are decodable
-  for (int wd = 0; wd < 3; ++wd) {
-    const int64_t lo = 32 * wd;
-    uint32_t m = cand[wd];
-    if (nvalid <= lo) m = 0;
-    else if (nvalid < lo + 32) m &= (1u << (nvalid - lo)) - 1;
-    while (m) {
-      const int64_t p = B + lo + __builtin_ctz(m);
-      m &= m - 1;
-      const EntryInfo e = classify_at(v, p);
-      if (plausible_start(e)) {
-        // cheap one-hop check: the implied next entry must pass the same stat-byte prefilter
-        // (or lie past the staged bytes / in the header-window EOF zone)
-        const uint64_t nx = (uint64_t)p + e.size;
-        if (nx + 8 > (uint64_t)(kW + kHalo) || v.R0 + nx + kMaxHeader > v.len || vbyte(v, (int64_t)nx + 4) <= 2u)
-          return (uint32_t)p;
-        continue;
-      }
-      if (e.status == LDB_EOF_SENTINEL && zero_window(v, p)) return (uint32_t)p;
+  for (int k = 0; k < 6; ++k) {
+    const Row16 q = row[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int qd = 4 * k + j - 1;   // dword qd + 1 of the slice holds stat bytes of positions 4qd..4qd+3
+      if (qd < 0 || qd >= kS / 4) continue;
+      cand[qd >> 3] |= msb4(small_bytes(q.w[j])) << (4 * (qd & 7));
     }
   }
-  return pe < Eeff ? (uint32_t)pe : kNone32;
+  const int nvalid = pe - B;  // positions [B, pe) are decodable
+  uint32_t m0 = cand[0], m1 = cand[1], m2 = cand[2];
+  if (nvalid < 32) { m0 &= nvalid <= 0 ? 0u : (0xFFFFFFFFu >> (32 - nvalid)); m1 = 0; m2 = 0; }
+  else if (nvalid < 64) { m1 &= nvalid == 32 ? 0u : (0xFFFFFFFFu >> (64 - nvalid)); m2 = 0; }
+  else if (nvalid < 96) { m2 &= nvalid == 64 ? 0u : (0xFFFFFFFFu >> (96 - nvalid)); }
+  while (m0 | m1 | m2) {
+    int bit;
+    if (m0) { bit = __builtin_ctz(m0); m0 &= m0 - 1; }
+    else if (m1) { bit = 32 + __builtin_ctz(m1); m1 &= m1 - 1; }
+    else { bit = 64 + __builtin_ctz(m2); m2 &= m2 - 1; }
+    const int p = B + bit;
+    LDB_COUNT(0);
+    const Hot e = classify_at(v, p);
+    if (e.plaus) {
+      // cheap one-hop check: the implied next entry must pass the same stat-byte prefilter
+      // (or lie past the staged bytes / in the header-window EOF zone)
+      const uint64_t nx = (uint64_t)p + e.size;
+      if (nx + 8 > (uint64_t)(kW + kHalo) || v.R0 + nx + kMaxHeader > v.len || vbyte(v, (int)nx + 4) <= 2u) {
+        *h = e;
+        return (uint32_t)p;
+      }
+      continue;
+    }
+    if (e.status == LDB_EOF_SENTINEL && zero_window(v, p)) { *h = e; return (uint32_t)p; }
+  }
+  if (pe < Eeff) {
+    h->status = LDB_EOF_WINDOW;
+    return (uint32_t)pe;
+  }
+  return kNone32;
 }
 
-// Process one lane's slice: start (by `force`), walk, CRC pieces, in-slice verification.
-LDB_HD void lane_process(const View& v, int lane, uint32_t force, LaneState* st, LaneKeep* kp) {
-  const int64_t B = (int64_t)lane * kS, E = B + kS;
-  const int64_t Eeff = E < (int64_t)v.rlen ? E : (int64_t)v.rlen;
+// Walk one lane's slice: start (by `force`), entries that start in the slice, in-slice CRC
+// verification of entries that end inside it. The open pieces are CRC'd later by lane_crc.
+LDB_HD void lane_walk(const View& v, int lane, uint32_t force, LaneState* st, LaneKeep* kp) {
+  const int B = lane * kS, E = B + kS;
+  const int Eeff = E < (int)v.rlen ? E : (int)v.rlen;
   LaneState r;
   r.s = kNone32; r.cnt = 0; r.term = kCont; r.tpos = 0; r.x = 0; r.raw = 0; r.sflag = 0; r.so = 0; r.scrc = 0;
   r.rout = 0;
-  if (B >= Eeff) { *st = r; return; }          // slice entirely past the end of the file
-  const uint32_t s = force == kForceSpec ? find_start(v, B, Eeff) : (force == kForceNone ? kNone32 : force);
-  r.s = s;
-  // a covered slice contributes its raw register; a slice with a start CRCs its prefix later
-  // (lane_finish), continuing the register carried in from the entry that covers it
-  if (s == kNone32) {
-    r.raw = crc_segment(v, B, Eeff, 0u);
-    *st = r;
-    return;
-  }
-  int64_t o = s;
-  for (;;) {
-    if (o >= Eeff) { r.x = v.R0 + (uint64_t)o; break; }   // next entry starts in a later slice
-    const EntryInfo e = classify_at(v, o);
-    if (e.status != kCont) { r.term = e.status; r.tpos = (uint32_t)o; break; }
-    const uint64_t end = (uint64_t)o + e.size;
-    if (e.h.size <= 4 && e.h.crc != 0) { r.term = LDB_ERR_CRC; r.tpos = (uint32_t)o; break; }  // getEntryCrc == 0
-    if (r.cnt < kKeep) {
-      kp->pos[r.cnt] = pack_pos(v.R0 + (uint64_t)o, e.h);
-      kp->k[r.cnt] = e.h.k_size;
-      kp->v[r.cnt] = e.h.v_size;
-    }
-    if (end <= (uint64_t)E) {
-      if (e.h.size > 4 && crc_segment(v, o + 4, (int64_t)end, 0xFFFFFFFFu) != ~e.h.crc) {  // ErrInvalidCrc
-        r.term = LDB_ERR_CRC; r.tpos = (uint32_t)o; break;
+  if (B < Eeff) {
+    Hot e;
+    e.status = kCont - 1;   // "not decoded yet"
+    const uint32_t s = force == kForceSpec ? find_start(v, B, Eeff, &e) : (force == kForceNone ? kNone32 : force);
+    r.s = s;
+    if (s != kNone32) {
+      int o = (int)s;
+      for (;;) {
+        if (o >= Eeff) { r.x = v.R0 + (uint64_t)o; break; }   // next entry starts in a later slice
+        if (e.status == kCont - 1 || o != (int)s) { LDB_COUNT(1); e = classify_at(v, o); }
+        if (e.status != kCont) { r.term = e.status; r.tpos = (uint32_t)o; break; }
+        if (e.hsize <= 4 && e.crc != 0) { r.term = LDB_ERR_CRC; r.tpos = (uint32_t)o; break; }  // getEntryCrc == 0
+        if (r.cnt < kKeep) kp->put(r.cnt, pack_hot(v.R0 + (uint64_t)o, e), e.k, e.v);
+        const uint64_t end = (uint64_t)o + e.size;
+        if (end <= (uint64_t)E) {
+          LDB_COUNT(2);
+          if (e.hsize > 4 && crc_segment(v, o + 4, (int)end, 0xFFFFFFFFu) != ~e.crc) {  // ErrInvalidCrc
+            r.term = LDB_ERR_CRC; r.tpos = (uint32_t)o; break;
+          }
+          r.cnt++;
+          o = (int)end;
+          continue;
+        }
+        // straddles out of the slice: lane_crc CRCs the part inside, the folds finish it
+        r.cnt++;
+        r.sflag = kStraddle; r.so = (uint32_t)o; r.scrc = e.crc; r.x = v.R0 + end;
+        if (e.hsize <= 4) r.sflag |= kNoCrc;
+        else if (o + 4 >= E) r.sflag |= kSkip;
+        break;
       }
-      r.cnt++;
-      o = (int64_t)end;
-      continue;
     }
-    // straddles out of the slice: CRC the part inside, finish in the fold
-    r.cnt++;
-    r.sflag = kStraddle; r.so = (uint32_t)o; r.scrc = e.h.crc; r.x = v.R0 + end;
-    if (e.h.size <= 4) r.sflag |= kNoCrc;
-    else if (E - (o + 4) >= 4) r.rout = crc_segment(v, o + 4, E, 0xFFFFFFFFu);
-    else r.sflag |= kSkip;
-    break;
   }
   *st = r;
+}
+
+// The lane's CRC pieces in one uniform pass (crc_slice2):
+//   raw  <- chain A: covered slice: raw register of the whole slice; slice with a start s:
+//           shift(raw([B, s)) ^ C, E - s), C = the covering entry's expected final register
+//           (inject = 1) or nothing (inject = 0: region entry / no CRC check pending);
+//   rout <- chain B: the straddling entry's CRC register at the slice end (init ~0).
+LDB_HD void lane_crc(const View& v, int lane, LaneState* a, uint32_t C, uint32_t inject) {
+  const int B = lane * kS, E = B + kS;
+  const int Eeff = E < (int)v.rlen ? E : (int)v.rlen;
+  const bool open = (a->sflag & kStraddle) && !(a->sflag & (kNoCrc | kSkip)) && a->term == kCont;
+  const int tA = a->s == kNone32 ? kS : (int)a->s - B;
+  const int uB = open ? (int)a->so + 4 - B : kS;
+  uint32_t ra, rb;
+  crc_slice2(v, B, tA, inject ? C : 0u, uB, &ra, &rb);
+  if (a->s == kNone32 && Eeff < E) ra = B < Eeff ? crc_segment(v, B, Eeff, 0u) : 0u;   // last slice of the file
+  a->raw = ra;
+  a->rout = open ? rb ^ v.tab[kKOff + (kS - uB)] : 0u;
 }
 
 // ---------------------------------------------------------------- wave-level state (LDS)
@@ -410,8 +533,6 @@ struct WaveSh {
   LaneState ln[kLanes];
   uint32_t force[kLanes];
   uint32_t prefix[kLanes];   // exclusive prefix of emitted tuples per lane
-  uint32_t inreg[kLanes];    // register carried into a lane's prefix piece by the fold chains
-  uint32_t owner[kLanes];    // lane whose entry covers the prefix piece (kLanes: region entry)
 };
 
 // Link check for lane j (phase after lane_process): returns the lane to repair and its force,
@@ -432,16 +553,18 @@ LDB_HD int lane_link(const View& v, const WaveSh& w, int j, uint64_t noneMask, u
 // Re-walk lane j's accepted entries beyond the kept ones (rare) and emit index tuples.
 template <class Emit>
 LDB_HD void lane_emit(const View& v, const LaneState& a, const LaneKeep& kp, Emit emit) {
-  int64_t o = a.s;
+  int o = (int)a.s;
   for (uint32_t i = 0; i < a.cnt; ++i) {
     if (i < kKeep) {
-      emit(i, kp.pos[i], kp.k[i], kp.v[i]);
-      o = (int64_t)(LDB_POS_OFFSET(kp.pos[i]) - v.R0) + LDB_POS_HDR(kp.pos[i]) + kp.k[i] + kp.v[i];
+      const uint64_t pos = i == 0 ? kp.pos0 : kp.pos1;
+      const uint32_t k = i == 0 ? kp.k0 : kp.k1, vv = i == 0 ? kp.v0 : kp.v1;
+      emit(i, pos, k, vv);
+      o = (int)(LDB_POS_OFFSET(pos) - v.R0) + (int)LDB_POS_HDR(pos) + (int)(k + vv);
       continue;
     }
-    const EntryInfo e = classify_at(v, o);
-    emit(i, pack_pos(v.R0 + (uint64_t)o, e.h), e.h.k_size, e.h.v_size);
-    o += (int64_t)e.size;
+    const Hot e = classify_at(v, o);
+    emit(i, pack_hot(v.R0 + (uint64_t)o, e), e.k, e.v);
+    o += (int)e.size;
   }
 }
 

@@ -115,11 +115,21 @@ LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
   }
   const uint64_t m = end / kW;  // region holding the entry's end (may be == nreg when end == len)
   for (; k < m; ++k) reg = multmodp(p.xw[kW], reg) ^ p.rpre[k];
+  const uint32_t want = ~p.scrc[r];
   if (m < p.nreg) {
     const uint64_t n = end - m * (uint64_t)kW;
-    if (n) reg = multmodp(p.xw[n], reg) ^ p.rpre[m];
+    if (n) {
+      if (p.start[m] == kNone64) {
+        reg = multmodp(p.xw[n], reg) ^ p.rpre[m];   // region covered up to the end of the file
+      } else {
+        // rpre[m] = shift(raw([R0, n)), E0 - n), E0 = end of the slice holding n (region_process):
+        // reg(n) == want  <=>  shift(reg, E0) ^ rpre[m] == shift(want, E0 - n)
+        const uint64_t E0 = (n / kS + 1) * (uint64_t)kS;
+        return (multmodp(p.xw[E0], reg) ^ p.rpre[m]) == multmodp(p.xw[E0 - n], want);
+      }
+    }
   }
-  return reg == ~p.scrc[r];
+  return reg == want;
 }
 
 LDB_HD uint64_t pack_term(uint64_t pos, int32_t status) {

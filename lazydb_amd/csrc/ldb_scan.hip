@@ -33,21 +33,22 @@ using namespace ldb;
 namespace {
 
 #ifndef LDB_WPB
-#define LDB_WPB 8
+#define LDB_WPB 12
 #endif
 #ifndef LDB_NB
-#define LDB_NB 2
+#define LDB_NB 1
 #endif
 constexpr int kWPB = LDB_WPB;  // wavefronts per workgroup in k_scan_main
 constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
 constexpr int kG = kW / 1024 + 1;  // LDS-DMA instructions per region (5 x 1 KiB + the halo)
 
 // ---------------------------------------------------------------- wave policy (SIMT)
+constexpr int kStampSlots = 10;   // phase ids of region_process / k_scan_main (tools/stamps.py)
 struct GpuWave {
   int lane;
 #ifdef LDB_STAMPS
   uint64_t t_last = 0;
-  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc[kStampSlots] = {};
   __device__ void stamp(int id) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
     if (t_last) acc[id] += t - t_last;
@@ -143,16 +144,52 @@ __device__ __forceinline__ void store_tuple(ldb_index_tuple* dst, uint64_t pos, 
   *reinterpret_cast<uint4*>(dst) = t;
 }
 
-__device__ __forceinline__ void write_region(const Pipe& p, uint64_t r, const RegionSum& s) { store_region(p, r, s); }
+__device__ __forceinline__ uint64_t sgpr64(const void* ptr) {
+  const uint64_t x = (uint64_t)(uintptr_t)ptr;
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+}
+
+// Wave-uniform SoA base addresses held in SGPRs (read once per kernel).
+struct SumPtrs {
+  uint64_t start, exitp, soff, status, count, rpre, rout, scrc, sflag;
+  __device__ explicit SumPtrs(const Pipe& p)
+      : start(sgpr64(p.start)), exitp(sgpr64(p.exitp)), soff(sgpr64(p.soff)), status(sgpr64(p.status)),
+        count(sgpr64(p.count)), rpre(sgpr64(p.rpre)), rout(sgpr64(p.rout)), scrc(sgpr64(p.scrc)), sflag(sgpr64(p.sflag)) {}
+};
+
+// Region summary to the SoA arrays as two vector store instructions (lanes 0-2: 64-bit fields,
+// lanes 0-5: 32-bit fields) -- k_scan_main counts them in its vmcnt waits. Bases are selected per
+// lane from SGPRs (integer selects, no vector load: that would cost a vmcnt(0) beside the DMA).
+__device__ __forceinline__ void write_region_wave(const SumPtrs& b, uint64_t r, const RegionSum& s, int lane) {
+  if (lane < 3) {
+    const uint64_t a = lane == 0 ? b.start : (lane == 1 ? b.exitp : b.soff);
+    const uint64_t val = lane == 0 ? s.start : (lane == 1 ? s.exitp : s.soff);
+    reinterpret_cast<uint64_t*>((uintptr_t)a)[r] = val;
+  }
+  if (lane < 6) {
+    const uint64_t a = lane == 0 ? b.status
+                                 : lane == 1 ? b.count : lane == 2 ? b.rpre : lane == 3 ? b.rout : lane == 4 ? b.scrc : b.sflag;
+    const uint32_t val = lane == 0 ? (uint32_t)s.status
+                                   : lane == 1 ? s.count : lane == 2 ? s.rpre : lane == 3 ? s.rout : lane == 4 ? s.scrc : s.sflag;
+    reinterpret_cast<uint32_t*>((uintptr_t)a)[r] = val;
+  }
+}
 
 #ifdef LDB_STAMPS
-__device__ uint64_t g_stamps[8];
+__device__ uint64_t g_stamps[kStampSlots];
 #endif
 // ---------------------------------------------------------------- k_scan_main
 __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
+  if (blockIdx.x == 0) {  // control words of the later stages (stream-ordered after this kernel)
+    const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
+    for (uint64_t i = threadIdx.x; i < nblk; i += blockDim.x) p.blk[i] = 0;
+    if (threadIdx.x < 4) p.ctr[threadIdx.x] = 0;
+    if (threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -163,25 +200,31 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   const uint64_t gw = (uint64_t)blockIdx.x * kWPB + wave, nw = (uint64_t)gridDim.x * kWPB;
   const uint64_t count = gw < p.nreg ? (p.nreg - gw + nw - 1) / nw : 0;
   GpuWave wp{lane};
-  for (int b = 0; b < kNB - 1; ++b)
+  const SumPtrs sump(p);
+  // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
+  // has read it for the last time (region_process's buffer_free), so the DMA overlaps the summary,
+  // its stores and the next region's wait.
+  for (int b = 0; b < kNB; ++b)
     if ((uint64_t)b < count) stage_dma(p.img, p.len, gw + (uint64_t)b * nw, ring_lds + b * kBuf, lane);
   for (uint64_t i = 0; i < count; ++i) {
-    // prefetch region i+kNB-1 into the slot freed by region i-1, then wait for region i:
-    // at least (issued-after) DMA batches remain in flight, whatever stores were issued between.
-    const uint64_t pf = i + kNB - 1;
-    if (pf < count) {
-      stage_dma(p.img, p.len, gw + pf * nw, ring_lds + (uint32_t)(pf % kNB) * kBuf, lane);
-      wait_vm<(kNB - 1) * kG>();
-    } else if (pf == count && kNB >= 3) {
-      wait_vm<(kNB - 2) * kG>();
+    // Wait for region i's DMA: vmcnt(N) retires all but the N youngest VM ops (issue order, global
+    // ops only in this kernel). Younger than DMA(i) are at least: in steady state the region
+    // summary store of iteration i-kNB (>= 1 instruction) and, for kNB > 1, the DMAs of regions
+    // i+1 .. i+kNB-1 (kG instructions each; their summary stores are not counted: conservative).
+    if (i >= (uint64_t)kNB) {
+      wait_vm<(kNB - 1) * kG + 1>();
     } else {
-      wait_vm<0>();
+      const uint64_t ahead = (count < (uint64_t)kNB ? count : (uint64_t)kNB) - 1 - i;   // prologue DMAs after i
+      if (kNB >= 3 && ahead >= 2) wait_vm<2 * kG>();
+      else if (kNB >= 2 && ahead >= 1) wait_vm<kG>();
+      else wait_vm<0>();
     }
     GpuWave::sync();
     wp.stamp(6);
     const uint64_t r = gw + i * nw;
+    const uint32_t slot = (uint32_t)(i % kNB);
     View v;
-    v.buf = ring + (uint32_t)(i % kNB) * kBuf;
+    v.buf = ring + slot * kBuf;
     v.tab = tab;
     v.xw = p.xw;
     v.R0 = r * (uint64_t)kW;
@@ -190,16 +233,23 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
     LaneKeep kp;
-    region_process(wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LaneKeep& { return kp; },
-                   [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); });
-    if (lane == 0) write_region(p, r, wl->rs);
+    region_process(
+        wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LaneKeep& { return kp; },
+        [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot_, pos, k, vv); },
+        [&] {
+          const uint64_t nx = i + kNB;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every LDS read of this buffer is back
+          GpuWave::sync();
+          if (nx < count) stage_dma(p.img, p.len, gw + nx * nw, ring_lds + slot * kBuf, lane);
+        });
+    write_region_wave(sump, r, wl->rs, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
     wp.stamp(7);
   }
 #ifdef LDB_STAMPS
   if (lane == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&g_stamps[k], (unsigned long long)wp.acc[k]);
+    for (int k = 0; k < kStampSlots; ++k) atomicAdd((unsigned long long*)&g_stamps[k], (unsigned long long)wp.acc[k]);
 #endif
 }
 
@@ -274,11 +324,12 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
     LaneKeep kp;
-    region_process(wp, v, wl->sh, enter, &wl->rs, [&](int) -> LaneKeep& { return kp; },
-                   [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); });
+    region_process(
+        wp, v, wl->sh, enter, &wl->rs, [&](int) -> LaneKeep& { return kp; },
+        [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); }, [] {});
     const RegionSum s = wl->rs;
     if (lane == 0) {
-      write_region(p, r, s);
+      store_region(p, r, s);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -497,12 +548,30 @@ struct ldb_ctx {
   uint32_t* d_xw = nullptr;    // kW + 1
   uint8_t* ws = nullptr;       // workspace
   uint64_t ws_bytes = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  // kernel timing: one event triple per timed launch, recorded without host synchronisation and
+  // resolved when the timing is queried (or when the pool is full)
+  struct EvTriple { hipEvent_t e0, e1, e2; };
+  std::vector<EvTriple> evs;
+  size_t ev_used = 0;
   bool timing = false;
   double t_main = 0, t_total = 0;
   uint64_t t_n = 0;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
 };
+
+static int resolve_timing(ldb_ctx* c) {
+  for (size_t i = 0; i < c->ev_used; ++i) {
+    const ldb_ctx::EvTriple& t = c->evs[i];
+    if (hipEventSynchronize(t.e2) != hipSuccess) return LDB_ERR_HIP;
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, t.e0, t.e1) != hipSuccess || hipEventElapsedTime(&b, t.e0, t.e2) != hipSuccess)
+      return LDB_ERR_HIP;
+    c->t_main += a;
+    c->t_total += b;
+    c->t_n += 1;
+  }
+  c->ev_used = 0;
+  return LDB_OK;
+}
 
 namespace {
 
@@ -598,19 +667,33 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   int rc = ensure_ws(c, L.total);
   if (rc != LDB_OK) return rc;
   const Pipe p = make_pipe(c, L, d_img, len, fid, io, kind, d_out, cap, d_res);
-  // control words: ctr = 0, tpos = ~0, blk = 0
-  LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 16, s));
-  LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
-  LDB_HIP(hipMemsetAsync(c->ws + L.o_blk, 0, 8 * L.nblk, s));
   if (serial || len < (uint64_t)kMaxHeader) {
+    // control words for k_serial (the parallel pipeline has k_scan_main initialise them)
+    LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 16, s));
+    LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 0);
     return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
   }
-  const bool tm = c->timing;
-  if (tm) LDB_HIP(hipEventRecord(c->ev0, s));
+  const ldb_ctx::EvTriple* ev = nullptr;
+  if (c->timing) {
+    if (c->ev_used == c->evs.size()) {
+      if (c->evs.size() < 4096) {
+        ldb_ctx::EvTriple t{};
+        LDB_HIP(hipEventCreate(&t.e0));
+        LDB_HIP(hipEventCreate(&t.e1));
+        LDB_HIP(hipEventCreate(&t.e2));
+        c->evs.push_back(t);
+      } else {
+        const int rc = resolve_timing(c);
+        if (rc != LDB_OK) return rc;
+      }
+    }
+    ev = &c->evs[c->ev_used++];
+    LDB_HIP(hipEventRecord(ev->e0, s));
+  }
   const int grid = (int)std::min<uint64_t>((L.nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * 2);
   hipLaunchKernelGGL(k_scan_main, dim3(grid), dim3(64 * kWPB), main_lds_bytes(), s, p);
-  if (tm) LDB_HIP(hipEventRecord(c->ev1, s));
+  if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   const int g256 = (int)((L.nreg + 255) / 256);
   hipLaunchKernelGGL(k_link, dim3(g256), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_repair, dim3(1), dim3(64), repair_lds_bytes(), s, p);
@@ -618,17 +701,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   hipLaunchKernelGGL(k_final, dim3(1), dim3(1024), 0, s, p);
   hipLaunchKernelGGL(k_compact, dim3((unsigned)L.nblk), dim3(1024), 0, s, p);
   hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 1);
-  if (tm) {
-    LDB_HIP(hipEventRecord(c->ev2, s));
-    // accumulate when the events complete (synchronously here: timing mode is for benchmarks)
-    LDB_HIP(hipEventSynchronize(c->ev2));
-    float a = 0, b = 0;
-    LDB_HIP(hipEventElapsedTime(&a, c->ev0, c->ev1));
-    LDB_HIP(hipEventElapsedTime(&b, c->ev0, c->ev2));
-    c->t_main += a;
-    c->t_total += b;
-    c->t_n += 1;
-  }
+  if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
 }
 
@@ -684,9 +757,6 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }
-  (void)hipEventCreate(&c->ev0);
-  (void)hipEventCreate(&c->ev1);
-  (void)hipEventCreate(&c->ev2);
   *out = c;
   return LDB_OK;
 }
@@ -697,9 +767,11 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->d_xw) (void)hipFree(c->d_xw);
   if (c->ws) (void)hipFree(c->ws);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  for (const ldb_ctx::EvTriple& t : c->evs) {
+    (void)hipEventDestroy(t.e0);
+    (void)hipEventDestroy(t.e1);
+    (void)hipEventDestroy(t.e2);
+  }
   delete c;
   return LDB_OK;
 }
@@ -775,11 +847,11 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
 }
 
 #ifdef LDB_STAMPS
-int ldb_debug_stamps(uint64_t* out8, int reset) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), 64) != hipSuccess) return LDB_ERR_HIP;
+int ldb_debug_stamps(uint64_t* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 8 * kStampSlots) != hipSuccess) return LDB_ERR_HIP;
   if (reset) {
-    uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 64) != hipSuccess) return LDB_ERR_HIP;
+    uint64_t z[kStampSlots] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 8 * kStampSlots) != hipSuccess) return LDB_ERR_HIP;
   }
   return LDB_OK;
 }
@@ -787,6 +859,9 @@ int ldb_debug_stamps(uint64_t* out8, int reset) {
 
 int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n) {
   if (!c) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  const int rc = resolve_timing(c);
+  if (rc != LDB_OK) return rc;
   if (avg_main_ms) *avg_main_ms = c->t_n ? c->t_main / c->t_n : 0.0;
   if (avg_total_ms) *avg_total_ms = c->t_n ? c->t_total / c->t_n : 0.0;
   if (n) *n = c->t_n;

@@ -16,10 +16,35 @@
 
 using namespace ldb;
 
+#ifdef LDB_EMU_COUNTERS
+namespace ldb { int g_emu_lane; uint32_t g_emu_cnt[8][64]; }
+static uint64_t g_sum[8], g_max[8], g_regions;
+extern "C" void emu_counters(uint64_t* out) {   // [0..7] sums over lanes, [8..15] sums of per-region lane maxima, [16] regions
+  for (int i = 0; i < 8; ++i) { out[i] = g_sum[i]; out[8 + i] = g_max[i]; g_sum[i] = g_max[i] = 0; }
+  out[16] = g_regions; g_regions = 0;
+}
+static void fold_counters() {
+  for (int i = 0; i < 8; ++i) {
+    uint32_t mx = 0;
+    for (int l = 0; l < 64; ++l) {
+      const uint32_t c = ldb::g_emu_cnt[i][l];
+      g_sum[i] += c; mx = c > mx ? c : mx; ldb::g_emu_cnt[i][l] = 0;
+    }
+    g_max[i] += mx;
+  }
+  ++g_regions;
+}
+#define EMU_SET_LANE(l) (ldb::g_emu_lane = (l))
+#define EMU_FOLD() fold_counters()
+#else
+#define EMU_SET_LANE(l) ((void)0)
+#define EMU_FOLD() ((void)0)
+#endif
+
 namespace {
 
 struct CpuWave {
-  template <class F> void each(F f) { for (int l = 0; l < kLanes; ++l) f(l); }
+  template <class F> void each(F f) { for (int l = 0; l < kLanes; ++l) { EMU_SET_LANE(l); f(l); } }
   template <class P> uint64_t ballot(P p) {
     uint64_t b = 0;
     for (int l = 0; l < kLanes; ++l)
@@ -85,8 +110,9 @@ struct Emu {
       sc[slot].pos = pos;
       sc[slot].k_size = k;
       sc[slot].v_size = vv;
-    });
+    }, [] {});
     store_region(p, r, s);
+    EMU_FOLD();
     return s;
   }
 };

@@ -1,0 +1,50 @@
+"""Summarise a tools/profile.sh output directory: kernel-trace stats + per-dispatch PMC averages.
+
+FETCH_SIZE is doubled (gfx950 reports half the bytes of wide coalesced streaming reads,
+MI355X_MICROARCH.md "HBM"); SQ_*CYCLES count quad-cycles.
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    for k in ("k_scan_main", "k_link", "k_repair", "k_combine", "k_final", "k_compact", "k_serial"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+def main(d: str) -> None:
+    for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_stats.csv"), recursive=True):
+        print(f"== kernel stats ({os.path.relpath(f, d)})")
+        with open(f) as fh:
+            rows = list(csv.DictReader(fh))
+        for r in rows:
+            print(f"{short(r['Name']):14s} calls={r['Calls']:>6s} avg_ms={float(r['AverageNs']) / 1e6:9.4f} "
+                  f"min_ms={float(r['MinNs']) / 1e6:9.4f} max_ms={float(r['MaxNs']) / 1e6:9.4f} pct={float(r['Percentage']):6.2f}")
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                key = (r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id"), r["Counter_Name"])
+                acc[short(r["Kernel_Name"])][key].append(float(r["Counter_Value"]))
+    for k, m in acc.items():
+        per = defaultdict(list)
+        for (disp, cname), vals in m.items():
+            per[cname].append(sum(vals))
+        print(f"== PMC {k} (per dispatch averages over {max(len(v) for v in per.values())} dispatches)")
+        for cname in sorted(per):
+            v = sum(per[cname]) / len(per[cname])
+            extra = ""
+            if cname == "FETCH_SIZE":
+                extra = f"  -> corrected x2 = {2 * v * 1024 / 1e6:.1f} MB (FETCH_SIZE unit KiB)"
+            if cname == "WRITE_SIZE":
+                extra = f"  -> {v * 1024 / 1e6:.1f} MB"
+            print(f"  {cname:24s} {v:16.1f}{extra}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

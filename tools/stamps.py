@@ -16,14 +16,14 @@ d = torch.from_numpy(img).cuda()
 res, tup = eng.scan_dev(d)
 L = N.lib()
 L.ldb_debug_stamps.argtypes = [C.c_void_p, C.c_int]
-buf = np.zeros(8, np.uint64)
+buf = np.zeros(10, np.uint64)
 L.ldb_debug_stamps(buf.ctypes.data, 1)
 for _ in range(3):
     eng.scan_dev(d)
 L.ldb_debug_stamps(buf.ctypes.data, 1)
-names = ["setup", "lane_process#1", "consistency+repair", "folds", "summary", "emit", "dma_wait", "tail"]
+names = ["setup", "walk#1", "link+repair", "folds", "summary", "emit", "dma_wait", "tail", "crc_pass", "-"]
 nreg = (img.size + 5119) // 5120
 tot = buf.sum()
-for k in range(8):
+for k in range(9):
     print(f"{names[k]:20s} {buf[k] / (3 * nreg):10.0f} cyc/region  {100 * buf[k] / tot:5.1f}%")
 print("status", res.status, "repairs", res.n_repairs)
