@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--gather", type=int, default=1)
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
+    ap.add_argument("--e2e", type=int, default=3, help="iterations of the PCIe-inclusive host-API leg (0: skip)")
     return ap.parse_args()
 
 
@@ -86,6 +87,22 @@ def cpu_baseline(img, end, sample_mib: int):
             "mentries_per_s": round(r.n_entries / dt / 1e6, 3),
             "optimized_mmap_port_gibs": round(r2.end_off / dt2 / 2**30, 3),
             "host_cpu": _cpu_model(), "host_nproc": os.cpu_count()}
+
+
+def _pmc_traffic(args):
+    """HBM read bytes per k_scan_main launch from the committed rocprofv3 PMC pass of this
+    workload (tools/profile.sh -> profiles/<round>_pmc_cfg<N>.json: FETCH_SIZE x 2, the gfx950
+    correction for wide streaming reads). PMC counters cannot be read inside this process."""
+    import glob
+    if args.io != 0 or args.kind != 0:
+        return None, None
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_cfg{args.config}.json")))
+    if not cands:
+        return None, None
+    with open(cands[-1]) as f:
+        pmc = json.load(f)
+    v = pmc.get("k_scan_main", {}).get("hbm_read_bytes_per_launch")
+    return (int(v) if v else None), os.path.relpath(cands[-1], ROOT)
 
 
 def _cpu_model():
@@ -161,36 +178,37 @@ def main():
 
     bytes_scanned = int(r.end_off)
     entries = int(r.n_entries)
-    t_t = torch.tensor([t], dtype=torch.float64, device=dev)
-    b_t = torch.tensor([bytes_scanned, entries], dtype=torch.float64, device=dev)
+    from lazydb_amd import multi
+    t_max = multi.max_over_ranks(t, dev)
+    tot_bytes, tot_entries = multi.sum_over_ranks([bytes_scanned, entries], dev)
     gather = None
-    if world > 1:
-        dist.all_reduce(t_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(b_t, op=dist.ReduceOp.SUM)
-        if args.gather:
-            # one RCCL gather of every rank's index tuples to rank 0 (padded to the largest count)
-            nbytes = torch.tensor([entries * 16], dtype=torch.int64, device=dev)
-            all_n = [torch.zeros_like(nbytes) for _ in range(world)]
-            dist.all_gather(all_n, nbytes)
-            mx = int(max(x.item() for x in all_n))
-            send = torch.zeros(mx, dtype=torch.uint8, device=dev)
-            send[: entries * 16] = out[: entries * 16]
-            bufs = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
-            torch.cuda.synchronize()
-            dist.barrier()
-            g0 = time.perf_counter()
-            dist.gather(send, bufs, dst=0)
-            torch.cuda.synchronize()
-            gt = time.perf_counter() - g0
-            gt_t = torch.tensor([gt], dtype=torch.float64, device=dev)
-            dist.all_reduce(gt_t, op=dist.ReduceOp.MAX)
-            tot = sum(int(x.item()) for x in all_n)
-            gather = {"bytes_to_rank0": tot, "ms": round(gt_t.item() * 1e3, 3),
-                      "GB_per_s": round(tot / gt_t.item() / 1e9, 2)}
-    t_max = t_t.item()
-    tot_bytes, tot_entries = b_t.tolist()
+    if world > 1 and args.gather:
+        # the north star's single exchange: every rank's index tuples to rank 0 over RCCL/xGMI
+        mine = out[: entries * (16 if args.kind == 0 else 48)]
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        got = multi.gather_tuples(mine)
+        torch.cuda.synchronize()
+        gt = multi.max_over_ranks(time.perf_counter() - g0, dev)
+        if rank == 0:
+            tot = sum(int(x.numel()) for x in got)
+            gather = {"bytes_to_rank0": tot, "ms": round(gt * 1e3, 3), "GB_per_s": round(tot / gt / 1e9, 2)}
+    e2e = None
+    if world == 1 and args.e2e > 0:
+        # PCIe-inclusive rate of the host-pointer API (ldb_scan_file: H2D of the image from pageable
+        # host memory, scan, D2H of the tuples) -- recorded for DESIGN.md, never the bench value
+        res_h, _ = eng.scan_host(img, fid=1, io_type=args.io, kind=args.kind, cap=cap)
+        t0e = time.perf_counter()
+        for _ in range(args.e2e):
+            res_h, _ = eng.scan_host(img, fid=1, io_type=args.io, kind=args.kind, cap=cap)
+        te = (time.perf_counter() - t0e) / args.e2e
+        e2e = {"GiB_per_s": round(int(res_h.end_off) / te / 2**30, 3), "ms": round(te * 1e3, 2),
+               "path": "ldb_scan_file: pageable host image -> H2D -> scan -> D2H tuples",
+               "status_matches": int(res_h.status) == int(r.status) and int(res_h.n_entries) == entries}
     ms_step = t_max / args.steps * 1e3
     value = tot_bytes / (t_max / args.steps) / 2**30
+    traffic, traffic_src = _pmc_traffic(args)
     if rank == 0:
         achieved = bytes_scanned / (main_ms * 1e-3) / 1e9 if main_ms > 0 else None
         line = {
@@ -219,7 +237,8 @@ def main():
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_kernel_ms": round(main_ms, 4),
                 "avg_pipeline_ms": round(total_ms, 4),
                 "algorithmic_bytes_per_launch": bytes_scanned,
@@ -230,6 +249,8 @@ def main():
         }
         if gather:
             line["gather"] = gather
+        if e2e:
+            line["e2e_host"] = e2e
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(img, end_expect, args.cpu_sample_mib)
         print(json.dumps(line))

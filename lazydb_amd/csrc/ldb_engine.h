@@ -528,17 +528,27 @@ LDB_HD void lane_crc(const View& v, int lane, LaneState* a, uint32_t C, uint32_t
   a->rout = open ? rb ^ v.tab[kKOff + (kS - uB)] : 0u;
 }
 
-// ---------------------------------------------------------------- wave-level state (LDS)
-struct WaveSh {
-  LaneState ln[kLanes];
-  uint32_t force[kLanes];
-  uint32_t prefix[kLanes];   // exclusive prefix of emitted tuples per lane
+// ---------------------------------------------------------------- wave-level state
+// Per-lane private state (registers on the GPU; one element per lane in the emulator).
+struct LanePriv {
+  LaneState ln;
+  LaneKeep kp;
+  uint32_t force;
+  uint32_t prefix;   // exclusive prefix of emitted tuples
 };
 
-// Link check for lane j (phase after lane_process): returns the lane to repair and its force,
-// or -1 when lane j's outgoing link is consistent.  `noneMask`: bit k set iff lane k has no start.
-LDB_HD int lane_link(const View& v, const WaveSh& w, int j, uint64_t noneMask, uint32_t* fix_force) {
-  const LaneState& a = w.ln[j];
+// The only per-lane values other lanes read (LDS): 1 KiB per wavefront.
+struct WaveSh {
+  uint32_t s[kLanes];      // first entry start (link checks)
+  uint32_t raw[kLanes];    // lane_crc chain A (fold chains, landing checks)
+  uint32_t want[kLanes];   // ~stored crc of the lane's straddling entry (the next start lane injects it)
+  uint32_t fl[kLanes];     // its sflag
+};
+
+// Link check for lane j (own state a): returns the lane to repair and its force, or -1 when
+// lane j's outgoing link is consistent. `noneMask`: bit k set iff lane k has no start.
+LDB_HD int lane_link(const View& v, const WaveSh& w, const LaneState& a, int j, uint64_t noneMask,
+                     uint32_t* fix_force) {
   if (a.s == kNone32 || a.term != kCont) return -1;
   const uint64_t xr = a.x - v.R0;           // region-relative exit (>= E_j)
   // lanes strictly between j and the landing lane must be covered
@@ -546,7 +556,7 @@ LDB_HD int lane_link(const View& v, const WaveSh& w, int j, uint64_t noneMask, u
   const uint64_t between = (m >= kLanes ? ~0ull : ((1ull << m) - 1)) & ~((2ull << j) - 1);
   const uint64_t bad = between & ~noneMask;
   if (bad) { *fix_force = kForceNone; return (int)ctz64(bad); }
-  if (m < kLanes && w.ln[m].s != (uint32_t)xr) { *fix_force = (uint32_t)xr; return m; }
+  if (m < kLanes && w.s[m] != (uint32_t)xr) { *fix_force = (uint32_t)xr; return m; }
   return -1;
 }
 

@@ -77,7 +77,7 @@ struct GpuWave {
     for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o);
     return x;
   }
-  template <class V> __device__ void excl_prefix(V v, uint32_t* out) {
+  template <class V, class O> __device__ void excl_prefix(V v, O out) {
     const uint32_t mine = v(lane);
     uint32_t x = mine;
 #pragma unroll
@@ -85,8 +85,17 @@ struct GpuWave {
       const uint32_t y = __shfl_up(x, o);
       if (lane >= o) x += y;
     }
-    out[lane] = x - mine;
-    sync();
+    out(lane, x - mine);
+  }
+  // f(l) of the wave-uniform lane `src`, broadcast (v_readlane); uniform control flow only
+  template <class F> __device__ uint32_t from(int src, F f) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)f(lane), src);
+  }
+  template <class F> __device__ uint64_t from64(int src, F f) {
+    const uint64_t x = f(lane);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), src);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
   }
   template <class F> __device__ void single(F f) {
     if (lane == 0) f();
@@ -146,8 +155,10 @@ __device__ __forceinline__ void store_tuple(ldb_index_tuple* dst, uint64_t pos, 
 
 __device__ __forceinline__ uint64_t sgpr64(const void* ptr) {
   const uint64_t x = (uint64_t)(uintptr_t)ptr;
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+  // readfirstlane returns int: widen through uint32_t (no sign extension of the low half)
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
 // Wave-uniform SoA base addresses held in SGPRs (read once per kernel).
@@ -232,9 +243,9 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     v.len = p.len;
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    LaneKeep kp;
+    LanePriv q;
     region_process(
-        wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LaneKeep& { return kp; },
+        wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LanePriv& { return q; },
         [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot_, pos, k, vv); },
         [&] {
           const uint64_t nx = i + kNB;
@@ -323,9 +334,9 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
     v.len = p.len;
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    LaneKeep kp;
+    LanePriv q;
     region_process(
-        wp, v, wl->sh, enter, &wl->rs, [&](int) -> LaneKeep& { return kp; },
+        wp, v, wl->sh, enter, &wl->rs, [&](int) -> LanePriv& { return q; },
         [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); }, [] {});
     const RegionSum s = wl->rs;
     if (lane == 0) {
@@ -554,6 +565,13 @@ struct ldb_ctx {
   std::vector<EvTriple> evs;
   size_t ev_used = 0;
   bool timing = false;
+  // host-pointer API staging (ldb_scan_file), grow-only
+  uint8_t* h_img = nullptr;
+  uint64_t h_img_cap = 0;
+  void* h_out = nullptr;
+  uint64_t h_out_cap = 0;
+  ldb_scan_result* h_res = nullptr;
+  hipStream_t h_stream = nullptr;
   double t_main = 0, t_total = 0;
   uint64_t t_n = 0;
 };
@@ -615,6 +633,10 @@ WsLayout layout(uint64_t len) {
 int ensure_ws(ldb_ctx* c, uint64_t bytes) {
   if (c->ws_bytes >= bytes) return LDB_OK;
   if (c->ws) (void)hipFree(c->ws);
+  if (c->h_img) (void)hipFree(c->h_img);
+  if (c->h_out) (void)hipFree(c->h_out);
+  if (c->h_res) (void)hipFree(c->h_res);
+  if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
   c->ws = nullptr;
   c->ws_bytes = 0;
   if (hipMalloc(&c->ws, bytes) != hipSuccess) return LDB_ERR_NOMEM;
@@ -767,6 +789,10 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->d_xw) (void)hipFree(c->d_xw);
   if (c->ws) (void)hipFree(c->ws);
+  if (c->h_img) (void)hipFree(c->h_img);
+  if (c->h_out) (void)hipFree(c->h_out);
+  if (c->h_res) (void)hipFree(c->h_res);
+  if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
   for (const ldb_ctx::EvTriple& t : c->evs) {
     (void)hipEventDestroy(t.e0);
     (void)hipEventDestroy(t.e1);
@@ -817,33 +843,40 @@ int ldb_scan_files_dev(ldb_ctx* c, int n_files, const uint8_t* const* d_images, 
 int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
                   void* h_out, uint64_t cap, ldb_scan_result* h_result) {
   if (!c || !h_result || (len && !h_image) || (cap && !h_out)) return LDB_ERR_ARG;
+  if (tuple_kind != LDB_TUPLE_INDEX && tuple_kind != LDB_TUPLE_ENTRY) return LDB_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
   const size_t tsz = tuple_kind == LDB_TUPLE_ENTRY ? sizeof(ldb_entry) : sizeof(ldb_index_tuple);
-  uint8_t* d_img = nullptr;
-  void* d_out = nullptr;
-  ldb_scan_result* d_res = nullptr;
-  int rc = LDB_OK;
-  hipStream_t s = nullptr;
-  if (hipStreamCreate(&s) != hipSuccess) return LDB_ERR_HIP;
-  if (hipMalloc(&d_img, len ? len : 16) != hipSuccess || hipMalloc(&d_res, sizeof(ldb_scan_result)) != hipSuccess ||
-      (cap && hipMalloc(&d_out, cap * tsz) != hipSuccess)) {
-    rc = LDB_ERR_NOMEM;
+  // context-owned staging (grow-only): image, tuples, result; one stream per context
+  if (!c->h_stream && hipStreamCreateWithFlags(&c->h_stream, hipStreamNonBlocking) != hipSuccess) return LDB_ERR_HIP;
+  const uint64_t img_need = (len + 15) & ~15ull, out_need = cap * tsz;
+  if (img_need > c->h_img_cap || !c->h_img) {
+    if (c->h_img) (void)hipFree(c->h_img);
+    c->h_img = nullptr;
+    c->h_img_cap = 0;
+    if (hipMalloc(&c->h_img, img_need ? img_need : 16) != hipSuccess) return LDB_ERR_NOMEM;
+    c->h_img_cap = img_need;
   }
-  if (rc == LDB_OK && len && hipMemcpyAsync(d_img, h_image, len, hipMemcpyHostToDevice, s) != hipSuccess) rc = LDB_ERR_HIP;
-  if (rc == LDB_OK) rc = enqueue_scan(c, d_img, len, fid, io_type, tuple_kind, d_out, cap, d_res, s, false);
+  if (out_need > c->h_out_cap || !c->h_out) {
+    if (c->h_out) (void)hipFree(c->h_out);
+    c->h_out = nullptr;
+    c->h_out_cap = 0;
+    if (hipMalloc(&c->h_out, out_need ? out_need : 16) != hipSuccess) return LDB_ERR_NOMEM;
+    c->h_out_cap = out_need;
+  }
+  if (!c->h_res && hipMalloc(&c->h_res, sizeof(ldb_scan_result)) != hipSuccess) return LDB_ERR_NOMEM;
+  hipStream_t s = c->h_stream;
+  // Host buffers are caller-owned pageable memory (a Go slice / mmap): only synchronous copies
+  // touch them, so no runtime staging work can outlive this call.
+  if (len && hipMemcpy(c->h_img, h_image, len, hipMemcpyHostToDevice) != hipSuccess) return LDB_ERR_HIP;
+  int rc = enqueue_scan(c, c->h_img, len, fid, io_type, tuple_kind, c->h_out, cap, c->h_res, s, false);
+  if (rc != LDB_OK) return rc;
+  if (hipStreamSynchronize(s) != hipSuccess) return LDB_ERR_HIP;
   ldb_scan_result res;
-  if (rc == LDB_OK && hipMemcpyAsync(&res, d_res, sizeof(res), hipMemcpyDeviceToHost, s) != hipSuccess) rc = LDB_ERR_HIP;
-  if (rc == LDB_OK && hipStreamSynchronize(s) != hipSuccess) rc = LDB_ERR_HIP;
-  if (rc == LDB_OK) {
-    const uint64_t n = std::min<uint64_t>(res.n_entries, cap);
-    if (n && hipMemcpy(h_out, d_out, n * tsz, hipMemcpyDeviceToHost) != hipSuccess) rc = LDB_ERR_HIP;
-    *h_result = res;
-  }
-  if (d_img) (void)hipFree(d_img);
-  if (d_out) (void)hipFree(d_out);
-  if (d_res) (void)hipFree(d_res);
-  (void)hipStreamDestroy(s);
-  return rc;
+  if (hipMemcpy(&res, c->h_res, sizeof(res), hipMemcpyDeviceToHost) != hipSuccess) return LDB_ERR_HIP;
+  const uint64_t n = std::min<uint64_t>(res.n_entries, cap);
+  if (n && hipMemcpy(h_out, c->h_out, n * tsz, hipMemcpyDeviceToHost) != hipSuccess) return LDB_ERR_HIP;
+  *h_result = res;
+  return LDB_OK;
 }
 
 #ifdef LDB_STAMPS

@@ -27,7 +27,7 @@ struct RegionSum {
 // absorbed). Constant-distance shifts only (shift_slice).
 LDB_HD uint32_t carry_full(const View& v, const WaveSh& sh, uint32_t reg, int k0, int X, int* kend) {
   int k = k0;
-  for (; k < kLanes && (k + 1) * kS <= X; ++k) reg = shift_slice(v.tab, reg) ^ sh.ln[k].raw;
+  for (; k < kLanes && (k + 1) * kS <= X; ++k) reg = shift_slice(v.tab, reg) ^ sh.raw[k];
   *kend = k;
   return reg;
 }
@@ -36,16 +36,16 @@ LDB_HD uint32_t carry_full(const View& v, const WaveSh& sh, uint32_t reg, int k0
 LDB_HD uint32_t carry_tail(const View& v, const WaveSh& sh, uint32_t reg, int k, int X) {
   const int n = X - k * kS;
   if (n <= 0 || k >= kLanes) return reg;
-  return multmodp(v.xw[n], reg) ^ sh.ln[k].raw;
+  return multmodp(v.xw[n], reg) ^ sh.raw[k];
 }
 
 // enter: kForceSpec (speculate), kForceNone (region covered by an earlier entry), or the
 // region-relative position where the verified chain enters this region.
-// keep(l): lane l's private LaneKeep (a register struct on the GPU).
+// priv(l): lane l's private state (registers on the GPU).
 // emit(slot, pos, k, v): tuple `slot` (0-based within the region) in file order.
 // buffer_free(): called once every lane is done reading v.buf (before the summary is written).
-template <class WP, class Keep, class Emit, class Free>
-LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, RegionSum* out, Keep keep,
+template <class WP, class Priv, class Emit, class Free>
+LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, RegionSum* out, Priv priv,
                            Emit emit, Free buffer_free) {
   int lt = -1;
   if (enter != kForceSpec && enter != kForceNone) lt = enter < v.rlen ? (int)(enter / kS) : kLanes;
@@ -54,7 +54,7 @@ LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, Re
     if (enter == kForceSpec) f = kForceSpec;
     else if (enter == kForceNone) f = kForceNone;
     else f = l < lt ? kForceNone : (l == lt ? enter : kForceSpec);
-    sh.force[l] = f;
+    priv(l).force = f;
   });
   wp.stamp(0);
   // ---- speculative lane walks + link verification / repair
@@ -63,16 +63,21 @@ LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, Re
   bool overflow = false;
   for (;;) {
     wp.each([&](int l) {
-      if ((todo >> l) & 1) lane_walk(v, l, sh.force[l], &sh.ln[l], &keep(l));
+      LanePriv& q = priv(l);
+      if ((todo >> l) & 1) {
+        lane_walk(v, l, q.force, &q.ln, &q.kp);
+        sh.s[l] = q.ln.s;
+      }
     });
     wp.stamp(iter == 0 ? 1 : 2);
-    const uint64_t none = wp.ballot([&](int l) { return sh.ln[l].s == kNone32; });
+    const uint64_t none = wp.ballot([&](int l) { return priv(l).ln.s == kNone32; });
     int fixl = -1;
     uint32_t fixf = 0;
     if (enter != kForceSpec) {  // lanes before the entry lane covered, entry lane starts at `enter`
       const int e = wp.first([&](int l) {
-        if (enter == kForceNone || l < lt) return sh.ln[l].s != kNone32;
-        return l == lt && sh.ln[l].s != enter;
+        const uint32_t s = priv(l).ln.s;
+        if (enter == kForceNone || l < lt) return s != kNone32;
+        return l == lt && s != enter;
       });
       if (e >= 0) {
         fixl = e;
@@ -80,42 +85,52 @@ LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, Re
       }
     }
     if (fixl < 0) {
-      const int tl = wp.first([&](int l) { return sh.ln[l].s != kNone32 && sh.ln[l].term != kCont; });
+      const int tl = wp.first([&](int l) { return priv(l).ln.s != kNone32 && priv(l).ln.term != kCont; });
       const int lim = tl < 0 ? kLanes - 1 : tl;
       const int j = wp.first([&](int l) {
         uint32_t f;
-        return l <= lim && lane_link(v, sh, l, none, &f) >= 0;
+        return l <= lim && lane_link(v, sh, priv(l).ln, l, none, &f) >= 0;
       });
       if (j >= 0) {
-        uint32_t f = 0;
-        fixl = lane_link(v, sh, j, none, &f);
-        fixf = f;
+        const uint64_t fx = wp.from64(j, [&](int l) {
+          uint32_t f = 0;
+          const int m = lane_link(v, sh, priv(l).ln, l, none, &f);
+          return ((uint64_t)(uint32_t)m << 32) | f;
+        });
+        fixl = (int)(fx >> 32);
+        fixf = (uint32_t)fx;
       }
     }
     if (fixl < 0) break;
     if (++iter > 4 * kLanes) { overflow = true; break; }
-    wp.single([&] { sh.force[fixl] = fixf; });
+    wp.each([&](int l) { if (l == fixl) priv(l).force = fixf; });
     todo = 1ull << fixl;
   }
   wp.stamp(2);
-  int tl = wp.first([&](int l) { return sh.ln[l].s != kNone32 && sh.ln[l].term != kCont; });
+  int tl = wp.first([&](int l) { return priv(l).ln.s != kNone32 && priv(l).ln.term != kCont; });
   int lim = tl < 0 ? kLanes - 1 : tl;
-  const int L0 = wp.first([&](int l) { return sh.ln[l].s != kNone32; });
-  const uint64_t starts = wp.ballot([&](int l) { return l <= lim && sh.ln[l].s != kNone32; });
+  const int L0 = wp.first([&](int l) { return priv(l).ln.s != kNone32; });
+  const uint64_t starts = wp.ballot([&](int l) { return l <= lim && priv(l).ln.s != kNone32; });
+  wp.each([&](int l) {
+    const LaneState& a = priv(l).ln;
+    sh.want[l] = ~a.scrc;
+    sh.fl[l] = a.sflag;
+  });
   // ---- CRC pieces: one uniform two-chain pass per lane. A start lane whose prefix belongs to an
   // entry started earlier in the region (its "owner") injects the owner's expected final register
   // at [s, s+4), so the owner's check at the fold becomes shift_slice(I_B) == raw (no variable shifts).
   wp.each([&](int l) {
-    LaneState& a = sh.ln[l];
+    LaneState& a = priv(l).ln;
     uint32_t C = 0, inj = 0;
     const uint64_t below = starts & ((1ull << l) - 1);
     if (l <= lim && a.s != kNone32 && below) {
       const int j = 63 - (int)__builtin_clzll(below);
-      const LaneState& o = sh.ln[j];
-      const bool direct = (o.sflag & kSkip) && (int)a.s <= (j + 2) * kS;   // owner verified directly below
-      if ((o.sflag & kStraddle) && !(o.sflag & kNoCrc) && !direct) { C = ~o.scrc; inj = 1; }
+      const uint32_t ofl = sh.fl[j];
+      const bool direct = (ofl & kSkip) && (int)a.s <= (j + 2) * kS;   // owner verified directly below
+      if ((ofl & kStraddle) && !(ofl & kNoCrc) && !direct) { C = sh.want[j]; inj = 1; }
     }
     lane_crc(v, l, &a, C, inj);
+    sh.raw[l] = a.raw;
   });
   wp.stamp(8);
   // ---- folds: every entry that leaves its slice carries its CRC register across the covered
@@ -126,13 +141,13 @@ LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, Re
     // delivered shifted to the end of L0's slice (A-form, see combine_region)
     if (l == (L0 < 0 ? 0 : L0)) {
       int kend;
-      const int X = L0 < 0 ? (int)v.rlen : (int)sh.ln[L0].s;
+      const int X = L0 < 0 ? (int)v.rlen : (int)priv(l).ln.s;
       const uint32_t reg = carry_full(v, sh, 0u, 0, X, &kend);
-      region_rpre = L0 < 0 ? carry_tail(v, sh, reg, kend, X) : (shift_slice(v.tab, reg) ^ sh.ln[L0].raw);
+      region_rpre = L0 < 0 ? carry_tail(v, sh, reg, kend, X) : (shift_slice(v.tab, reg) ^ priv(l).ln.raw);
     }
   });
   wp.each([&](int l) {
-    LaneState& a = sh.ln[l];
+    LaneState& a = priv(l).ln;
     if (!(l <= lim && a.s != kNone32 && a.term == kCont && (a.sflag & kStraddle)) || (a.sflag & kNoCrc)) return;
     const uint64_t xr = a.x - v.R0;
     const int X = xr < (uint64_t)kW ? (int)xr : kW;
@@ -167,63 +182,63 @@ LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, Re
     }
     bool ok;
     if (X >= (int)v.rlen) ok = carry_tail(v, sh, reg, kend, X) == want;   // ends exactly at the end of the file
-    else ok = shift_slice(v.tab, reg) == sh.ln[kend].raw;                  // lane kend starts at X, injected want
+    else ok = shift_slice(v.tab, reg) == sh.raw[kend];                    // lane kend starts at X, injected want
     if (!ok) { a.term = LDB_ERR_CRC; a.tpos = a.so; a.cnt -= 1; a.sflag = 0; }
   });
   region_rpre = wp.bcast_or(region_rpre);
   region_rout = wp.bcast_or(region_rout);
   region_sflag_clear = wp.bcast_or(region_sflag_clear);
   wp.stamp(3);
-  tl = wp.first([&](int l) { return sh.ln[l].s != kNone32 && sh.ln[l].term != kCont; });
+  tl = wp.first([&](int l) { return priv(l).ln.s != kNone32 && priv(l).ln.term != kCont; });
   lim = tl < 0 ? kLanes - 1 : tl;
-  const int lz = wp.last([&](int l) { return l <= lim && sh.ln[l].s != kNone32; });
-  wp.excl_prefix([&](int l) { return (l <= lim && sh.ln[l].s != kNone32) ? sh.ln[l].cnt : 0u; }, sh.prefix);
-  const uint32_t total = wp.sum([&](int l) { return (l <= lim && sh.ln[l].s != kNone32) ? sh.ln[l].cnt : 0u; });
+  const int lz = wp.last([&](int l) { return l <= lim && priv(l).ln.s != kNone32; });
+  auto cnt_of = [&](int l) { return (l <= lim && priv(l).ln.s != kNone32) ? priv(l).ln.cnt : 0u; };
+  wp.excl_prefix(cnt_of, [&](int l, uint32_t x) { priv(l).prefix = x; });
+  const uint32_t total = wp.sum(cnt_of);
   if (!overflow && total <= (uint32_t)kRegionCap) {
     wp.each([&](int l) {
-      const LaneState& a = sh.ln[l];
-      if (l <= lim && a.s != kNone32 && a.cnt) {
-        const uint32_t base = sh.prefix[l];
-        lane_emit(v, a, keep(l), [&](uint32_t i, uint64_t pos, uint32_t k, uint32_t vv) { emit(base + i, pos, k, vv); });
+      const LanePriv& q = priv(l);
+      if (l <= lim && q.ln.s != kNone32 && q.ln.cnt) {
+        const uint32_t base = q.prefix;
+        lane_emit(v, q.ln, q.kp, [&](uint32_t i, uint64_t pos, uint32_t k, uint32_t vv) { emit(base + i, pos, k, vv); });
       }
     });
   }
   wp.stamp(5);
   buffer_free();   // last read of the staging buffer is behind us: the caller may refill it
-  wp.single([&] {
-    RegionSum r;
-    r.soff = 0; r.rout = 0; r.scrc = 0; r.sflag = 0; r.count = total; r.exitp = 0;
-    r.rpre = region_rpre;
-    if (L0 < 0) {
-      r.start = kNone64;
-      r.status = kCont;
+  // ---- region summary (wave-uniform values broadcast from the lanes that own them)
+  RegionSum r;
+  r.soff = 0; r.rout = 0; r.scrc = 0; r.sflag = 0; r.count = total; r.exitp = 0;
+  r.rpre = region_rpre;
+  if (L0 < 0) {
+    r.start = kNone64;
+    r.status = kCont;
+  } else {
+    r.start = v.R0 + wp.from(L0, [&](int l) { return priv(l).ln.s; });
+    if (tl >= 0) {
+      r.status = (int32_t)wp.from(tl, [&](int l) { return (uint32_t)priv(l).ln.term; });
+      r.exitp = v.R0 + wp.from(tl, [&](int l) { return priv(l).ln.tpos; });
     } else {
-      r.start = v.R0 + sh.ln[L0].s;
-      if (tl >= 0) {
-        r.status = sh.ln[tl].term;
-        r.exitp = v.R0 + sh.ln[tl].tpos;
-      } else {
-        const LaneState& z = sh.ln[lz];
-        r.status = kCont;
-        r.exitp = z.x;
-        if ((z.sflag & kStraddle) && z.x - v.R0 >= (uint64_t)kW) {
-          r.sflag = z.sflag;
-          r.soff = v.R0 + z.so;
-          r.scrc = z.scrc;
-          if (z.sflag & kNoCrc) {
-            r.rout = 0;
-          } else if ((z.sflag & kSkip) && lz == kLanes - 1) {
-            r.rout = 0;   // span starts at/after the region end - 3: k_combine computes it
-          } else {
-            r.rout = region_rout;
-            if (region_sflag_clear) r.sflag = z.sflag & ~kSkip;
-          }
+      r.status = kCont;
+      r.exitp = wp.from64(lz, [&](int l) { return priv(l).ln.x; });
+      const uint32_t zf = wp.from(lz, [&](int l) { return priv(l).ln.sflag; });
+      if ((zf & kStraddle) && r.exitp - v.R0 >= (uint64_t)kW) {
+        r.sflag = zf;
+        r.soff = v.R0 + wp.from(lz, [&](int l) { return priv(l).ln.so; });
+        r.scrc = wp.from(lz, [&](int l) { return priv(l).ln.scrc; });
+        if (zf & kNoCrc) {
+          r.rout = 0;
+        } else if ((zf & kSkip) && lz == kLanes - 1) {
+          r.rout = 0;   // span starts at/after the region end - 3: k_combine computes it
+        } else {
+          r.rout = region_rout;
+          if (region_sflag_clear) r.sflag = zf & ~kSkip;
         }
       }
     }
-    if (overflow || total > (uint32_t)kRegionCap) r.status = kOverflow;
-    *out = r;
-  });
+  }
+  if (overflow || total > (uint32_t)kRegionCap) r.status = kOverflow;
+  wp.single([&] { *out = r; });
   wp.stamp(4);
 }
 

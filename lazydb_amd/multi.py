@@ -1,0 +1,54 @@
+"""Multi-GPU plumbing for the scan.
+
+Log files are independent (every replay chain starts at offset 0, index.go:68-95), so ranks
+scan disjoint files with no collective on the scan path (weak scaling). The only data exchange
+is the single gather of index tuples to rank 0 — RCCL over xGMI on GPUs (backend "nccl"),
+gloo in the CPU tests — plus scalar reductions of the timing.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def files_for_rank(fids, rank: int, world: int):
+    """Round-robin files by fid; each rank keeps ascending fid order (index.go:103-108 order)."""
+    return sorted(fids)[rank::world]
+
+
+def max_over_ranks(x: float, device) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(xs, device):
+    t = torch.tensor(list(xs), dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0):
+    """Gather every rank's tuple byte buffer (uint8, 1-D, on the rank's device) to `dst`.
+
+    One all_gather of the byte counts, then one gather of buffers padded to the largest count.
+    Returns the list of per-rank buffers (trimmed, rank order) on `dst`, None elsewhere.
+    """
+    assert tuple_bytes.dtype == torch.uint8 and tuple_bytes.dim() == 1
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    dev = tuple_bytes.device
+    n = torch.tensor([tuple_bytes.numel()], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    mx = max(max(counts), 1)
+    send = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    send[: tuple_bytes.numel()] = tuple_bytes
+    bufs = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == dst else None
+    dist.gather(send, bufs, dst=dst)
+    if rank != dst:
+        return None
+    return [b[:c] for b, c in zip(bufs, counts)]

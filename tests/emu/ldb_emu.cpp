@@ -66,10 +66,12 @@ struct CpuWave {
     for (int l = 0; l < kLanes; ++l) s += v(l);
     return s;
   }
-  template <class V> void excl_prefix(V v, uint32_t* out) {
+  template <class V, class O> void excl_prefix(V v, O out) {
     uint32_t s = 0;
-    for (int l = 0; l < kLanes; ++l) { out[l] = s; s += v(l); }
+    for (int l = 0; l < kLanes; ++l) { const uint32_t x = v(l); out(l, s); s += x; }
   }
+  template <class F> uint32_t from(int src, F f) { return (uint32_t)f(src); }
+  template <class F> uint64_t from64(int src, F f) { return (uint64_t)f(src); }
   template <class F> void single(F f) { f(); }
   uint32_t bcast_or(uint32_t x) { return x; }
   void stamp(int) {}
@@ -105,8 +107,8 @@ struct Emu {
     RegionSum s;
     CpuWave wp;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    LaneKeep keep[kLanes];
-    region_process(wp, v, sh, enter, &s, [&](int l) -> LaneKeep& { return keep[l]; }, [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
+    LanePriv priv[kLanes];
+    region_process(wp, v, sh, enter, &s, [&](int l) -> LanePriv& { return priv[l]; }, [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
       sc[slot].pos = pos;
       sc[slot].k_size = k;
       sc[slot].v_size = vv;

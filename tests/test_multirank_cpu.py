@@ -1,0 +1,79 @@
+"""World-size-2 gloo test of the multi-GPU path's host logic (lazydb_amd.multi): one file per
+rank, max-over-ranks timing, summed bytes, and the single tuple gather to rank 0. The per-rank
+scan is the CPU oracle here (this container has no GPU); the GPU run uses the same module with
+backend "nccl" (RCCL) in bench.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lazydb_amd import multi
+        from oracle import coracle
+        fids = multi.files_for_rank(list(range(1, 2 * world + 1)), rank, world)
+        bufs, nbytes, nent = [], 0, 0
+        for fid in fids:
+            img, n, end = coracle.gen_log(1 << 18, 100 + fid, ksize=16, vsize=48)
+            res, tup = coracle.scan(img, 0, fid=fid)
+            bufs.append(np.frombuffer(tup.tobytes(), np.uint8))
+            nbytes += int(res.end_off)
+            nent += int(res.n_entries)
+        mine = torch.from_numpy(np.concatenate(bufs).copy())
+        t = multi.max_over_ranks(0.5 + rank, "cpu")
+        tot = multi.sum_over_ranks([nbytes, nent], "cpu")
+        got = multi.gather_tuples(mine)
+        if rank == 0:
+            q.put((t, tot, [g.numpy().tobytes() for g in got]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gather_matches_per_file_scans():
+    from lazydb_amd import multi
+    from oracle import coracle
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    t, tot, got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert t == pytest.approx(1.5)
+    exp_bytes = exp_ent = 0
+    for r in range(world):
+        exp = b""
+        for fid in multi.files_for_rank(list(range(1, 2 * world + 1)), r, world):
+            img, n, end = coracle.gen_log(1 << 18, 100 + fid, ksize=16, vsize=48)
+            res, tup = coracle.scan(img, 0, fid=fid)
+            exp += tup.tobytes()
+            exp_bytes += int(res.end_off)
+            exp_ent += int(res.n_entries)
+        assert got[r] == exp
+    assert tot == [float(exp_bytes), float(exp_ent)]
+
+
+def test_files_for_rank_round_robin():
+    from lazydb_amd import multi
+    assert multi.files_for_rank([5, 1, 3, 2, 4], 0, 2) == [1, 3, 5]
+    assert multi.files_for_rank([5, 1, 3, 2, 4], 1, 2) == [2, 4]
+    assert multi.files_for_rank([1], 1, 8) == []

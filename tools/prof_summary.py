@@ -5,6 +5,7 @@ MI355X_MICROARCH.md "HBM"); SQ_*CYCLES count quad-cycles.
 """
 import csv
 import glob
+import json
 import os
 import sys
 from collections import defaultdict
@@ -31,6 +32,7 @@ def main(d: str) -> None:
             for r in csv.DictReader(fh):
                 key = (r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id"), r["Counter_Name"])
                 acc[short(r["Kernel_Name"])][key].append(float(r["Counter_Value"]))
+    pmc = {}
     for k, m in acc.items():
         per = defaultdict(list)
         for (disp, cname), vals in m.items():
@@ -44,6 +46,11 @@ def main(d: str) -> None:
             if cname == "WRITE_SIZE":
                 extra = f"  -> {v * 1024 / 1e6:.1f} MB"
             print(f"  {cname:24s} {v:16.1f}{extra}")
+            pmc.setdefault(k, {})[cname] = v
+    if "k_scan_main" in pmc and "FETCH_SIZE" in pmc["k_scan_main"]:
+        pmc["k_scan_main"]["hbm_read_bytes_per_launch"] = pmc["k_scan_main"]["FETCH_SIZE"] * 2 * 1024
+    with open(os.path.join(d, "pmc.json"), "w") as f:
+        json.dump(pmc, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
