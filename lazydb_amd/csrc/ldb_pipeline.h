@@ -23,6 +23,7 @@ struct Pipe {
   uint64_t nreg;
   const uint32_t* gtab;     // kTabWords table block (global copy)
   const uint32_t* xw;       // x^(8n) mod P for n = 0..kW
+  const uint32_t* gsh;      // kGsTables x 1024 register-shift byte tables (build_gshift)
   // SoA region summaries
   uint64_t* start;
   uint64_t* exitp;
@@ -38,15 +39,39 @@ struct Pipe {
   int64_t* fail_src;          // regions whose outgoing link failed (-1: region 0 does not start at 0)
   uint32_t* ctr;              // [0] fail count, [1] overflow, [2] repairs, [3] first terminal region (min)
   uint64_t* tpos;             // [0] min terminal position, [1] its status (packed with position)
-  uint64_t* blk;              // per 1024-region block: [0] count sum
-  uint64_t* blk_prefix;
+  uint64_t* blk;              // per kBlkRegions-region block: count sum (k_combine)
   void* out;
   uint64_t cap;
   int kind;
   ldb_scan_result* result;
 };
 
-constexpr int kBlkRegions = 1024;
+constexpr int kBlkRegions = 256;   // regions per k_combine / k_compact workgroup
+
+// Register-shift byte tables for k_combine (global memory, L2-resident): table t holds
+// T[q * 256 + b] = shift(b << 8q, n_t bytes) = (b << 8q) * x^(8 n_t) mod P, so a shift by n_t is
+// 4 independent lookups instead of a 32-step GF(2) multiply.
+//   t = kGsW            : n = kW           (a whole covered region)
+//   t = kGsE0 + k - 1   : n = kS * k       (k = 1..64: to the end of the landing slice)
+//   t = kGsD + d        : n = d            (d = 0..kS)
+constexpr int kGsW = 0, kGsE0 = 1, kGsD = kGsE0 + kLanes, kGsTables = kGsD + kS + 1;
+constexpr uint64_t kGsWords = (uint64_t)kGsTables * 1024;
+
+inline void build_gshift(uint32_t* g) {
+  auto fill = [&](int t, uint64_t n) {
+    const uint32_t xn = x8n_modp(n);
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b) g[(uint64_t)t * 1024 + q * 256 + b] = multmodp(xn, b << (8 * q));
+  };
+  fill(kGsW, kW);
+  for (int k = 1; k <= kLanes; ++k) fill(kGsE0 + k - 1, (uint64_t)kS * k);
+  for (int d = 0; d <= kS; ++d) fill(kGsD + d, d);
+}
+
+LDB_HD uint32_t gshift(const uint32_t* g, int t, uint32_t r) {
+  const uint32_t* T = g + (uint64_t)t * 1024;
+  return T[r & 0xFFu] ^ T[256 + ((r >> 8) & 0xFFu)] ^ T[512 + ((r >> 16) & 0xFFu)] ^ T[768 + (r >> 24)];
+}
 
 LDB_HD void store_region(const Pipe& p, uint64_t r, const RegionSum& s) {
   p.start[r] = s.start;
@@ -78,12 +103,6 @@ LDB_HD bool link_broken(const Pipe& p, uint64_t r) {
 }
 
 // ---------------------------------------------------------------- CRC helpers (global memory)
-LDB_HD uint32_t g_shift(const Pipe& p, uint32_t reg, uint64_t n) {
-  // n <= kW uses the table; larger n folds whole regions
-  while (n > (uint64_t)kW) { reg = multmodp(p.xw[kW], reg); n -= kW; }
-  return n ? multmodp(p.xw[n], reg) : reg;
-}
-
 // CRC-32 register over image bytes [a, b) from register `reg` (byte at a time; rare paths only).
 LDB_HD uint32_t g_crc_bytes(const Pipe& p, uint32_t reg, uint64_t a, uint64_t b) {
   const uint32_t* t8 = p.gtab + kT8Off;
@@ -114,7 +133,7 @@ LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
     k = r + 1;
   }
   const uint64_t m = end / kW;  // region holding the entry's end (may be == nreg when end == len)
-  for (; k < m; ++k) reg = multmodp(p.xw[kW], reg) ^ p.rpre[k];
+  for (; k < m; ++k) reg = gshift(p.gsh, kGsW, reg) ^ p.rpre[k];
   const uint32_t want = ~p.scrc[r];
   if (m < p.nreg) {
     const uint64_t n = end - m * (uint64_t)kW;
@@ -124,8 +143,9 @@ LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
       } else {
         // rpre[m] = shift(raw([R0, n)), E0 - n), E0 = end of the slice holding n (region_process):
         // reg(n) == want  <=>  shift(reg, E0) ^ rpre[m] == shift(want, E0 - n)
-        const uint64_t E0 = (n / kS + 1) * (uint64_t)kS;
-        return (multmodp(p.xw[E0], reg) ^ p.rpre[m]) == multmodp(p.xw[E0 - n], want);
+        const int k0 = (int)(n / kS) + 1;   // E0 = kS * k0
+        const int d = kS * k0 - (int)n;     // 1..kS
+        return (gshift(p.gsh, kGsE0 + k0 - 1, reg) ^ p.rpre[m]) == gshift(p.gsh, kGsD + d, want);
       }
     }
   }

@@ -33,7 +33,7 @@ using namespace ldb;
 namespace {
 
 #ifndef LDB_WPB
-#define LDB_WPB 12
+#define LDB_WPB 16
 #endif
 #ifndef LDB_NB
 #define LDB_NB 1
@@ -153,38 +153,19 @@ __device__ __forceinline__ void store_tuple(ldb_index_tuple* dst, uint64_t pos, 
   *reinterpret_cast<uint4*>(dst) = t;
 }
 
-__device__ __forceinline__ uint64_t sgpr64(const void* ptr) {
-  const uint64_t x = (uint64_t)(uintptr_t)ptr;
-  // readfirstlane returns int: widen through uint32_t (no sign extension of the low half)
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-
-// Wave-uniform SoA base addresses held in SGPRs (read once per kernel).
-struct SumPtrs {
-  uint64_t start, exitp, soff, status, count, rpre, rout, scrc, sflag;
-  __device__ explicit SumPtrs(const Pipe& p)
-      : start(sgpr64(p.start)), exitp(sgpr64(p.exitp)), soff(sgpr64(p.soff)), status(sgpr64(p.status)),
-        count(sgpr64(p.count)), rpre(sgpr64(p.rpre)), rout(sgpr64(p.rout)), scrc(sgpr64(p.scrc)), sflag(sgpr64(p.sflag)) {}
-};
-
-// Region summary to the SoA arrays as two vector store instructions (lanes 0-2: 64-bit fields,
-// lanes 0-5: 32-bit fields) -- k_scan_main counts them in its vmcnt waits. Bases are selected per
-// lane from SGPRs (integer selects, no vector load: that would cost a vmcnt(0) beside the DMA).
-__device__ __forceinline__ void write_region_wave(const SumPtrs& b, uint64_t r, const RegionSum& s, int lane) {
-  if (lane < 3) {
-    const uint64_t a = lane == 0 ? b.start : (lane == 1 ? b.exitp : b.soff);
-    const uint64_t val = lane == 0 ? s.start : (lane == 1 ? s.exitp : s.soff);
-    reinterpret_cast<uint64_t*>((uintptr_t)a)[r] = val;
-  }
-  if (lane < 6) {
-    const uint64_t a = lane == 0 ? b.status
-                                 : lane == 1 ? b.count : lane == 2 ? b.rpre : lane == 3 ? b.rout : lane == 4 ? b.scrc : b.sflag;
-    const uint32_t val = lane == 0 ? (uint32_t)s.status
-                                   : lane == 1 ? s.count : lane == 2 ? s.rpre : lane == 3 ? s.rout : lane == 4 ? s.scrc : s.sflag;
-    reinterpret_cast<uint32_t*>((uintptr_t)a)[r] = val;
-  }
+// Region summary to the SoA arrays: one single-lane GLOBAL store per field, straight from the
+// kernarg pointers (address space known to the compiler). k_scan_main's vmcnt waits rely on these
+// being global_store (in-order on vmcnt); a flat_store would retire out of order.
+__device__ __forceinline__ void write_region_wave(const Pipe& p, uint64_t r, const RegionSum& s, int lane) {
+  if (lane == 0) p.start[r] = s.start;
+  if (lane == 1) p.exitp[r] = s.exitp;
+  if (lane == 2) p.soff[r] = s.soff;
+  if (lane == 3) p.status[r] = s.status;
+  if (lane == 4) p.count[r] = s.count;
+  if (lane == 5) p.rpre[r] = s.rpre;
+  if (lane == 6) p.rout[r] = s.rout;
+  if (lane == 7) p.scrc[r] = s.scrc;
+  if (lane == 8) p.sflag[r] = s.sflag;
 }
 
 #ifdef LDB_STAMPS
@@ -196,8 +177,6 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
   if (blockIdx.x == 0) {  // control words of the later stages (stream-ordered after this kernel)
-    const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
-    for (uint64_t i = threadIdx.x; i < nblk; i += blockDim.x) p.blk[i] = 0;
     if (threadIdx.x < 4) p.ctr[threadIdx.x] = 0;
     if (threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
   }
@@ -211,7 +190,6 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   const uint64_t gw = (uint64_t)blockIdx.x * kWPB + wave, nw = (uint64_t)gridDim.x * kWPB;
   const uint64_t count = gw < p.nreg ? (p.nreg - gw + nw - 1) / nw : 0;
   GpuWave wp{lane};
-  const SumPtrs sump(p);
   // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
   // has read it for the last time (region_process's buffer_free), so the DMA overlaps the summary,
   // its stores and the next region's wait.
@@ -253,7 +231,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
           GpuWave::sync();
           if (nx < count) stage_dma(p.img, p.len, gw + nx * nw, ring_lds + slot * kBuf, lane);
         });
-    write_region_wave(sump, r, wl->rs, lane);
+    write_region_wave(p, r, wl->rs, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
     wp.stamp(7);
@@ -380,59 +358,7 @@ __global__ __launch_bounds__(256) void k_combine(Pipe p) {
     if (threadIdx.x < o) s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&p.blk[(r / kBlkRegions)], (unsigned long long)s_sum[0]);
-}
-
-// ---------------------------------------------------------------- k_final (1 block)
-// blk_prefix[b] = exclusive prefix of effective counts; blk_prefix[nblk] = regT; result filled.
-__global__ __launch_bounds__(1024) void k_final(Pipe p) {
-  __shared__ uint64_t s_part[1024];
-  __shared__ uint64_t s_base;
-  const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
-  const uint64_t T = p.tpos[0];
-  uint64_t tp = term_pos(T);
-  int32_t ts = term_status(T);
-  if (T == ~0ull) { tp = p.len; ts = LDB_ERR_MALFORMED; }  // unreachable: the chain always stops
-  const uint64_t regT = tp / kW;
-  if (threadIdx.x == 0) {
-    uint64_t acc = 0;
-    for (uint64_t b = 0; b < nblk; ++b) {
-      p.blk_prefix[b] = acc;
-      if ((b + 1) * kBlkRegions <= regT) acc += p.blk[b];
-    }
-    s_base = acc;  // sum of all blocks fully before regT's block
-  }
-  __syncthreads();
-  // partial sum inside regT's block (regions before regT) + regT's effective count
-  const uint64_t b0 = (regT / kBlkRegions) * kBlkRegions;
-  uint64_t part = 0;
-  for (uint64_t r = b0 + threadIdx.x; r < regT && r < p.nreg; r += blockDim.x) part += p.count[r];
-  s_part[threadIdx.x] = part;
-  __syncthreads();
-  for (int o = 512; o; o >>= 1) {
-    if (threadIdx.x < o) s_part[threadIdx.x] += s_part[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    uint64_t eff = 0;
-    if (regT < p.nreg) {
-      eff = p.count[regT];
-      // the terminal is this region's straddle-out entry failing its CRC
-      if (p.status[regT] == kCont && (p.sflag[regT] & kStraddle) && p.soff[regT] == tp && eff > 0) eff -= 1;
-    }
-    const uint64_t n = s_base + s_part[0] + eff;
-    ldb_scan_result res;
-    res.status = ts;
-    res.fid = p.fid;
-    res.n_entries = n;
-    res.end_off = tp;
-    res.n_repairs = p.ctr[2];
-    res.n_regions = (uint32_t)p.nreg;
-    if (n > p.cap) res.status = LDB_ERR_CAPACITY;
-    if (p.ctr[1]) res.status = kOverflow;  // k_serial redoes the scan
-    *p.result = res;
-    p.blk_prefix[nblk] = regT;
-  }
+  if (threadIdx.x == 0) p.blk[blockIdx.x] = s_sum[0];   // blockDim == kBlkRegions
 }
 
 // ---------------------------------------------------------------- k_compact
@@ -460,43 +386,82 @@ __device__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out)
   *out = e;
 }
 
-__global__ __launch_bounds__(1024) void k_compact(Pipe p) {
-  __shared__ uint32_t s_cnt[kBlkRegions];
-  __shared__ uint64_t s_off[kBlkRegions];
-  const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
-  const uint64_t regT = p.blk_prefix[nblk];
-  const uint64_t b = blockIdx.x;
-  const uint64_t r0 = b * kBlkRegions;
-  if (r0 > regT || p.ctr[1]) return;
-  const uint64_t r = r0 + threadIdx.x;
+// One workgroup per kBlkRegions regions: its output base is the sum of the earlier blocks'
+// counts (k_combine), its regions are scanned in LDS, and tuples are copied flat (thread j of
+// the block's output range finds its region by binary search). The block holding the terminal
+// region writes the ldb_scan_result.
+__global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
+  __shared__ uint32_t s_off[kBlkRegions + 1];
+  __shared__ uint32_t s_wsum[kBlkRegions / 64];
+  __shared__ uint64_t s_part[kBlkRegions / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t T = p.tpos[0];
+  uint64_t tp = term_pos(T);
+  int32_t ts = term_status(T);
+  if (T == ~0ull) { tp = p.len; ts = LDB_ERR_MALFORMED; }  // unreachable: the chain always stops
+  const uint64_t regT = tp / kW;                          // may be nreg when tp == len == nreg * kW
+  const uint64_t lastR = regT < p.nreg ? regT : p.nreg - 1;
+  const uint64_t b = blockIdx.x, r0 = b * kBlkRegions;
+  if (r0 > lastR) return;
+  // base = sum of the counts of every earlier block (all their regions precede the terminal)
+  uint64_t part = 0;
+  for (uint64_t i = tid; i < b; i += kBlkRegions) part += p.blk[i];
+#pragma unroll
+  for (int o = 32; o; o >>= 1) part += __shfl_xor(part, o);
+  if (lane == 0) s_part[wave] = part;
+  // this block's effective counts, exclusive scan
+  const uint64_t r = r0 + tid;
   uint32_t c = 0;
   if (r < p.nreg && r <= regT) {
     c = p.count[r];
-    if (r == regT && p.status[r] == kCont && (p.sflag[r] & kStraddle) && p.soff[r] == term_pos(p.tpos[0]) && c > 0)
-      c -= 1;
+    // the terminal is this region's straddle-out entry failing its CRC
+    if (r == regT && p.status[r] == kCont && (p.sflag[r] & kStraddle) && p.soff[r] == tp && c > 0) c -= 1;
   }
-  s_cnt[threadIdx.x] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t acc = p.blk_prefix[b];
-    for (int i = 0; i < kBlkRegions; ++i) { s_off[i] = acc; acc += s_cnt[i]; }
+  uint32_t x = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
+  if (lane == 63) s_wsum[wave] = x;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = wave; i < kBlkRegions; i += 16) {
-    const uint32_t n = s_cnt[i];
-    const uint64_t base = s_off[i];
-    const ldb_index_tuple* src = p.scratch + (r0 + i) * (uint64_t)kRegionCap;
-    for (uint32_t j = lane; j < n; j += 64) {
-      const uint64_t dst = base + j;
-      if (dst >= p.cap) break;
-      const ldb_index_tuple t = src[j];
-      if (p.kind == LDB_TUPLE_ENTRY) {
-        decode_entry_global(p, t.pos & 0xFFFFFFFFFFull, reinterpret_cast<ldb_entry*>(p.out) + dst);
-      } else {
-        reinterpret_cast<ldb_index_tuple*>(p.out)[dst] = t;
-      }
+  uint32_t wbase = 0;
+  uint64_t base = 0;
+#pragma unroll
+  for (int w = 0; w < kBlkRegions / 64; ++w) {
+    wbase += w < wave ? s_wsum[w] : 0u;
+    base += s_part[w];
+  }
+  s_off[tid] = wbase + x - c;
+  if (tid == kBlkRegions - 1) s_off[kBlkRegions] = wbase + x;
+  __syncthreads();
+  const uint32_t total = s_off[kBlkRegions];
+  if (b == lastR / kBlkRegions && tid == 0) {
+    const uint64_t n = base + total;
+    ldb_scan_result res;
+    res.status = ts;
+    res.fid = p.fid;
+    res.n_entries = n;
+    res.end_off = tp;
+    res.n_repairs = p.ctr[2];
+    res.n_regions = (uint32_t)p.nreg;
+    if (n > p.cap) res.status = LDB_ERR_CAPACITY;
+    if (p.ctr[1]) res.status = kOverflow;  // k_serial redoes the scan
+    *p.result = res;
+  }
+  if (p.ctr[1]) return;
+  for (uint32_t j = tid; j < total; j += kBlkRegions) {
+    // region i: the last with s_off[i] <= j (empty regions share their successor's offset)
+    int lo = 0, hi = kBlkRegions - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= j) lo = mid; else hi = mid - 1;
     }
+    const uint64_t dst = base + j;
+    if (dst >= p.cap) break;
+    const ldb_index_tuple t = p.scratch[(r0 + lo) * (uint64_t)kRegionCap + (j - s_off[lo])];
+    if (p.kind == LDB_TUPLE_ENTRY) decode_entry_global(p, t.pos & 0xFFFFFFFFFFull, reinterpret_cast<ldb_entry*>(p.out) + dst);
+    else reinterpret_cast<ldb_index_tuple*>(p.out)[dst] = t;
   }
 }
 
@@ -557,6 +522,7 @@ struct ldb_ctx {
   int n_cu = 256;
   uint32_t* d_tab = nullptr;   // kTabWords
   uint32_t* d_xw = nullptr;    // kW + 1
+  uint32_t* d_gsh = nullptr;   // kGsWords register-shift tables (k_combine)
   uint8_t* ws = nullptr;       // workspace
   uint64_t ws_bytes = 0;
   // kernel timing: one event triple per timed launch, recorded without host synchronisation and
@@ -596,7 +562,7 @@ namespace {
 struct WsLayout {
   uint64_t nreg, nblk;
   uint64_t o_start, o_exitp, o_soff, o_status, o_count, o_rpre, o_rout, o_scrc, o_sflag, o_scratch, o_fail, o_ctr,
-      o_tpos, o_blk, o_blkp, total;
+      o_tpos, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -614,7 +580,6 @@ WsLayout layout(uint64_t len) {
   L.o_ctr = take(16);
   L.o_tpos = take(16);
   L.o_blk = take(8 * L.nblk);
-  L.o_blkp = take(8 * (L.nblk + 1));
   L.o_start = take(8 * L.nreg);
   L.o_exitp = take(8 * L.nreg);
   L.o_soff = take(8 * L.nreg);
@@ -633,10 +598,6 @@ WsLayout layout(uint64_t len) {
 int ensure_ws(ldb_ctx* c, uint64_t bytes) {
   if (c->ws_bytes >= bytes) return LDB_OK;
   if (c->ws) (void)hipFree(c->ws);
-  if (c->h_img) (void)hipFree(c->h_img);
-  if (c->h_out) (void)hipFree(c->h_out);
-  if (c->h_res) (void)hipFree(c->h_res);
-  if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
   c->ws = nullptr;
   c->ws_bytes = 0;
   if (hipMalloc(&c->ws, bytes) != hipSuccess) return LDB_ERR_NOMEM;
@@ -655,6 +616,7 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.nreg = L.nreg;
   p.gtab = c->d_tab;
   p.xw = c->d_xw;
+  p.gsh = c->d_gsh;
   p.start = reinterpret_cast<uint64_t*>(w + L.o_start);
   p.exitp = reinterpret_cast<uint64_t*>(w + L.o_exitp);
   p.soff = reinterpret_cast<uint64_t*>(w + L.o_soff);
@@ -669,7 +631,6 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.ctr = reinterpret_cast<uint32_t*>(w + L.o_ctr);
   p.tpos = reinterpret_cast<uint64_t*>(w + L.o_tpos);
   p.blk = reinterpret_cast<uint64_t*>(w + L.o_blk);
-  p.blk_prefix = reinterpret_cast<uint64_t*>(w + L.o_blkp);
   p.out = out;
   p.cap = cap;
   p.kind = kind;
@@ -720,8 +681,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   hipLaunchKernelGGL(k_link, dim3(g256), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_repair, dim3(1), dim3(64), repair_lds_bytes(), s, p);
   hipLaunchKernelGGL(k_combine, dim3(g256), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(k_final, dim3(1), dim3(1024), 0, s, p);
-  hipLaunchKernelGGL(k_compact, dim3((unsigned)L.nblk), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_compact, dim3((unsigned)L.nblk), dim3(kBlkRegions), 0, s, p);
   hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 1);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
@@ -760,15 +720,18 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
   c->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-  std::vector<uint32_t> tab(kTabWords), xw(kW + 1);
+  std::vector<uint32_t> tab(kTabWords), xw(kW + 1), gsh(kGsWords);
   build_tables(tab.data());
   for (int n = 0; n <= kW; ++n) xw[n] = x8n_modp((uint64_t)n);
-  if (hipMalloc(&c->d_tab, tab.size() * 4) != hipSuccess || hipMalloc(&c->d_xw, xw.size() * 4) != hipSuccess) {
+  build_gshift(gsh.data());
+  if (hipMalloc(&c->d_tab, tab.size() * 4) != hipSuccess || hipMalloc(&c->d_xw, xw.size() * 4) != hipSuccess ||
+      hipMalloc(&c->d_gsh, gsh.size() * 4) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_NOMEM;
   }
   if (hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_xw, xw.data(), xw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(c->d_xw, xw.data(), xw.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_gsh, gsh.data(), gsh.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }
@@ -788,6 +751,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->d_xw) (void)hipFree(c->d_xw);
+  if (c->d_gsh) (void)hipFree(c->d_gsh);
   if (c->ws) (void)hipFree(c->ws);
   if (c->h_img) (void)hipFree(c->h_img);
   if (c->h_out) (void)hipFree(c->h_out);

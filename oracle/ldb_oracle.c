@@ -341,7 +341,7 @@ uint64_t ldbo_gen_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint32_t 
     do { num[nd++] = (char)('0' + t % 10); t /= 10; } while (t);
     memset(key, '0', ksize);
     if (ksize >= 4) memcpy(key, "key-", 4);
-    for (int i = 0; i < nd && (uint32_t)i < ksize - 4; ++i) key[ksize - 1 - i] = (uint8_t)num[i];
+    for (int i = 0; ksize >= 4 && i < nd && (uint32_t)i < ksize - 4; ++i) key[ksize - 1 - i] = (uint8_t)num[i];
     for (uint32_t i = 0; i < vl; i += 8) {
       uint64_t r = ldbo_splitmix64(&st);
       for (int b = 0; b < 8 && i + b < vl; ++b) { val[i + b] = (uint8_t)kAlphabet[(r & 0xff) % 36]; r >>= 8; }

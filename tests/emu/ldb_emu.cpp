@@ -78,12 +78,13 @@ struct CpuWave {
 };
 
 struct Emu {
-  std::vector<uint32_t> tab, xw;
+  std::vector<uint32_t> tab, xw, gsh;
   std::vector<uint8_t> buf;
   WaveSh sh;
   uint64_t garbage = 0x1234567;
-  Emu() : tab(kTabWords), xw(kW + 1), buf(kBuf) {
+  Emu() : tab(kTabWords), xw(kW + 1), gsh(kGsWords), buf(kBuf) {
     build_tables(tab.data());
+    build_gshift(gsh.data());
     for (int n = 0; n <= kW; ++n) xw[n] = x8n_modp((uint64_t)n);
   }
   void stage(const Pipe& p, uint64_t r) {
@@ -132,18 +133,18 @@ extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, 
   Emu emu;
   const uint64_t nreg = std::max<uint64_t>(1, (len + kW - 1) / kW);
   const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
-  std::vector<uint64_t> start(nreg), exitp(nreg), soff(nreg), blk(nblk, 0), blkp(nblk + 1, 0), tpos(2, ~0ull);
+  std::vector<uint64_t> start(nreg), exitp(nreg), soff(nreg), blk(nblk, 0), tpos(2, ~0ull);
   std::vector<int32_t> status(nreg);
   std::vector<uint32_t> count(nreg), rpre(nreg), rout(nreg), scrc(nreg), sflag(nreg), ctr(4, 0);
   std::vector<ldb_index_tuple> scratch(nreg * (uint64_t)kRegionCap);
   std::vector<int64_t> fail(nreg + 1);
   Pipe p;
   p.img = img; p.len = len; p.io = io; p.fid = fid; p.nreg = nreg;
-  p.gtab = emu.tab.data(); p.xw = emu.xw.data();
+  p.gtab = emu.tab.data(); p.xw = emu.xw.data(); p.gsh = emu.gsh.data();
   p.start = start.data(); p.exitp = exitp.data(); p.soff = soff.data(); p.status = status.data();
   p.count = count.data(); p.rpre = rpre.data(); p.rout = rout.data(); p.scrc = scrc.data(); p.sflag = sflag.data();
   p.scratch = scratch.data(); p.fail_src = fail.data(); p.ctr = ctr.data(); p.tpos = tpos.data();
-  p.blk = blk.data(); p.blk_prefix = blkp.data(); p.out = out; p.cap = cap; p.kind = LDB_TUPLE_INDEX; p.result = res;
+  p.blk = blk.data(); p.out = out; p.cap = cap; p.kind = LDB_TUPLE_INDEX; p.result = res;
   if (len < (uint64_t)kMaxHeader) {
     // the kernels route tiny images to k_serial; mirror it
     res->status = LDB_EOF_WINDOW; res->fid = fid; res->n_entries = 0; res->end_off = 0; res->n_repairs = 0;
