@@ -206,21 +206,24 @@ LDB_HD uint32_t crc_slice_from(const View& v, int B, int r0) {
 // tA >= kS: A = raw of the whole slice (C must be 0); uB >= kS: Bv = 0.
 LDB_HD void crc_slice2(const View& v, int B, int tA, uint32_t C, int uB, uint32_t* ra, uint32_t* rb) {
   const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
+  // per-lane boundary words, computed once: chain A keeps words < kA, the low ta bytes of word kA
+  // with C injected at byte ta (its bytes past the word spill into word kA + 1); chain B keeps the
+  // bytes >= ub of word kB and every word after it.
+  const int kA = tA >> 3, ta = tA & 7, kB = uB >> 3, ub = uB & 7;
+  const uint64_t mA = ta ? (~0ull >> (64 - 8 * ta)) : 0ull;
+  const uint64_t iA = (uint64_t)C << (8 * ta);
+  const uint64_t sA = ta > 4 ? ((uint64_t)C >> (8 * (8 - ta))) : 0ull;
+  const uint64_t mB = ~0ull << (8 * ub);
   uint32_t a = 0, b = 0;
 #pragma unroll
-  for (int k = 0; k < kS / 16; ++k) {
-    const Row16 q = row[k];
+  for (int k2 = 0; k2 < kS / 16; ++k2) {
+    const Row16 q = row[k2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int off = 16 * k + 8 * h;
+      const int k = 2 * k2 + h;
       const uint64_t w = ((uint64_t)q.w[2 * h + 1] << 32) | q.w[2 * h];
-      const int t = tA - off;    // bytes of this word chain A keeps
-      const int u = uB - off;    // bytes of this word chain B drops
-      const int tc = t < 0 ? 0 : (t > 8 ? 8 : t), uc = u < 0 ? 0 : (u > 8 ? 8 : u);
-      const uint64_t keepA = tc == 8 ? ~0ull : ~(~0ull << (8 * tc));
-      const uint64_t keepB = uc == 8 ? 0ull : (~0ull << (8 * uc));
-      const uint64_t inj = (t >= 0 && t < 8) ? ((uint64_t)C << (8 * t)) : ((t > -4 && t < 0) ? ((uint64_t)C >> (-8 * t)) : 0ull);
-      const uint64_t wa = (w & keepA) ^ inj, wb = w & keepB;
+      const uint64_t wa = k < kA ? w : (k == kA ? ((w & mA) ^ iA) : (k == kA + 1 ? sA : 0ull));
+      const uint64_t wb = k > kB ? w : (k == kB ? (w & mB) : 0ull);
       a = crc_step8(v.tab, a, (uint32_t)wa, (uint32_t)(wa >> 32));
       b = crc_step8(v.tab, b, (uint32_t)wb, (uint32_t)(wb >> 32));
     }

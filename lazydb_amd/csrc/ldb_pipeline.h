@@ -54,7 +54,8 @@ constexpr int kBlkRegions = 256;   // regions per k_combine / k_compact workgrou
 //   t = kGsW            : n = kW           (a whole covered region)
 //   t = kGsE0 + k - 1   : n = kS * k       (k = 1..64: to the end of the landing slice)
 //   t = kGsD + d        : n = d            (d = 0..kS)
-constexpr int kGsW = 0, kGsE0 = 1, kGsD = kGsE0 + kLanes, kGsTables = kGsD + kS + 1;
+//   t = kGsU + d        : n = -d           (d = 0..3: inverse shifts, CRC spans starting past a region end)
+constexpr int kGsW = 0, kGsE0 = 1, kGsD = kGsE0 + kLanes, kGsU = kGsD + kS + 1, kGsTables = kGsU + 4;
 constexpr uint64_t kGsWords = (uint64_t)kGsTables * 1024;
 
 inline void build_gshift(uint32_t* g) {
@@ -66,6 +67,28 @@ inline void build_gshift(uint32_t* g) {
   fill(kGsW, kW);
   for (int k = 1; k <= kLanes; ++k) fill(kGsE0 + k - 1, (uint64_t)kS * k);
   for (int d = 0; d <= kS; ++d) fill(kGsD + d, d);
+  // inverse shifts: invert the 32x32 GF(2) matrix of "shift by d bytes" (Gauss-Jordan)
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t xn = x8n_modp((uint64_t)d);
+    uint32_t m[32], inv[32];   // m[j] = image of basis vector j; row-reduce [m | I] column-wise
+    for (int j = 0; j < 32; ++j) { m[j] = multmodp(xn, 1u << j); inv[j] = 1u << j; }
+    for (int bit = 0; bit < 32; ++bit) {   // make m[bit] the only vector with `bit` set
+      int piv = bit;
+      while (!((m[piv] >> bit) & 1u)) ++piv;
+      uint32_t t = m[piv]; m[piv] = m[bit]; m[bit] = t;
+      t = inv[piv]; inv[piv] = inv[bit]; inv[bit] = t;
+      for (int j = 0; j < 32; ++j)
+        if (j != bit && ((m[j] >> bit) & 1u)) { m[j] ^= m[bit]; inv[j] ^= inv[bit]; }
+    }
+    // now m[j] = e_j and inv[j] = S^-1(e_j)
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t x = b << (8 * q), y = 0;
+        for (int j = 0; j < 32; ++j)
+          if ((x >> j) & 1u) y ^= inv[j];
+        g[(uint64_t)(kGsU + d) * 1024 + q * 256 + b] = y;
+      }
+  }
 }
 
 LDB_HD uint32_t gshift(const uint32_t* g, int t, uint32_t r) {
@@ -121,17 +144,18 @@ LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
   uint32_t reg;
   uint64_t k;
   if (fl & kSkip) {
-    // span starts within 3 bytes of (or after) the region end: compute its first piece directly
-    // up to the end of region r+1, then fold the rest.
-    const uint64_t e1 = (r + 2) * (uint64_t)kW;
-    const uint64_t b = end < e1 ? end : e1;
-    reg = g_crc_bytes(p, 0xFFFFFFFFu, lo, b);
-    if (end <= e1) return reg == ~p.scrc[r];
-    k = r + 2;
+    // the span starts d = lo - R1 in [0, 3] bytes into region r+1 (lane_walk: o + 4 >= region end).
+    // Use the virtual register V at R1 for which the usual fold is exact:
+    //   shift(V, d) ^ raw(bytes [R1, lo)) = ~0   ->   V = shift^-1(~0 ^ raw_d, d)
+    const uint64_t R1 = (r + 1) * (uint64_t)kW;
+    const int d = (int)(lo - R1);
+    uint32_t raw_d = 0;
+    for (int i = 0; i < d; ++i) raw_d = crc_byte(p.gtab + kT8Off, raw_d, p.img[R1 + i]);
+    reg = gshift(p.gsh, kGsU + d, 0xFFFFFFFFu ^ raw_d);
   } else {
     reg = p.rout[r];
-    k = r + 1;
   }
+  k = r + 1;
   const uint64_t m = end / kW;  // region holding the entry's end (may be == nreg when end == len)
   for (; k < m; ++k) reg = gshift(p.gsh, kGsW, reg) ^ p.rpre[k];
   const uint32_t want = ~p.scrc[r];

@@ -173,8 +173,10 @@ __device__ uint64_t g_stamps[kStampSlots];
 #endif
 // ---------------------------------------------------------------- k_scan_main
 __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
+  // CRC tables in a static LDS array: its address is a link-time constant, so every table read
+  // folds the table base into the ds_read offset field
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
   if (blockIdx.x == 0) {  // control words of the later stages (stream-ordered after this kernel)
     if (threadIdx.x < 4) p.ctr[threadIdx.x] = 0;
@@ -183,7 +185,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* wbase = smem + kTabBytes + wave * (sizeof(WaveLds) + kNB * kBuf);
+  uint8_t* wbase = smem + wave * (sizeof(WaveLds) + kNB * kBuf);
   WaveLds* wl = reinterpret_cast<WaveLds*>(wbase);
   uint8_t* ring = wbase + sizeof(WaveLds);
   const uint32_t ring_lds = (uint32_t)(uintptr_t)smem + (uint32_t)(ring - smem);
@@ -271,11 +273,13 @@ struct CohRd {
 __global__ __launch_bounds__(64) void k_repair(Pipe p) {
   const uint32_t nfail = p.ctr[0];
   if (nfail == 0) return;
+  // CRC tables in a static LDS array: its address is a link-time constant, so every table read
+  // folds the table base into the ds_read offset field
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
-  WaveLds* wl = reinterpret_cast<WaveLds*>(smem + kTabBytes);
-  uint8_t* buf = smem + kTabBytes + sizeof(WaveLds);
+  WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
+  uint8_t* buf = smem + sizeof(WaveLds);
   __syncthreads();
   const int lane = threadIdx.x;
   GpuWave wp{lane};
@@ -511,8 +515,8 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   *p.result = res;
 }
 
-size_t main_lds_bytes() { return kTabBytes + kWPB * (sizeof(WaveLds) + kNB * kBuf); }
-size_t repair_lds_bytes() { return kTabBytes + sizeof(WaveLds) + kBuf; }
+size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
+size_t repair_lds_bytes() { return sizeof(WaveLds) + kBuf; }
 
 }  // namespace
 

@@ -96,3 +96,48 @@ def test_emulated_engine_random(seed):
             res, tup, st = emu_scan(img, io)
             ref, rt = coracle.scan(img, io)
             assert_same(res, tup, ref, rt)
+
+
+def _log_with_entry_at(target: int, big_value: int, seed: int) -> np.ndarray:
+    """Entries of 16-B keys and 100-B values (128-B entries) up to `target`, one 12-B-header
+    filler that makes the next entry start exactly at `target`, that entry with a `big_value`-byte
+    value, then a short tail entry."""
+    from oracle import pyoracle as P
+    rng = random.Random(seed)
+    out = bytearray()
+
+    def ent(klen, vlen):
+        return P.encode_entry(P.Entry(key=bytes(rng.randrange(97, 123) for _ in range(klen)),
+                                      value=bytes(rng.randrange(48, 58) for _ in range(vlen)), k_size=klen,
+                                      v_size=vlen))
+    while target - len(out) > 128 + 200:
+        out += ent(16, 100)
+    gap = target - len(out) - 10          # header of (k=0 or small, v) is 10 B while v < 64
+    klen = 8
+    vlen = gap - klen
+    if vlen >= 64:                        # 2-byte vsize varint: one byte less of value
+        vlen -= 1
+    e = ent(klen, vlen)
+    assert len(out) + len(e) == target, (len(out), len(e), target)
+    out += e
+    out += ent(16, big_value)
+    out += ent(16, 40)
+    return np.frombuffer(bytes(out) + bytes(64), np.uint8).copy()
+
+
+@pytest.mark.parametrize("d", [-5, -4, -3, -2, -1, 0, 1])
+@pytest.mark.parametrize("big", [200, 6000, 12000])
+def test_emulated_span_starting_at_region_boundary(d, big):
+    """The entry's CRC span (offset+4) starts d+4 bytes after region 1's start (d = -4..-1: the
+    stored crc straddles the boundary; the k_combine skip path) and ends in the next region, a
+    covered region later, or two regions later; both intact and with a flipped byte."""
+    R1 = 5120
+    img = _log_with_entry_at(R1 + d, big, seed=d * 31 + big)
+    for flip in (None, R1 + d + 4 + big // 2, R1 + d + 2):
+        im = img.copy()
+        if flip is not None:
+            im[flip] ^= 0x20
+        for io in (0, 1):
+            res, tup, st = emu_scan(im, io)
+            ref, rt = coracle.scan(im, io)
+            assert_same(res, tup, ref, rt)
