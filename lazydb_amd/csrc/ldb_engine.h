@@ -301,9 +301,16 @@ LDB_HD uint64_t pack_hot(uint64_t off, const Hot& h) {
 // with ts/k/v varints <= 4 bytes and expiredAt/txID <= 5 bytes (every header LazyDB's writer
 // emits for sizes < 128 MiB). Everything else, and every status other than kCont, goes through
 // the exact byte-wise decoder (classify_entry, Go semantics).
-LDB_HD Hot classify_at(const View& v, int p) {
+// Returns false when the fast path cannot decide (the caller falls back to the exact decoder).
+LDB_HD bool classify_fast(const View& v, int p, Hot* out) {
   const uint64_t off = v.R0 + (uint64_t)p;
-  if (!read_eof(v.len, v.io, (int64_t)off, kMaxHeader)) {
+  if (read_eof(v.len, v.io, (int64_t)off, kMaxHeader)) {
+    out->status = LDB_EOF_WINDOW;
+    out->plaus = 0;
+    out->size = 0;
+    return true;
+  }
+  {
     const int a = p + kPre;
     const int q = a & ~3;
     const uint32_t sh = (uint32_t)(a & 3);
@@ -374,10 +381,19 @@ LDB_HD Hot classify_at(const View& v, int p) {
         r.size = (uint64_t)r.hsize + kv;
         r.plaus = (r.status == kCont && r.stat <= 2u && ts >= 0 && ts <= 2 && ks >= 0 && vs >= 0 && sign0 == 0 &&
                    (uint32_t)r.hsize == r.esize && r.crc != 0) ? 1u : 0u;
-        return r;
+        *out = r;
+        return true;
       }
     }
   }
+  return false;
+}
+
+// ReadLogEntry(off) up to the CRC comparison, exact for every input.
+LDB_HD Hot classify_at(const View& v, int p) {
+  Hot r;
+  if (classify_fast(v, p, &r)) return r;
+  LDB_COUNT(3);
   return hot_from(classify_slow(v, p));
 }
 
@@ -450,7 +466,10 @@ LDB_HD uint32_t find_start(const View& v, int B, int Eeff, Hot* h) {
     else { bit = 64 + __builtin_ctz(m2); m2 &= m2 - 1; }
     const int p = B + bit;
     LDB_COUNT(0);
-    const Hot e = classify_at(v, p);
+    Hot e;
+    // speculation only: a header the fast decoder cannot take (non-canonical or very long varints)
+    // is not a plausible start; the true chain still reaches such entries through the link repair
+    if (!classify_fast(v, p, &e)) continue;
     if (e.plaus) {
       // cheap one-hop check: the implied next entry must pass the same stat-byte prefilter
       // (or lie past the staged bytes / in the header-window EOF zone)
@@ -538,6 +557,10 @@ struct LanePriv {
   LaneKeep kp;
   uint32_t force;
   uint32_t prefix;   // exclusive prefix of emitted tuples
+  // fold results produced by one lane and broadcast with wp.from (no cross-lane reductions)
+  uint32_t rpre;     // region prefix (the region-entry lane)
+  uint32_t rout;     // register at the region end of the entry that runs past it
+  uint32_t rout_set; // 1: this lane produced rout; 2: ... and its span began past its slice (kSkip)
 };
 
 // The only per-lane values other lanes read (LDS): 1 KiB per wavefront.

@@ -40,6 +40,9 @@ namespace {
 #endif
 constexpr int kWPB = LDB_WPB;  // wavefronts per workgroup in k_scan_main
 constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
+#ifndef LDB_BLOCKS_PER_CU
+#define LDB_BLOCKS_PER_CU 0   // 0: as many as fit in a CU's 160 KiB of LDS
+#endif
 constexpr int kG = kW / 1024 + 1;  // LDS-DMA instructions per region (5 x 1 KiB + the halo)
 
 // ---------------------------------------------------------------- wave policy (SIMT)
@@ -71,21 +74,24 @@ struct GpuWave {
     const uint64_t b = __ballot(p(lane) ? 1 : 0);
     return b ? 63 - __builtin_clzll(b) : -1;
   }
+  // Sums / exclusive prefixes of small per-lane counts (< 128) by bit-planes: one ballot per
+  // bit and v_mbcnt for "set bits below me" -- no cross-lane data movement (ds_bpermute).
   template <class V> __device__ uint32_t sum(V v) {
-    uint32_t x = v(lane);
+    const uint32_t x = v(lane);
+    uint32_t s = 0;
 #pragma unroll
-    for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o);
-    return x;
+    for (int b = 0; b < 7; ++b) s += (uint32_t)__builtin_popcountll(__ballot((x >> b) & 1u)) << b;
+    return s;
   }
   template <class V, class O> __device__ void excl_prefix(V v, O out) {
-    const uint32_t mine = v(lane);
-    uint32_t x = mine;
+    const uint32_t x = v(lane);
+    uint32_t s = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
+    for (int b = 0; b < 7; ++b) {
+      const uint64_t m = __ballot((x >> b) & 1u);
+      s += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
     }
-    out(lane, x - mine);
+    out(lane, s);
   }
   // f(l) of the wave-uniform lane `src`, broadcast (v_readlane); uniform control flow only
   template <class F> __device__ uint32_t from(int src, F f) {
@@ -100,12 +106,6 @@ struct GpuWave {
   template <class F> __device__ void single(F f) {
     if (lane == 0) f();
     sync();
-  }
-  __device__ uint32_t bcast_or(uint32_t x) {
-    uint32_t y = x;
-#pragma unroll
-    for (int o = 32; o; o >>= 1) y |= __shfl_xor(y, o);
-    return y;
   }
 };
 
@@ -678,7 +678,11 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
     ev = &c->evs[c->ev_used++];
     LDB_HIP(hipEventRecord(ev->e0, s));
   }
-  const int grid = (int)std::min<uint64_t>((L.nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * 2);
+  // persistent waves: exactly the workgroups that are resident at once (LDS-limited), so no
+  // second dispatch round leaves a tail
+  const int per_cu = LDB_BLOCKS_PER_CU > 0 ? LDB_BLOCKS_PER_CU
+                                           : std::max(1, (int)(163840 / (main_lds_bytes() + kTabBytes)));
+  const int grid = (int)std::min<uint64_t>((L.nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * per_cu);
   hipLaunchKernelGGL(k_scan_main, dim3(grid), dim3(64 * kWPB), main_lds_bytes(), s, p);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   const int g256 = (int)((L.nreg + 255) / 256);

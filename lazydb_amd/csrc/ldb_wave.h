@@ -133,61 +133,66 @@ LDB_HD void region_process(WP& wp, const View& v, WaveSh& sh, uint32_t enter, Re
     sh.raw[l] = a.raw;
   });
   wp.stamp(8);
-  // ---- folds: every entry that leaves its slice carries its CRC register across the covered
-  // slices (constant 80-byte shifts) to the lane where it ends and checks it there.
-  uint32_t region_rpre = 0, region_rout = 0, region_sflag_clear = 0;
+  // ---- folds (one pass: the region prefix chain and every entry's chain run side by side)
+  // The region prefix chain (raw register over [R0, start)) runs in the same carry loop as the
+  // entries' chains, on a lane that owns no chain: L0 - 1 (covered), or lane 0 when no lane starts
+  // an entry. With L0 == 0 the prefix is lane 0's own chain-A value.
+  const int elane = L0 < 0 ? 0 : L0 - 1;
   wp.each([&](int l) {
-    // region prefix (lane L0, or lane 0 for a covered region): the raw register over [R0, start),
-    // delivered shifted to the end of L0's slice (A-form, see combine_region)
-    if (l == (L0 < 0 ? 0 : L0)) {
-      int kend;
-      const int X = L0 < 0 ? (int)v.rlen : (int)priv(l).ln.s;
-      const uint32_t reg = carry_full(v, sh, 0u, 0, X, &kend);
-      region_rpre = L0 < 0 ? carry_tail(v, sh, reg, kend, X) : (shift_slice(v.tab, reg) ^ priv(l).ln.raw);
-    }
-  });
-  wp.each([&](int l) {
-    LaneState& a = priv(l).ln;
-    if (!(l <= lim && a.s != kNone32 && a.term == kCont && (a.sflag & kStraddle)) || (a.sflag & kNoCrc)) return;
-    const uint64_t xr = a.x - v.R0;
-    const int X = xr < (uint64_t)kW ? (int)xr : kW;
-    const uint32_t want = ~a.scrc;
-    uint32_t reg;
-    int k0;
-    if (a.sflag & kSkip) {   // span starts < 4 bytes before the slice end: first piece directly
-      if (l == kLanes - 1) return;  // region-level skip: k_combine computes it from global memory
-      const int e1 = (l + 2) * kS;
-      const int hi = X < e1 ? X : e1;
-      reg = crc_segment(v, (int)a.so + 4, hi, 0xFFFFFFFFu);
-      if (X <= e1) {
-        if (X < kW) {
-          if (reg != want) { a.term = LDB_ERR_CRC; a.tpos = a.so; a.cnt -= 1; a.sflag = 0; }
+    LanePriv& q = priv(l);
+    LaneState& a = q.ln;
+    q.rout_set = 0;
+    uint32_t reg = 0;
+    int k0 = 0, X = 0;
+    const bool entry_role = l == elane;
+    if (entry_role) {
+      X = L0 < 0 ? (int)v.rlen : (int)sh.s[L0];
+    } else {
+      // every entry that leaves its slice carries its CRC register across the covered slices
+      // (constant 80-byte shifts) to the lane where it ends and checks it there
+      if (!(l <= lim && a.s != kNone32 && a.term == kCont && (a.sflag & kStraddle)) || (a.sflag & kNoCrc)) return;
+      const uint64_t xr = a.x - v.R0;
+      X = xr < (uint64_t)kW ? (int)xr : kW;
+      if (a.sflag & kSkip) {   // span starts < 4 bytes before the slice end: first piece directly
+        if (l == kLanes - 1) return;  // region-level skip: k_combine handles it
+        const int e1 = (l + 2) * kS;
+        const int hi = X < e1 ? X : e1;
+        reg = crc_segment(v, (int)a.so + 4, hi, 0xFFFFFFFFu);
+        if (X <= e1) {
+          if (X < kW) {
+            if (reg != ~a.scrc) { a.term = LDB_ERR_CRC; a.tpos = a.so; a.cnt -= 1; a.sflag = 0; }
+            return;
+          }
+          q.rout = reg;   // reaches the region end
+          q.rout_set = 2;
           return;
         }
-        region_rout = reg;   // reaches the region end
-        region_sflag_clear = 1;
-        return;
+        k0 = l + 2;
+      } else {
+        reg = a.rout;
+        k0 = l + 1;
       }
-      k0 = l + 2;
-    } else {
-      reg = a.rout;
-      k0 = l + 1;
     }
     int kend;
     reg = carry_full(v, sh, reg, k0, X, &kend);
+    if (entry_role) {   // A-form prefix (see combine_region), or the raw register of a covered region
+      q.rpre = L0 < 0 ? carry_tail(v, sh, reg, kend, X) : (shift_slice(v.tab, reg) ^ sh.raw[L0]);
+      return;
+    }
     if (X >= kW) {        // runs past the region: register at the region end
-      region_rout = reg;
-      region_sflag_clear = (a.sflag & kSkip) ? 1u : 0u;
+      q.rout = reg;
+      q.rout_set = (a.sflag & kSkip) ? 2u : 1u;
       return;
     }
     bool ok;
-    if (X >= (int)v.rlen) ok = carry_tail(v, sh, reg, kend, X) == want;   // ends exactly at the end of the file
-    else ok = shift_slice(v.tab, reg) == sh.raw[kend];                    // lane kend starts at X, injected want
+    if (X >= (int)v.rlen) ok = carry_tail(v, sh, reg, kend, X) == ~a.scrc;   // ends exactly at the end of the file
+    else ok = shift_slice(v.tab, reg) == sh.raw[kend];                       // lane kend starts at X, injected ~crc
     if (!ok) { a.term = LDB_ERR_CRC; a.tpos = a.so; a.cnt -= 1; a.sflag = 0; }
   });
-  region_rpre = wp.bcast_or(region_rpre);
-  region_rout = wp.bcast_or(region_rout);
-  region_sflag_clear = wp.bcast_or(region_sflag_clear);
+  const uint32_t region_rpre = L0 == 0 ? sh.raw[0] : wp.from(elane, [&](int l) { return priv(l).rpre; });
+  const int rsrc = wp.first([&](int l) { return priv(l).rout_set != 0; });
+  const uint32_t region_rout = rsrc >= 0 ? wp.from(rsrc, [&](int l) { return priv(l).rout; }) : 0u;
+  const uint32_t region_sflag_clear = rsrc >= 0 ? (wp.from(rsrc, [&](int l) { return priv(l).rout_set; }) == 2u) : 0u;
   wp.stamp(3);
   tl = wp.first([&](int l) { return priv(l).ln.s != kNone32 && priv(l).ln.term != kCont; });
   lim = tl < 0 ? kLanes - 1 : tl;

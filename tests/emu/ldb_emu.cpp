@@ -73,7 +73,6 @@ struct CpuWave {
   template <class F> uint32_t from(int src, F f) { return (uint32_t)f(src); }
   template <class F> uint64_t from64(int src, F f) { return (uint64_t)f(src); }
   template <class F> void single(F f) { f(); }
-  uint32_t bcast_or(uint32_t x) { return x; }
   void stamp(int) {}
 };
 

@@ -21,6 +21,8 @@ def build(name: str) -> str:
         defs = [f"-DLDB_WPB={m.group(1)}", f"-DLDB_NB={m.group(2)}"]
     elif name == "stamps":
         defs = ["-DLDB_STAMPS=1"]
+    elif name == "stamps1":   # one wave per SIMD: phase stamps measure each wave's own critical path
+        defs = ["-DLDB_STAMPS=1", "-DLDB_WPB=4", "-DLDB_NB=3", "-DLDB_BLOCKS_PER_CU=1"]   # 112 KB LDS: 1 block/CU
     else:
         raise SystemExit(f"unknown variant {name}")
     out = os.path.join(OUT, f"var_{name}.so")

@@ -15,7 +15,7 @@ L = C.CDLL(os.path.join(ROOT, "tests/emu/_build/libldb_emu_cnt.so"))
 L.emu_scan.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_void_p, C.c_uint64,
                        C.POINTER(coracle.ScanResult), C.c_void_p]
 L.emu_counters.argtypes = [C.c_void_p]
-names = ["spec classify", "walk classify", "in-slice entry crc", "ev3", "ev4"]
+names = ["spec classify", "walk classify", "in-slice entry crc", "slow decode", "ev4"]
 cases = {"cfg2 64/256": dict(ksize=64, vsize=256),
          "zipf s=1.1 max 4096": dict(ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096),
          "small 16/16": dict(ksize=16, vsize=16)}

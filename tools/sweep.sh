@@ -7,7 +7,9 @@ for v in liblazydb_gpu ${VARIANTS:-}; do
   LAZYDB_GPU_LIB=$PWD/lazydb_amd/_lib/$v.so timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/b_$v.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/b_$v.log; exit 1; }
   python -c "import json,sys; d=json.loads(open('gpurun_out/b_$v.log').read().strip().splitlines()[-1]); print('$v', d['value'], 'GiB/s', d['roofline']['avg_kernel_ms'], 'ms main', d['roofline']['avg_pipeline_ms'], 'ms total', 'verified', d['verified_vs_oracle'], 'repairs', d['repairs'])"
 done
-if [ -f lazydb_amd/_lib/var_stamps.so ]; then
-  LAZYDB_GPU_LIB=$PWD/lazydb_amd/_lib/var_stamps.so timeout -k 10 200 python tools/stamps.py > gpurun_out/stamps.log 2>&1 || { echo "stamps failed"; tail -5 gpurun_out/stamps.log; exit 1; }
-  cat gpurun_out/stamps.log
-fi
+for st in stamps stamps1; do
+  if [ -f lazydb_amd/_lib/var_$st.so ]; then
+    LAZYDB_GPU_LIB=$PWD/lazydb_amd/_lib/var_$st.so timeout -k 10 200 python tools/stamps.py > gpurun_out/$st.log 2>&1 || { echo "$st failed"; tail -5 gpurun_out/$st.log; exit 1; }
+    echo "== $st"; cat gpurun_out/$st.log
+  fi
+done
