@@ -24,16 +24,7 @@ struct Pipe {
   const uint32_t* gtab;     // kTabWords table block (global copy)
   const uint32_t* xw;       // x^(8n) mod P for n = 0..kW
   const uint32_t* gsh;      // kGsTables x 1024 register-shift byte tables (build_gshift)
-  // SoA region summaries
-  uint64_t* start;
-  uint64_t* exitp;
-  uint64_t* soff;
-  int32_t* status;
-  uint32_t* count;
-  uint32_t* rpre;
-  uint32_t* rout;
-  uint32_t* scrc;
-  uint32_t* sflag;
+  RegionSum* rs;             // per-region summaries (48-B records)
   ldb_index_tuple* scratch;   // nreg * kRegionCap
   // control
   int64_t* fail_src;          // regions whose outgoing link failed (-1: region 0 does not start at 0)
@@ -96,17 +87,7 @@ LDB_HD uint32_t gshift(const uint32_t* g, int t, uint32_t r) {
   return T[r & 0xFFu] ^ T[256 + ((r >> 8) & 0xFFu)] ^ T[512 + ((r >> 16) & 0xFFu)] ^ T[768 + (r >> 24)];
 }
 
-LDB_HD void store_region(const Pipe& p, uint64_t r, const RegionSum& s) {
-  p.start[r] = s.start;
-  p.exitp[r] = s.exitp;
-  p.soff[r] = s.soff;
-  p.status[r] = s.status;
-  p.count[r] = s.count;
-  p.rpre[r] = s.rpre;
-  p.rout[r] = s.rout;
-  p.scrc[r] = s.scrc;
-  p.sflag[r] = s.sflag;
-}
+LDB_HD void store_region(const Pipe& p, uint64_t r, const RegionSum& s) { p.rs[r] = s; }
 
 LDB_HD uint32_t region_len(const Pipe& p, uint64_t r) {
   const uint64_t R0 = r * (uint64_t)kW;
@@ -116,13 +97,13 @@ LDB_HD uint32_t region_len(const Pipe& p, uint64_t r) {
 // Link check of region r. Returns true when r's outgoing link is broken (or r == 0 does not
 // start at offset 0, reported by the caller as source -1).
 LDB_HD bool link_broken(const Pipe& p, uint64_t r) {
-  if (p.start[r] == kNone64 || p.status[r] != kCont) return false;
-  const uint64_t x = p.exitp[r];
+  if (p.rs[r].start == kNone64 || p.rs[r].status != kCont) return false;
+  const uint64_t x = p.rs[r].exitp;
   if (x >= p.len) return false;  // chain ends exactly at the file end (tail terminal)
   const uint64_t m = x / kW;
   for (uint64_t k = r + 1; k < m; ++k)
-    if (p.start[k] != kNone64) return true;
-  return p.start[m] != x;
+    if (p.rs[k].start != kNone64) return true;
+  return p.rs[m].start != x;
 }
 
 // ---------------------------------------------------------------- CRC helpers (global memory)
@@ -136,10 +117,10 @@ LDB_HD uint32_t g_crc_bytes(const Pipe& p, uint32_t reg, uint64_t a, uint64_t b)
 // Verify the straddle-out entry of region r (its CRC span crosses into later regions).
 // Returns true when it matches its stored crc.
 LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
-  const uint32_t fl = p.sflag[r];
+  const uint32_t fl = p.rs[r].sflag;
   if (fl & kNoCrc) return true;
-  const uint64_t o = p.soff[r];
-  const uint64_t end = p.exitp[r];
+  const uint64_t o = p.rs[r].soff;
+  const uint64_t end = p.rs[r].exitp;
   const uint64_t lo = o + 4;
   uint32_t reg;
   uint64_t k;
@@ -153,23 +134,23 @@ LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
     for (int i = 0; i < d; ++i) raw_d = crc_byte(p.gtab + kT8Off, raw_d, p.img[R1 + i]);
     reg = gshift(p.gsh, kGsU + d, 0xFFFFFFFFu ^ raw_d);
   } else {
-    reg = p.rout[r];
+    reg = p.rs[r].rout;
   }
   k = r + 1;
   const uint64_t m = end / kW;  // region holding the entry's end (may be == nreg when end == len)
-  for (; k < m; ++k) reg = gshift(p.gsh, kGsW, reg) ^ p.rpre[k];
-  const uint32_t want = ~p.scrc[r];
+  for (; k < m; ++k) reg = gshift(p.gsh, kGsW, reg) ^ p.rs[k].rpre;
+  const uint32_t want = ~p.rs[r].scrc;
   if (m < p.nreg) {
     const uint64_t n = end - m * (uint64_t)kW;
     if (n) {
-      if (p.start[m] == kNone64) {
-        reg = multmodp(p.xw[n], reg) ^ p.rpre[m];   // region covered up to the end of the file
+      if (p.rs[m].start == kNone64) {
+        reg = multmodp(p.xw[n], reg) ^ p.rs[m].rpre;   // region covered up to the end of the file
       } else {
         // rpre[m] = shift(raw([R0, n)), E0 - n), E0 = end of the slice holding n (region_process):
         // reg(n) == want  <=>  shift(reg, E0) ^ rpre[m] == shift(want, E0 - n)
         const int k0 = (int)(n / kS) + 1;   // E0 = kS * k0
         const int d = kS * k0 - (int)n;     // 1..kS
-        return (gshift(p.gsh, kGsE0 + k0 - 1, reg) ^ p.rpre[m]) == gshift(p.gsh, kGsD + d, want);
+        return (gshift(p.gsh, kGsE0 + k0 - 1, reg) ^ p.rs[m].rpre) == gshift(p.gsh, kGsD + d, want);
       }
     }
   }

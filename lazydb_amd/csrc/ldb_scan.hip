@@ -53,7 +53,10 @@ struct GpuWave {
   uint64_t t_last = 0;
   uint64_t acc[kStampSlots] = {};
   __device__ void stamp(int id) {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
+    // s_memtime returns out of order with LDS reads on lgkmcnt: drain it inside the stamp, or the
+    // compiler's counted lgkmcnt waits around it stop meaning what they say (MI355X guide)
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
     if (t_last) acc[id] += t - t_last;
     t_last = t;
   }
@@ -153,19 +156,13 @@ __device__ __forceinline__ void store_tuple(ldb_index_tuple* dst, uint64_t pos, 
   *reinterpret_cast<uint4*>(dst) = t;
 }
 
-// Region summary to the SoA arrays: one single-lane GLOBAL store per field, straight from the
-// kernarg pointers (address space known to the compiler). k_scan_main's vmcnt waits rely on these
-// being global_store (in-order on vmcnt); a flat_store would retire out of order.
-__device__ __forceinline__ void write_region_wave(const Pipe& p, uint64_t r, const RegionSum& s, int lane) {
-  if (lane == 0) p.start[r] = s.start;
-  if (lane == 1) p.exitp[r] = s.exitp;
-  if (lane == 2) p.soff[r] = s.soff;
-  if (lane == 3) p.status[r] = s.status;
-  if (lane == 4) p.count[r] = s.count;
-  if (lane == 5) p.rpre[r] = s.rpre;
-  if (lane == 6) p.rout[r] = s.rout;
-  if (lane == 7) p.scrc[r] = s.scrc;
-  if (lane == 8) p.sflag[r] = s.sflag;
+// Region summary record (48 B) from its LDS copy: lanes 0-11 move one dword each -- one LDS read
+// and one coalesced global_store_dword (global, in-order on vmcnt: k_scan_main counts it).
+__device__ __forceinline__ void write_region_wave(const Pipe& p, uint64_t r, const RegionSum* lds_rs, int lane) {
+  if (lane < 12) {
+    const uint32_t x = reinterpret_cast<const uint32_t*>(lds_rs)[lane];
+    reinterpret_cast<uint32_t*>(p.rs + r)[lane] = x;
+  }
 }
 
 #ifdef LDB_STAMPS
@@ -233,7 +230,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
           GpuWave::sync();
           if (nx < count) stage_dma(p.img, p.len, gw + nx * nw, ring_lds + slot * kBuf, lane);
         });
-    write_region_wave(p, r, wl->rs, lane);
+    write_region_wave(p, r, &wl->rs, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
     wp.stamp(7);
@@ -253,7 +250,7 @@ __global__ void k_link(Pipe p) {
     const uint32_t i = atomicAdd(&p.ctr[0], 1u);
     p.fail_src[i] = (int64_t)r;
   }
-  if (r == 0 && p.start[0] != 0) {
+  if (r == 0 && p.rs[0].start != 0) {
     const uint32_t i = atomicAdd(&p.ctr[0], 1u);
     p.fail_src[i] = -1;
   }
@@ -263,10 +260,10 @@ __global__ void k_link(Pipe p) {
 struct CohRd {
   const Pipe* p;
   __device__ uint64_t start(uint64_t r) const {
-    return __hip_atomic_load(&p->start[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(&p->rs[r].start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __device__ uint64_t exitp(uint64_t r) const {
-    return __hip_atomic_load(&p->exitp[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(&p->rs[r].exitp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 };
 
@@ -289,7 +286,7 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
       const int64_t r = b + lane;
       bool t = false;
       if (r >= 0 && r <= hi && (uint64_t)r < p.nreg) {
-        const int32_t st = __hip_atomic_load(&p.status[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t st = __hip_atomic_load(&p.rs[r].status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = st != kCont && rd.start((uint64_t)r) != kNone64;
       }
       const uint64_t m = __ballot(t ? 1 : 0);
@@ -340,19 +337,19 @@ __global__ __launch_bounds__(256) void k_combine(Pipe p) {
   __shared__ uint64_t s_sum[256];
   uint64_t cnt = 0;
   if (r < p.nreg) {
-    const int32_t st = p.status[r];
-    const uint64_t start = p.start[r];
-    cnt = p.count[r];
+    const int32_t st = p.rs[r].status;
+    const uint64_t start = p.rs[r].start;
+    cnt = p.rs[r].count;
     if (st == kOverflow) {
       atomicOr(&p.ctr[1], 1u);
     } else if (start != kNone64) {
       if (st != kCont) {
-        atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.exitp[r], st));
+        atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.rs[r].exitp, st));
       } else {
-        const uint64_t x = p.exitp[r];
+        const uint64_t x = p.rs[r].exitp;
         if (x >= p.len) atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.len, LDB_EOF_WINDOW));
-        if ((p.sflag[r] & kStraddle) && !combine_region(p, r))
-          atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.soff[r], LDB_ERR_CRC));
+        if ((p.rs[r].sflag & kStraddle) && !combine_region(p, r))
+          atomicMin((unsigned long long*)&p.tpos[0], (unsigned long long)pack_term(p.rs[r].soff, LDB_ERR_CRC));
       }
     }
   }
@@ -417,9 +414,9 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
   const uint64_t r = r0 + tid;
   uint32_t c = 0;
   if (r < p.nreg && r <= regT) {
-    c = p.count[r];
+    c = p.rs[r].count;
     // the terminal is this region's straddle-out entry failing its CRC
-    if (r == regT && p.status[r] == kCont && (p.sflag[r] & kStraddle) && p.soff[r] == tp && c > 0) c -= 1;
+    if (r == regT && p.rs[r].status == kCont && (p.rs[r].sflag & kStraddle) && p.rs[r].soff == tp && c > 0) c -= 1;
   }
   uint32_t x = c;
 #pragma unroll
@@ -565,8 +562,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_start, o_exitp, o_soff, o_status, o_count, o_rpre, o_rout, o_scrc, o_sflag, o_scratch, o_fail, o_ctr,
-      o_tpos, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -584,15 +580,7 @@ WsLayout layout(uint64_t len) {
   L.o_ctr = take(16);
   L.o_tpos = take(16);
   L.o_blk = take(8 * L.nblk);
-  L.o_start = take(8 * L.nreg);
-  L.o_exitp = take(8 * L.nreg);
-  L.o_soff = take(8 * L.nreg);
-  L.o_status = take(4 * L.nreg);
-  L.o_count = take(4 * L.nreg);
-  L.o_rpre = take(4 * L.nreg);
-  L.o_rout = take(4 * L.nreg);
-  L.o_scrc = take(4 * L.nreg);
-  L.o_sflag = take(4 * L.nreg);
+  L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1));
   L.o_scratch = take(sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg);
   L.total = o;
@@ -621,15 +609,7 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.gtab = c->d_tab;
   p.xw = c->d_xw;
   p.gsh = c->d_gsh;
-  p.start = reinterpret_cast<uint64_t*>(w + L.o_start);
-  p.exitp = reinterpret_cast<uint64_t*>(w + L.o_exitp);
-  p.soff = reinterpret_cast<uint64_t*>(w + L.o_soff);
-  p.status = reinterpret_cast<int32_t*>(w + L.o_status);
-  p.count = reinterpret_cast<uint32_t*>(w + L.o_count);
-  p.rpre = reinterpret_cast<uint32_t*>(w + L.o_rpre);
-  p.rout = reinterpret_cast<uint32_t*>(w + L.o_rout);
-  p.scrc = reinterpret_cast<uint32_t*>(w + L.o_scrc);
-  p.sflag = reinterpret_cast<uint32_t*>(w + L.o_sflag);
+  p.rs = reinterpret_cast<RegionSum*>(w + L.o_rs);
   p.scratch = reinterpret_cast<ldb_index_tuple*>(w + L.o_scratch);
   p.fail_src = reinterpret_cast<int64_t*>(w + L.o_fail);
   p.ctr = reinterpret_cast<uint32_t*>(w + L.o_ctr);

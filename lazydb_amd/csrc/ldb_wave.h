@@ -8,7 +8,7 @@
 namespace ldb {
 
 // Region-level result (mirrors the SoA summary arrays of ldb_scan.hip).
-struct RegionSum {
+struct alignas(16) RegionSum {
   uint64_t start;    // absolute first entry start in the region, or kNone64 (covered region)
   uint64_t exitp;    // status == kCont: absolute offset after the region's last entry; else terminal offset
   uint64_t soff;     // straddle-out entry start (absolute)
@@ -20,6 +20,7 @@ struct RegionSum {
   uint32_t scrc;     // straddler's stored crc
   uint32_t sflag;    // kStraddle | kSkip | kNoCrc
 };
+static_assert(sizeof(RegionSum) == 48, "RegionSum is stored as 12 dwords");
 
 // Carry register `reg` (valid at region-relative position k0 * kS) across the covered slices
 // k0, k0+1, ... whose whole bytes belong to the same entry, up to position `X` rounded down to a

@@ -121,8 +121,8 @@ struct Emu {
 
 struct Rd {
   const Pipe* p;
-  uint64_t start(uint64_t r) const { return p->start[r]; }
-  uint64_t exitp(uint64_t r) const { return p->exitp[r]; }
+  uint64_t start(uint64_t r) const { return p->rs[r].start; }
+  uint64_t exitp(uint64_t r) const { return p->rs[r].exitp; }
 };
 
 }  // namespace
@@ -132,16 +132,15 @@ extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, 
   Emu emu;
   const uint64_t nreg = std::max<uint64_t>(1, (len + kW - 1) / kW);
   const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
-  std::vector<uint64_t> start(nreg), exitp(nreg), soff(nreg), blk(nblk, 0), tpos(2, ~0ull);
-  std::vector<int32_t> status(nreg);
-  std::vector<uint32_t> count(nreg), rpre(nreg), rout(nreg), scrc(nreg), sflag(nreg), ctr(4, 0);
+  std::vector<uint64_t> blk(nblk, 0), tpos(2, ~0ull);
+  std::vector<RegionSum> rs(nreg);
+  std::vector<uint32_t> ctr(4, 0);
   std::vector<ldb_index_tuple> scratch(nreg * (uint64_t)kRegionCap);
   std::vector<int64_t> fail(nreg + 1);
   Pipe p;
   p.img = img; p.len = len; p.io = io; p.fid = fid; p.nreg = nreg;
   p.gtab = emu.tab.data(); p.xw = emu.xw.data(); p.gsh = emu.gsh.data();
-  p.start = start.data(); p.exitp = exitp.data(); p.soff = soff.data(); p.status = status.data();
-  p.count = count.data(); p.rpre = rpre.data(); p.rout = rout.data(); p.scrc = scrc.data(); p.sflag = sflag.data();
+  p.rs = rs.data();
   p.scratch = scratch.data(); p.fail_src = fail.data(); p.ctr = ctr.data(); p.tpos = tpos.data();
   p.blk = blk.data(); p.out = out; p.cap = cap; p.kind = LDB_TUPLE_INDEX; p.result = res;
   if (len < (uint64_t)kMaxHeader) {
@@ -157,35 +156,35 @@ extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, 
     if (link_broken(p, r)) {
       fail[ctr[0]++] = (int64_t)r;
       if (getenv("LDB_EMU_DEBUG")) {
-        const uint64_t m = exitp[r] / kW;
-        fprintf(stderr, "fail r=%llu start=%llu exit=%llu st=%d -> m=%llu start[m]=%llu (rel %lld) st[m]=%d\n",
-                (unsigned long long)r, (unsigned long long)start[r], (unsigned long long)exitp[r], status[r],
-                (unsigned long long)m, (unsigned long long)start[m], (long long)(start[m] - m * kW), status[m]);
+        const uint64_t m = rs[r].exitp / kW;
+        fprintf(stderr, "fail r=%llu start=%llu exit=%llu st=%d -> m=%llu rs[m].start=%llu (rel %lld) st[m]=%d\n",
+                (unsigned long long)r, (unsigned long long)rs[r].start, (unsigned long long)rs[r].exitp, rs[r].status,
+                (unsigned long long)m, (unsigned long long)rs[m].start, (long long)(rs[m].start - m * kW), rs[m].status);
       }
     }
-    if (r == 0 && start[0] != 0) fail[ctr[0]++] = -1;
+    if (r == 0 && rs[0].start != 0) fail[ctr[0]++] = -1;
   }
   const uint32_t nfail = ctr[0];
   // k_repair
   if (nfail) {
     auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
       for (int64_t r = std::max<int64_t>(lo + 1, 0); r <= hi && (uint64_t)r < nreg; ++r)
-        if (status[r] != kCont && start[r] != kNone64) return r;
+        if (rs[r].status != kCont && rs[r].start != kNone64) return r;
       return -1;
     };
     ctr[2] = repair(p, nfail, Rd{&p}, first_term, [&](uint64_t r, uint32_t enter) { return emu.run(p, r, enter); });
   }
   // k_combine
   for (uint64_t r = 0; r < nreg; ++r) {
-    const int32_t st = status[r];
+    const int32_t st = rs[r].status;
     if (st == kOverflow) { ctr[1] = 1; continue; }
-    blk[r / kBlkRegions] += count[r];
-    if (start[r] == kNone64) continue;
+    blk[r / kBlkRegions] += rs[r].count;
+    if (rs[r].start == kNone64) continue;
     if (st != kCont) {
-      tpos[0] = std::min(tpos[0], pack_term(exitp[r], st));
+      tpos[0] = std::min(tpos[0], pack_term(rs[r].exitp, st));
     } else {
-      if (exitp[r] >= len) tpos[0] = std::min(tpos[0], pack_term(len, LDB_EOF_WINDOW));
-      if ((sflag[r] & kStraddle) && !combine_region(p, r)) tpos[0] = std::min(tpos[0], pack_term(soff[r], LDB_ERR_CRC));
+      if (rs[r].exitp >= len) tpos[0] = std::min(tpos[0], pack_term(len, LDB_EOF_WINDOW));
+      if ((rs[r].sflag & kStraddle) && !combine_region(p, r)) tpos[0] = std::min(tpos[0], pack_term(rs[r].soff, LDB_ERR_CRC));
     }
   }
   if (ctr[1]) return -100;  // overflow: the GPU pipeline re-runs k_serial
@@ -196,8 +195,8 @@ extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, 
   const uint64_t regT = tp / kW;
   uint64_t n = 0;
   for (uint64_t r = 0; r < nreg && r <= regT; ++r) {
-    uint64_t c = count[r];
-    if (r == regT && status[r] == kCont && (sflag[r] & kStraddle) && soff[r] == tp && c > 0) c -= 1;
+    uint64_t c = rs[r].count;
+    if (r == regT && rs[r].status == kCont && (rs[r].sflag & kStraddle) && rs[r].soff == tp && c > 0) c -= 1;
     for (uint64_t j = 0; j < c; ++j)
       if (n + j < cap) out[n + j] = scratch[r * (uint64_t)kRegionCap + j];
     n += c;
