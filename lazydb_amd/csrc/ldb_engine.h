@@ -379,7 +379,10 @@ LDB_HD bool classify_fast(const View& v, int p, Hot* out) {
         r.status = sentinel ? LDB_EOF_SENTINEL
                             : ((kv && read_eof(v.len, v.io, (int64_t)(off + (uint64_t)r.hsize), kv)) ? LDB_EOF_KV : kCont);
         r.size = (uint64_t)r.hsize + kv;
-        r.plaus = (r.status == kCont && r.stat <= 2u && ts >= 0 && ts <= 2 && ks >= 0 && vs >= 0 && sign0 == 0 &&
+        // speculation heuristic only (results never depend on it): what LazyDB's writers emit --
+        // every call site passes a user key (str.go, list.go, tx.go), so an empty key is a hint
+        // that this "header" is really the tail of a CRC field (k_size read from the stat byte)
+        r.plaus = (r.status == kCont && r.stat <= 2u && ts >= 0 && ts <= 2 && ks >= 1 && vs >= 0 && sign0 == 0 &&
                    (uint32_t)r.hsize == r.esize && r.crc != 0) ? 1u : 0u;
         *out = r;
         return true;
