@@ -58,7 +58,10 @@ constexpr int kTBOff = 5120;              // 2048 + 2048 + 1024
 constexpr int kT8Off = 10240;             // 256: byte-at-a-time table (rare paths)
 constexpr int kZSOff = 10496;             // 4 x 256: register shift by kS zero bytes (fold chains)
 constexpr int kKOff = 11520;              // kS + 1: K[n] = register after n zero bytes from ~0
-constexpr int kTabWords = 11616;
+// chained fast path (ldb_chain.h): register shifts as 4 byte-indexed tables of 256 each
+constexpr int kVSOff = 11616;             // 4 x 1024: shift by 8, 16, 32, 64 bytes (check-point shifts)
+constexpr int kSCOff = kVSOff + 4 * 1024; // 5 x 1024: shift by 2, 4, 8, 16, 32 slices (lane scan; 1 slice = kZSOff)
+constexpr int kTabWords = kSCOff + 5 * 1024;
 constexpr int kTabBytes = kTabWords * 4;
 
 // Force codes for a lane (re)run.
@@ -87,7 +90,13 @@ inline void build_tables(uint32_t* tab) {
   for (uint32_t i = 0; i < 256; ++i) tab[kT8Off + i] = step_bits(i, 8);
   for (int q = 0; q < 4; ++q)
     for (uint32_t b = 0; b < 256; ++b) tab[kZSOff + q * 256 + b] = step_bits(b << (8 * q), 8 * kS);
-  for (int n = 0; n < kTabWords - kKOff; ++n) tab[kKOff + n] = n <= kS ? step_bits(0xFFFFFFFFu, 8 * n) : 0u;
+  for (int n = 0; n < kVSOff - kKOff; ++n) tab[kKOff + n] = n <= kS ? step_bits(0xFFFFFFFFu, 8 * n) : 0u;
+  auto shift_table = [&](int off, int nbytes) {
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b) tab[off + q * 256 + b] = step_bits(b << (8 * q), 8 * nbytes);
+  };
+  for (int i = 0; i < 4; ++i) shift_table(kVSOff + i * 1024, 8 << i);
+  for (int i = 0; i < 5; ++i) shift_table(kSCOff + i * 1024, kS << (i + 1));
 }
 
 // ---------------------------------------------------------------- memory views
@@ -98,6 +107,7 @@ struct View {
   const uint8_t* buf;
   const uint32_t* tab;
   const uint32_t* xw;
+  const uint32_t* gsh;  // register-shift byte tables in global memory (build_gshift), uniform lookups
   uint64_t R0;      // absolute offset of region byte 0
   uint32_t rlen;    // bytes of the region inside the file (<= kW)
   uint64_t len;     // file length (= IOController bound)

@@ -11,7 +11,7 @@
 //   final   : the scan stops at the first terminal along the chain; tuples before it are kept.
 #pragma once
 
-#include "ldb_wave.h"
+#include "ldb_chain.h"
 
 namespace ldb {
 
@@ -119,6 +119,11 @@ LDB_HD uint32_t g_crc_bytes(const Pipe& p, uint32_t reg, uint64_t a, uint64_t b)
 LDB_HD bool combine_region(const Pipe& p, uint64_t r) {
   const uint32_t fl = p.rs[r].sflag;
   if (fl & kNoCrc) return true;
+  {
+    // the region the entry ends in verified it in-wave (kOwnerOk, ldb_chain.h)
+    const uint64_t x = p.rs[r].exitp, m = x / kW;
+    if (m < p.nreg && (p.rs[m].sflag & kOwnerOk) && p.rs[m].start == x) return true;
+  }
   const uint64_t o = p.rs[r].soff;
   const uint64_t end = p.rs[r].exitp;
   const uint64_t lo = o + 4;
@@ -194,7 +199,14 @@ LDB_HD uint32_t repair(const Pipe& p, uint32_t nfail, Rd rd, FirstTerm first_ter
       for (int64_t k = cur + 1; k < (int64_t)m; ++k) {
         if (rd.start((uint64_t)k) != kNone64) { run((uint64_t)k, kForceNone); ++repairs; }
       }
-      if (rd.start(m) == x) { done = (int64_t)m - 1; break; }
+      if (rd.start(m) == x) {
+        // Merged into a region whose first start is x. If that region verified its owner in-wave
+        // (kOwnerOk, ldb_chain.h), it checked the entry ending at x on ITS run's chain, which need
+        // not be the entry the true chain ends there with: re-run it so k_combine checks the owner.
+        if (rd.sflag(m) & kOwnerOk) { run(m, (uint32_t)(x - m * kW)); ++repairs; }
+        done = (int64_t)m - 1;
+        break;
+      }
       const RegionSum s = run(m, (uint32_t)(x - m * (uint64_t)kW));
       ++repairs;
       if (s.status != kCont) { stop = true; break; }

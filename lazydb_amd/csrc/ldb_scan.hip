@@ -33,7 +33,7 @@ using namespace ldb;
 namespace {
 
 #ifndef LDB_WPB
-#define LDB_WPB 16
+#define LDB_WPB 12
 #endif
 #ifndef LDB_NB
 #define LDB_NB 1
@@ -109,6 +109,14 @@ struct GpuWave {
   template <class F> __device__ void single(F f) {
     if (lane == 0) f();
     sync();
+  }
+  // put(lane, value of lane - d, lane >= d): DPP wave_shr for d = 1, ds_bpermute otherwise
+  template <class G, class P> __device__ void shfl_up(int d, G get, P put) {
+    const uint32_t x = get(lane);
+    uint32_t y;
+    if (d == 1) y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+    else y = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - d) << 2, (int)x);
+    put(lane, y, lane >= d);
   }
 };
 
@@ -186,14 +194,20 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   WaveLds* wl = reinterpret_cast<WaveLds*>(wbase);
   uint8_t* ring = wbase + sizeof(WaveLds);
   const uint32_t ring_lds = (uint32_t)(uintptr_t)smem + (uint32_t)(ring - smem);
+  // each wavefront scans a contiguous run of regions in file order, so the chain state of one
+  // region (ldb_chain.h) carries into the next
   const uint64_t gw = (uint64_t)blockIdx.x * kWPB + wave, nw = (uint64_t)gridDim.x * kWPB;
-  const uint64_t count = gw < p.nreg ? (p.nreg - gw + nw - 1) / nw : 0;
+  const uint64_t per = (p.nreg + nw - 1) / nw;
+  const uint64_t rb = gw * per;
+  const uint64_t count = rb < p.nreg ? (p.nreg - rb < per ? p.nreg - rb : per) : 0;
   GpuWave wp{lane};
+  ChainState st;
+  st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
   // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
-  // has read it for the last time (region_process's buffer_free), so the DMA overlaps the summary,
-  // its stores and the next region's wait.
+  // has read it for the last time (buffer_free), so the DMA overlaps the summary, its stores and
+  // the next region's wait.
   for (int b = 0; b < kNB; ++b)
-    if ((uint64_t)b < count) stage_dma(p.img, p.len, gw + (uint64_t)b * nw, ring_lds + b * kBuf, lane);
+    if ((uint64_t)b < count) stage_dma(p.img, p.len, rb + (uint64_t)b, ring_lds + b * kBuf, lane);
   for (uint64_t i = 0; i < count; ++i) {
     // Wait for region i's DMA: vmcnt(N) retires all but the N youngest VM ops (issue order, global
     // ops only in this kernel). Younger than DMA(i) are at least: in steady state the region
@@ -209,26 +223,29 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     }
     GpuWave::sync();
     wp.stamp(6);
-    const uint64_t r = gw + i * nw;
+    const uint64_t r = rb + i;
     const uint32_t slot = (uint32_t)(i % kNB);
     View v;
     v.buf = ring + slot * kBuf;
     v.tab = tab;
     v.xw = p.xw;
+    v.gsh = p.gsh;
     v.R0 = r * (uint64_t)kW;
     v.rlen = region_len(p, r);
     v.len = p.len;
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
     LanePriv q;
-    region_process(
-        wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LanePriv& { return q; },
+    ChainPriv cq;
+    run_region(
+        wp, v, ring + slot * kBuf, wl->sh, st, &wl->rs, [&](int) -> LanePriv& { return q; },
+        [&](int) -> ChainPriv& { return cq; },
         [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot_, pos, k, vv); },
         [&] {
           const uint64_t nx = i + kNB;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every LDS read of this buffer is back
           GpuWave::sync();
-          if (nx < count) stage_dma(p.img, p.len, gw + nx * nw, ring_lds + slot * kBuf, lane);
+          if (nx < count) stage_dma(p.img, p.len, rb + nx, ring_lds + slot * kBuf, lane);
         });
     write_region_wave(p, r, &wl->rs, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -264,6 +281,9 @@ struct CohRd {
   }
   __device__ uint64_t exitp(uint64_t r) const {
     return __hip_atomic_load(&p->rs[r].exitp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ uint32_t sflag(uint64_t r) const {
+    return __hip_atomic_load(&p->rs[r].sflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 };
 
@@ -308,6 +328,7 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
     v.buf = buf;
     v.tab = tab;
     v.xw = p.xw;
+    v.gsh = p.gsh;
     v.R0 = R0;
     v.rlen = region_len(p, r);
     v.len = p.len;

@@ -73,6 +73,12 @@ struct CpuWave {
   template <class F> uint32_t from(int src, F f) { return (uint32_t)f(src); }
   template <class F> uint64_t from64(int src, F f) { return (uint64_t)f(src); }
   template <class F> void single(F f) { f(); }
+  // put(l, value of lane l - d, l >= d) for every lane, all reads before any write
+  template <class G, class P> void shfl_up(int d, G get, P put) {
+    uint32_t t[kLanes];
+    for (int l = 0; l < kLanes; ++l) t[l] = get(l);
+    for (int l = 0; l < kLanes; ++l) { EMU_SET_LANE(l); put(l, l >= d ? t[l - d] : 0u, l >= d); }
+  }
   void stamp(int) {}
 };
 
@@ -94,12 +100,47 @@ struct Emu {
       buf[i] = (a >= 0 && (uint64_t)a < p.len) ? p.img[a] : (uint8_t)(garbage >> 56);
     }
   }
+  View view(const Pipe& p, uint64_t r) {
+    View v;
+    v.buf = buf.data();
+    v.tab = tab.data();
+    v.xw = xw.data();
+    v.gsh = gsh.data();
+    v.R0 = r * (uint64_t)kW;
+    v.rlen = region_len(p, r);
+    v.len = p.len;
+    v.io = p.io;
+    return v;
+  }
+  // one region of a wavefront's run (k_scan_main): chained fast path or region_process
+  RegionSum run_chained(const Pipe& p, uint64_t r, ChainState& st, uint32_t* n_fast) {
+    stage(p, r);
+    const View v = view(p, r);
+    RegionSum s;
+    CpuWave wp;
+    ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
+    LanePriv priv[kLanes];
+    ChainPriv cpriv[kLanes];
+    const uint32_t on = st.on;
+    run_region(wp, v, buf.data(), sh, st, &s, [&](int l) -> LanePriv& { return priv[l]; },
+               [&](int l) -> ChainPriv& { return cpriv[l]; },
+               [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
+                 sc[slot].pos = pos;
+                 sc[slot].k_size = k;
+                 sc[slot].v_size = vv;
+               }, [] {});
+    if (on && (s.sflag & kOwnerOk || s.start == kNone64)) ++*n_fast;
+    store_region(p, r, s);
+    EMU_FOLD();
+    return s;
+  }
   RegionSum run(const Pipe& p, uint64_t r, uint32_t enter) {
     stage(p, r);
     View v;
     v.buf = buf.data();
     v.tab = tab.data();
     v.xw = xw.data();
+    v.gsh = gsh.data();
     v.R0 = r * (uint64_t)kW;
     v.rlen = region_len(p, r);
     v.len = p.len;
@@ -123,12 +164,15 @@ struct Rd {
   const Pipe* p;
   uint64_t start(uint64_t r) const { return p->rs[r].start; }
   uint64_t exitp(uint64_t r) const { return p->rs[r].exitp; }
+  uint32_t sflag(uint64_t r) const { return p->rs[r].sflag; }
 };
 
 }  // namespace
 
-extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
-                        ldb_scan_result* res, uint32_t* stats) {
+// run_len: regions per wavefront run (k_scan_main gives each wave a contiguous run); 0 = every
+// region speculative (the pre-chain pipeline).
+extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                             ldb_scan_result* res, uint32_t* stats, uint64_t run_len) {
   Emu emu;
   const uint64_t nreg = std::max<uint64_t>(1, (len + kW - 1) / kW);
   const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
@@ -150,7 +194,16 @@ extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, 
     return 0;
   }
   // k_scan_main
-  for (uint64_t r = 0; r < nreg; ++r) emu.run(p, r, kForceSpec);
+  uint32_t n_fast = 0;
+  if (run_len == 0) {
+    for (uint64_t r = 0; r < nreg; ++r) emu.run(p, r, kForceSpec);
+  } else {
+    for (uint64_t r0 = 0; r0 < nreg; r0 += run_len) {
+      ChainState st;
+      st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
+      for (uint64_t r = r0; r < nreg && r < r0 + run_len; ++r) emu.run_chained(p, r, st, &n_fast);
+    }
+  }
   // k_link
   for (uint64_t r = 0; r < nreg; ++r) {
     if (link_broken(p, r)) {
@@ -207,6 +260,11 @@ extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, 
   res->end_off = tp;
   res->n_repairs = ctr[2];
   res->n_regions = (uint32_t)nreg;
-  if (stats) { stats[0] = nfail; stats[1] = ctr[2]; }
+  if (stats) { stats[0] = nfail; stats[1] = ctr[2]; stats[2] = n_fast; }
   return 0;
+}
+
+extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                        ldb_scan_result* res, uint32_t* stats) {
+  return emu_scan_runs(img, len, io, fid, out, cap, res, stats, 0);
 }

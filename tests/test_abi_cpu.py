@@ -44,20 +44,25 @@ def _emu():
         import subprocess
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "emu")], check=True)
     L = C.CDLL(so)
-    L.emu_scan.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_void_p, C.c_uint64,
-                           C.POINTER(coracle.ScanResult), C.c_void_p]
+    L.emu_scan_runs.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_void_p, C.c_uint64,
+                                C.POINTER(coracle.ScanResult), C.c_void_p, C.c_uint64]
     return L
 
 
-def emu_scan(img: np.ndarray, io: int):
+# regions per wavefront run: 0 = every region speculative (region_process only); >0 = contiguous
+# runs through the chained fast path (ldb_chain.h), as k_scan_main assigns them
+RUNS = [0, 1, 3, 64]
+
+
+def emu_scan(img: np.ndarray, io: int, run_len: int = 0):
     L = _emu()
     img = np.ascontiguousarray(img, dtype=np.uint8)
     cap = img.size // 5 + 8
     out = np.zeros(cap, coracle.INDEX_TUPLE)
     res = coracle.ScanResult()
-    st = np.zeros(2, np.uint32)
-    rc = L.emu_scan(img.ctypes.data if img.size else None, img.size, io, 0, out.ctypes.data, cap, C.byref(res),
-                    st.ctypes.data)
+    st = np.zeros(4, np.uint32)
+    rc = L.emu_scan_runs(img.ctypes.data if img.size else None, img.size, io, 0, out.ctypes.data, cap, C.byref(res),
+                         st.ctypes.data, run_len)
     assert rc == 0, rc
     return res, out[: res.n_entries], st
 
@@ -68,18 +73,20 @@ def assert_same(res, tup, ref, rt):
     assert np.array_equal(tup["k_size"], rt["k_size"]) and np.array_equal(tup["v_size"], rt["v_size"])
 
 
-def test_emulated_engine_golden(golden):
+@pytest.mark.parametrize("run_len", RUNS)
+def test_emulated_engine_golden(golden, run_len):
     meta, imgs = golden
     for m in meta:
         img = np.frombuffer(imgs[m["name"]], np.uint8)
-        res, tup, st = emu_scan(img, m["io_type"])
+        res, tup, st = emu_scan(img, m["io_type"], run_len)
         assert (res.status, res.end_off, res.n_entries) == (m["status"], m["end_off"], len(m["tuples"])), m["name"]
         want = [t[0] | (t[1] << 40) | (t[2] << 46) | (t[3] << 52) for t in m["tuples"]]
         assert list(tup["pos"]) == want, m["name"]
 
 
+@pytest.mark.parametrize("run_len", RUNS)
 @pytest.mark.parametrize("seed", range(4))
-def test_emulated_engine_random(seed):
+def test_emulated_engine_random(seed, run_len):
     from tests.golden import make_golden as G
     rng = random.Random(1000 + seed)
     cases = [
@@ -93,7 +100,7 @@ def test_emulated_engine_random(seed):
         for _ in range(rng.randrange(0, 3)):
             img[rng.randrange(img.size)] ^= rng.randrange(1, 256)
         for io in (0, 1):
-            res, tup, st = emu_scan(img, io)
+            res, tup, st = emu_scan(img, io, run_len)
             ref, rt = coracle.scan(img, io)
             assert_same(res, tup, ref, rt)
 
@@ -125,9 +132,10 @@ def _log_with_entry_at(target: int, big_value: int, seed: int) -> np.ndarray:
     return np.frombuffer(bytes(out) + bytes(64), np.uint8).copy()
 
 
-@pytest.mark.parametrize("d", [-5, -4, -3, -2, -1, 0, 1])
+@pytest.mark.parametrize("run_len", [0, 64])
+@pytest.mark.parametrize("d", [-9, -8, -7, -5, -4, -3, -2, -1, 0, 1])
 @pytest.mark.parametrize("big", [200, 6000, 12000])
-def test_emulated_span_starting_at_region_boundary(d, big):
+def test_emulated_span_starting_at_region_boundary(d, big, run_len):
     """The entry's CRC span (offset+4) starts d+4 bytes after region 1's start (d = -4..-1: the
     stored crc straddles the boundary; the k_combine skip path) and ends in the next region, a
     covered region later, or two regions later; both intact and with a flipped byte."""
@@ -138,6 +146,30 @@ def test_emulated_span_starting_at_region_boundary(d, big):
         if flip is not None:
             im[flip] ^= 0x20
         for io in (0, 1):
-            res, tup, st = emu_scan(im, io)
+            res, tup, st = emu_scan(im, io, run_len)
+            ref, rt = coracle.scan(im, io)
+            assert_same(res, tup, ref, rt)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_emulated_chained_path(seed):
+    """Contiguous runs through the chained fast path (ldb_chain.h): entry sizes 93 B .. ~1.1 KiB
+    put entry starts (and their stored-crc fields) at every offset of a slice, including the last
+    4 bytes (owner checked by the next lane) and the last 8 bytes of a region (fallback). Intact
+    logs must take the fast path for most regions; single-byte corruptions anywhere (headers,
+    crc fields, values) must give exactly the oracle's result."""
+    img, n, end = coracle.gen_log(600_000, 40 + seed, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=64)
+    nreg = (img.size + 5119) // 5120
+    res, tup, st = emu_scan(img, 0, 64)
+    ref, rt = coracle.scan(img, 0)
+    assert_same(res, tup, ref, rt)
+    assert st[2] >= 0.8 * nreg, (int(st[2]), nreg)      # regions done by the fast path
+    rng = random.Random(seed)
+    for _ in range(12):
+        im = img.copy()
+        at = rng.randrange(0, end)
+        im[at] ^= 1 << rng.randrange(8)
+        for io in (0, 1):
+            res, tup, st = emu_scan(im, io, 64)
             ref, rt = coracle.scan(im, io)
             assert_same(res, tup, ref, rt)
