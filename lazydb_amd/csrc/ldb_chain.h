@@ -36,6 +36,13 @@
 
 #include "ldb_wave.h"
 
+#ifdef LDB_EMU_COUNTERS   // CPU emulator instrumentation only: why region_chained declined a region
+namespace ldb { extern uint64_t g_chain_why[16]; }
+#define LDB_DECLINE(id) (++ldb::g_chain_why[id], false)
+#else
+#define LDB_DECLINE(id) false
+#endif
+
 namespace ldb {
 
 constexpr uint32_t kOwnerOk = 8u;     // sflag: owner of the region's first start CRC-verified in-wave
@@ -232,7 +239,8 @@ LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv) {
 template <class WP, class CPriv, class Emit>
 LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, RegionSum* out,
                            CPriv cpriv, Emit emit) {
-  if (!st.on || v.rlen != (uint32_t)kW || v.R0 + (uint64_t)(kW + kHalo) > v.len || st.x < v.R0) return false;
+  if (!st.on) return false;
+  if (v.rlen != (uint32_t)kW || v.R0 + (uint64_t)(kW + kHalo) > v.len || st.x < v.R0) return LDB_DECLINE(1);
   const uint64_t xr64 = st.x - v.R0;
   if (xr64 >= (uint64_t)kW) {
     // ---- covered region: the open entry runs through it; no header can start here
@@ -262,14 +270,14 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     }
     sh.s[l] = c.s;
   });
-  if (wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) return false;
+  if (wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) return LDB_DECLINE(2);
   // ---- links from the entry lane: each start's exit is the next start, no start in between
   uint64_t starts = 0;
   for (int it = 0;; ++it) {
     starts = wp.ballot([&](int l) { return cpriv(l).s != kNone32; });
     const uint64_t sts = starts;
     const int irr = wp.first([&](int l) { const ChainPriv& c = cpriv(l); return c.s != kNone32 && c.X - c.s < kMinFast; });
-    if (irr >= 0) return false;
+    if (irr >= 0) return LDB_DECLINE(3);
     const int j = wp.first([&](int l) {
       const ChainPriv& c = cpriv(l);
       if (c.s == kNone32) return false;
@@ -278,7 +286,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       return (between & sts) != 0 || (m < kLanes && sh.s[m] != c.X);
     });
     if (j < 0) break;
-    if (it == 3) return false;
+    if (it == 3) return LDB_DECLINE(5);
     const uint32_t Xj = wp.from(j, [&](int l) { return cpriv(l).X; });
     const int m = Xj >= (uint32_t)kW ? kLanes : (int)(Xj / kS);
     wp.each([&](int l) {
@@ -293,11 +301,11 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       }
       sh.s[l] = c.s;
     });
-    if (m < kLanes && wp.from(m, [&](int l) { return cpriv(l).s; }) == kNone32) return false;
+    if (m < kLanes && wp.from(m, [&](int l) { return cpriv(l).s; }) == kNone32) return LDB_DECLINE(6);
   }
   const int z = 63 - (int)__builtin_clzll(starts);
   const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).s; });
-  if (sz + 8 > (uint32_t)kW) return false;   // the rewrite of the last start would spill past the region
+  if (sz + 8 > (uint32_t)kW) return LDB_DECLINE(7);   // the rewrite of the last start would spill past the region
   // ---- owners, check assignment, buffer rewrite
   wp.each([&](int l) { sh.want[l] = ~cpriv(l).crc; });
   const uint32_t want_x = ~st.owner;
@@ -330,7 +338,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   const int bad = wp.first([&](int l) { const ChainPriv& c = cpriv(l); return c.chk && c.y != 0u; });
   if (bad >= 0) {
     wp.each([&](int l) { const ChainPriv& c = cpriv(l); if (c.s != kNone32) rewrite8(wbuf, c, false); });
-    return false;
+    return LDB_DECLINE(8);
   }
   // ---- tuples and summary
   wp.each([&](int l) {

@@ -51,15 +51,19 @@ constexpr int kRegionCap = kW / 10 + 8;   // tuple slots per region (entries >= 
 constexpr int kKeep = 2;                  // tuples a lane keeps in registers for emission
 
 // Table block (uint32 offsets) shared by every wave of a workgroup (LDS) / the emulator.
-// 8-byte CRC step: reg' = A(reg ^ w0) ^ B(w1), A = 64 bit-steps, B = 32 bit-steps, each as three
-// lookups on 11/11/10-bit chunks.
-constexpr int kTAOff = 0;                 // 2048 + 2048 + 1024
-constexpr int kTBOff = 5120;              // 2048 + 2048 + 1024
-constexpr int kT8Off = 10240;             // 256: byte-at-a-time table (rare paths)
-constexpr int kZSOff = 10496;             // 4 x 256: register shift by kS zero bytes (fold chains)
-constexpr int kKOff = 11520;              // kS + 1: K[n] = register after n zero bytes from ~0
+// 8-byte CRC step on 11/11/10-bit chunk tables. Default (LDB_CRC_AB=0): one table set S = shift by
+// 32 bits, reg' = S(S(reg ^ w0) ^ w1) (20 KB of LDS). LDB_CRC_AB=1: A = shift by 64 bits and
+// B = shift by 32 bits, reg' = A(reg ^ w0) ^ B(w1) (40 KB, B's lookups off the register chain).
+#ifndef LDB_CRC_AB
+#define LDB_CRC_AB 0
+#endif
+constexpr int kTAOff = 0;                 // 2048 + 2048 + 1024: A (LDB_CRC_AB) or S
+constexpr int kTBOff = LDB_CRC_AB ? 5120 : 0;   // 2048 + 2048 + 1024: B (LDB_CRC_AB) or S again
+constexpr int kT8Off = LDB_CRC_AB ? 10240 : 5120;   // 256: byte-at-a-time table (rare paths)
+constexpr int kZSOff = kT8Off + 256;      // 4 x 256: register shift by kS zero bytes (fold chains)
+constexpr int kKOff = kZSOff + 1024;      // kS + 1 (padded to 96): K[n] = register after n zero bytes from ~0
 // chained fast path (ldb_chain.h): register shifts as 4 byte-indexed tables of 256 each
-constexpr int kVSOff = 11616;             // 4 x 1024: shift by 8, 16, 32, 64 bytes (check-point shifts)
+constexpr int kVSOff = kKOff + 96;        // 4 x 1024: shift by 8, 16, 32, 64 bytes (check-point shifts)
 constexpr int kSCOff = kVSOff + 4 * 1024; // 5 x 1024: shift by 2, 4, 8, 16, 32 slices (lane scan; 1 slice = kZSOff)
 constexpr int kTabWords = kSCOff + 5 * 1024;
 constexpr int kTabBytes = kTabWords * 4;
@@ -84,7 +88,7 @@ inline void build_tables(uint32_t* tab) {
   const int off[3] = {0, 11, 22}, wid[3] = {11, 11, 10}, base[3] = {0, 2048, 4096};
   for (int q = 0; q < 3; ++q)
     for (uint32_t v = 0; v < (1u << wid[q]); ++v) {
-      tab[kTAOff + base[q] + v] = step_bits(v << off[q], 64);
+      if (LDB_CRC_AB) tab[kTAOff + base[q] + v] = step_bits(v << off[q], 64);
       tab[kTBOff + base[q] + v] = step_bits(v << off[q], 32);
     }
   for (uint32_t i = 0; i < 256; ++i) tab[kT8Off + i] = step_bits(i, 8);
@@ -143,9 +147,15 @@ LDB_HD uint32_t ctz64(uint64_t x) {
 // ---------------------------------------------------------------- CRC
 LDB_HD uint32_t crc_step8(const uint32_t* tab, uint32_t reg, uint32_t w0, uint32_t w1) {
   const uint32_t x = reg ^ w0;
+#if LDB_CRC_AB
   const uint32_t b = tab[kTBOff + (w1 & 0x7FFu)] ^ tab[kTBOff + 2048 + ((w1 >> 11) & 0x7FFu)] ^
                      tab[kTBOff + 4096 + (w1 >> 22)];
   return tab[kTAOff + (x & 0x7FFu)] ^ tab[kTAOff + 2048 + ((x >> 11) & 0x7FFu)] ^ tab[kTAOff + 4096 + (x >> 22)] ^ b;
+#else
+  const uint32_t y = tab[kTBOff + (x & 0x7FFu)] ^ tab[kTBOff + 2048 + ((x >> 11) & 0x7FFu)] ^
+                     tab[kTBOff + 4096 + (x >> 22)] ^ w1;
+  return tab[kTBOff + (y & 0x7FFu)] ^ tab[kTBOff + 2048 + ((y >> 11) & 0x7FFu)] ^ tab[kTBOff + 4096 + (y >> 22)];
+#endif
 }
 
 LDB_HD uint32_t mask_from(uint32_t nbytes) {  // bytes [nbytes, 4) kept, nbytes in [0, 4]

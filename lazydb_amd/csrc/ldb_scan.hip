@@ -33,7 +33,7 @@ using namespace ldb;
 namespace {
 
 #ifndef LDB_WPB
-#define LDB_WPB 12
+#define LDB_WPB 16
 #endif
 #ifndef LDB_NB
 #define LDB_NB 1

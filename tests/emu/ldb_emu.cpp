@@ -17,7 +17,8 @@
 using namespace ldb;
 
 #ifdef LDB_EMU_COUNTERS
-namespace ldb { int g_emu_lane; uint32_t g_emu_cnt[8][64]; }
+namespace ldb { int g_emu_lane; uint32_t g_emu_cnt[8][64]; uint64_t g_chain_why[16]; }
+extern "C" void emu_chain_why(uint64_t* out) { for (int i = 0; i < 16; ++i) { out[i] = ldb::g_chain_why[i]; ldb::g_chain_why[i] = 0; } }
 static uint64_t g_sum[8], g_max[8], g_regions;
 extern "C" void emu_counters(uint64_t* out) {   // [0..7] sums over lanes, [8..15] sums of per-region lane maxima, [16] regions
   for (int i = 0; i < 8; ++i) { out[i] = g_sum[i]; out[8 + i] = g_max[i]; g_sum[i] = g_max[i] = 0; }

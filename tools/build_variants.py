@@ -16,9 +16,9 @@ OUT = os.path.join(ROOT, "lazydb_amd", "_lib")
 
 def build(name: str) -> str:
     defs = []
-    m = re.fullmatch(r"w(\d+)n(\d+)", name)
+    m = re.fullmatch(r"(ab)?w(\d+)n(\d+)", name)
     if m:
-        defs = [f"-DLDB_WPB={m.group(1)}", f"-DLDB_NB={m.group(2)}"]
+        defs = [f"-DLDB_WPB={m.group(2)}", f"-DLDB_NB={m.group(3)}"] + (["-DLDB_CRC_AB=1"] if m.group(1) else [])
     elif name == "stamps":
         defs = ["-DLDB_STAMPS=1"]
     elif name == "stamps1":   # one wave per SIMD: phase stamps measure each wave's own critical path
