@@ -246,6 +246,8 @@ def main():
             "verified_vs_oracle": verified,
             "status": int(r.status),
             "repairs": int(r.n_repairs),
+            "fast_regions": int(r.n_fast),
+            "regions": int(r.n_regions),
         }
         if gather:
             line["gather"] = gather

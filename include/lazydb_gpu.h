@@ -100,6 +100,8 @@ typedef struct ldb_scan_result {
                             append position index.go:97-99 stores into LogFile.Offset */
   uint32_t n_repairs;    /* diagnostics: speculative-walk repairs performed (0 on well-formed logs) */
   uint32_t n_regions;    /* diagnostics: parallel regions the image was cut into */
+  uint32_t n_fast;       /* diagnostics: regions verified by the chained fast path (ldb_chain.h) */
+  uint32_t reserved_;
 } ldb_scan_result;
 
 /* ---- context ---------------------------------------------------------------

@@ -27,14 +27,15 @@ ENTRY_TUPLE = np.dtype([("offset", "<u8"), ("expired_at", "<i8"), ("tx_id", "<u8
 
 class ScanResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("fid", C.c_uint32), ("n_entries", C.c_uint64), ("end_off", C.c_uint64),
-                ("n_repairs", C.c_uint32), ("n_regions", C.c_uint32)]
+                ("n_repairs", C.c_uint32), ("n_regions", C.c_uint32),
+                ("n_fast", C.c_uint32), ("reserved_", C.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 RESULT_BYTES = C.sizeof(ScanResult)
-assert RESULT_BYTES == 32
+assert RESULT_BYTES == 40
 
 _lib = None
 

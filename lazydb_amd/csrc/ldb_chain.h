@@ -43,6 +43,13 @@ namespace ldb { extern uint64_t g_chain_why[16]; }
 #define LDB_DECLINE(id) false
 #endif
 
+// Timing ablations (tools/build_variants.py abl<N>; results are NOT valid in these builds):
+// bit 0: main-chain CRC without table lookups, bit 1: lane scan and check without lookups,
+// bit 2: no tuple stores. Checks always pass so the fast path runs.
+#ifndef LDB_ABLATE
+#define LDB_ABLATE 0
+#endif
+
 namespace ldb {
 
 constexpr uint32_t kOwnerOk = 8u;     // sflag: owner of the region's first start CRC-verified in-wave
@@ -56,8 +63,32 @@ struct ChainState {
   uint64_t x;        // absolute offset of the next entry start (>= region start)
 };
 
+// A wave-uniform value in a scalar register on the GPU (table lookups with it become scalar loads,
+// counted on lgkmcnt: a vector load's vmcnt wait would also wait for the region DMA in flight).
+LDB_HD uint32_t uniform(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+#else
+  return x;
+#endif
+}
+
+// shift_tab with a wave-uniform register on a global-memory table: on the GPU the table is read
+// through the constant address space so the four lookups are scalar loads (s_load, lgkmcnt).
+LDB_HD uint32_t shift_tab_uniform(const uint32_t* gtab, uint32_t r) {
+  r = uniform(r);
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const uint32_t __attribute__((address_space(4))) * cptr;
+  const cptr t = (cptr)gtab;
+  return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
+#else
+  return gtab[r & 0xFFu] ^ gtab[256 + ((r >> 8) & 0xFFu)] ^ gtab[512 + ((r >> 16) & 0xFFu)] ^ gtab[768 + (r >> 24)];
+#endif
+}
+
 // register shift by a fixed byte count: 4 lookups in a byte-indexed table set at `off`
 LDB_HD uint32_t shift_tab(const uint32_t* tab, int off, uint32_t r) {
+  if (LDB_ABLATE & 2) return (r << 1) ^ (r >> 3) ^ (uint32_t)off;
   return tab[off + (r & 0xFFu)] ^ tab[off + 256 + ((r >> 8) & 0xFFu)] ^ tab[off + 512 + ((r >> 16) & 0xFFu)] ^
          tab[off + 768 + (r >> 24)];
 }
@@ -86,17 +117,19 @@ struct Lean {
   uint32_t X;    // region-relative exit p + hs + k + vv
 };
 
-LDB_HD uint32_t byte_of(const uint32_t* w, uint32_t b) {   // window byte b in [4, 20) (else some byte)
+// Header-window bytes [b, b+4), b in [4, 20], from the window dwords w[0..5] (bytes 0..23).
+// Written as a chain of >= selects: an equality switch over the word index is turned into a
+// lookup in a private (scratch) array, whose vmcnt wait would also wait for the in-flight DMA.
+LDB_HD uint32_t win_word(const uint32_t* w, uint32_t b) {
   const uint32_t d = b >> 2;
-  const uint32_t x = d == 1 ? w[1] : d == 2 ? w[2] : d == 3 ? w[3] : w[4];
-  return (x >> (8 * (b & 3))) & 0xFFu;
-}
-
-LDB_HD uint32_t bytes4_at(const uint32_t* w, uint32_t b) {  // window bytes [b, b+4), b in [8, 20) (else some bytes)
-  const uint32_t d = b >> 2;
-  const uint32_t lo = d == 2 ? w[2] : d == 3 ? w[3] : w[4];
-  const uint32_t hi = d == 2 ? w[3] : d == 3 ? w[4] : w[5];
-  return funnel(hi, lo, b & 3);
+  uint32_t lo = w[1], hi = w[2];
+  lo = d >= 2u ? w[2] : lo;
+  hi = d >= 2u ? w[3] : hi;
+  lo = d >= 3u ? w[3] : lo;
+  hi = d >= 3u ? w[4] : hi;
+  lo = d >= 4u ? w[4] : lo;
+  hi = d >= 4u ? w[5] : hi;
+  return funnel(hi, lo, b & 3u);
 }
 
 LDB_HD uint32_t ctz_or(uint32_t x, uint32_t dflt) { return x ? (uint32_t)__builtin_ctz(x) : dflt; }
@@ -131,13 +164,13 @@ LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   // field lengths: expiredAt e0, txID e1-e0, txStat e2-e1 (== 1), kSize e3-e2, vSize e4-e3
   bool ok = e4 < 16u && e0 <= 5u && e1 - e0 <= 5u && e2 - e1 == 1u && e3 - e2 <= 4u && e4 - e3 <= 4u;
   const uint32_t stat = w[1] & 0xFFu;
-  const uint32_t ts = byte_of(w, 4 + e2);          // txStat byte: zz(0..2) = 0, 2, 4
+  const uint32_t ts = win_word(w, 4 + e2) & 0xFFu;   // txStat byte: zz(0..2) = 0, 2, 4
   ok = ok && stat <= 2u && (ts == 0u || ts == 2u || ts == 4u) && ((w[1] >> 8) & 1u) == 0u && w[0] != 0u;
   // minimal expiredAt / txID encodings (EncodeEntry re-emits them as read only then)
-  ok = ok && (e0 == 1u || byte_of(w, 4 + e0) != 0u) && (e1 - e0 == 1u || byte_of(w, 4 + e1) != 0u);
+  ok = ok && (e0 == 1u || (win_word(w, 4 + e0) & 0xFFu) != 0u) && (e1 - e0 == 1u || (win_word(w, 4 + e1) & 0xFFu) != 0u);
   bool ck, cv;
-  const uint32_t uk = field_value(bytes4_at(w, 5 + e2), e3 - e2, &ck);
-  const uint32_t uv = field_value(bytes4_at(w, 5 + e3), e4 - e3, &cv);
+  const uint32_t uk = field_value(win_word(w, (5 + e2) & 31u), e3 - e2, &ck);
+  const uint32_t uv = field_value(win_word(w, (5 + e3) & 31u), e4 - e3, &cv);
   ok = ok && ck && cv && (uk & 1u) == 0u && uk >= 2u && (uv & 1u) == 0u;
   const uint32_t hs = 5 + e4;
   const uint32_t k = uk >> 1, vv = uv >> 1;
@@ -174,27 +207,48 @@ LDB_HD uint32_t first_cand(const View& v, int B) {
   return best == 0xFFFFFFFFu ? kNone32 : (uint32_t)B + (best >> 3);
 }
 
-// Raw register over the slice (natural 8-byte grid), plus the check register: the register
-// before step kb continued by one step over that step's word masked with mlo.
-LDB_HD void crc_slice_cap(const View& v, int B, uint32_t kb, uint64_t mlo, uint32_t* y, uint32_t* yc) {
+// Raw register over the slice (natural 8-byte grid) as two independent chains, bytes [0, 48)
+// (steps 0-5) and [48, 80) (steps 6-9), joined by one shift of 32 bytes: half the dependent LDS
+// round trips of one 10-step chain. Also keeps, for the owner check, the register of the chain
+// holding step kb just before that step (*cap) and the step's word (*wc); *ya = the first chain.
+constexpr int kSplit = 6;   // steps in the first chain
+static_assert(kS == 80 && kSplit == 6, "slice split: 48 + 32 bytes (kVSOff shift-by-32 joins them)");
+
+LDB_HD void crc_slice_cap(const View& v, int B, uint32_t kb, uint32_t* y, uint32_t* ya, uint32_t* cap, uint64_t* wc) {
   const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
-  uint32_t reg = 0, cap = 0;
-  uint64_t wc = 0;
+  uint32_t ra = 0, rb = 0, c = 0;
+  uint64_t cw = 0;
+  Row16 q[kS / 16];
 #pragma unroll
-  for (int k2 = 0; k2 < kS / 16; ++k2) {
-    const Row16 q = row[k2];
+  for (int k2 = 0; k2 < kS / 16; ++k2) q[k2] = row[k2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t k = 2 * k2 + h;
-      const uint64_t w = ((uint64_t)q.w[2 * h + 1] << 32) | q.w[2 * h];
-      cap = k == kb ? reg : cap;
-      wc = k == kb ? w : wc;
-      reg = crc_step8(v.tab, reg, q.w[2 * h], q.w[2 * h + 1]);
+  for (int k = 0; k < kSplit; ++k) {   // interleaved: step k of chain A, step kSplit + k of chain B
+    {
+      const uint64_t w = ((uint64_t)q[k >> 1].w[2 * (k & 1) + 1] << 32) | q[k >> 1].w[2 * (k & 1)];
+      c = (uint32_t)k == kb ? ra : c;
+      cw = (uint32_t)k == kb ? w : cw;
+      ra = (LDB_ABLATE & 1) ? ((ra << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(v.tab, ra, (uint32_t)w, (uint32_t)(w >> 32));
+    }
+    const int kbb = kSplit + k;
+    if (kbb < kS / 8) {
+      const uint64_t w = ((uint64_t)q[kbb >> 1].w[2 * (kbb & 1) + 1] << 32) | q[kbb >> 1].w[2 * (kbb & 1)];
+      c = (uint32_t)kbb == kb ? rb : c;
+      cw = (uint32_t)kbb == kb ? w : cw;
+      rb = (LDB_ABLATE & 1) ? ((rb << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(v.tab, rb, (uint32_t)w, (uint32_t)(w >> 32));
     }
   }
-  *y = reg;
-  wc &= mlo;
-  *yc = crc_step8(v.tab, cap, (uint32_t)wc, (uint32_t)(wc >> 32));
+  *ya = ra;
+  *y = shift_tab(v.tab, kVSOff + 2 * 1024, ra) ^ rb;
+  *cap = c;
+  *wc = cw;
+}
+
+// Raw register over the whole slice (two chains as above).
+LDB_HD uint32_t crc_slice_raw2(const View& v, int B) {
+  uint32_t y, ya, cap;
+  uint64_t wc;
+  crc_slice_cap(v, B, 0, &y, &ya, &cap, &wc);
+  return y;
 }
 
 // Per-lane registers of the chained path.
@@ -205,8 +259,9 @@ struct ChainPriv {
   uint32_t wo;      // ~crc of its owner (injected at [s, s+4))
   uint32_t kb;      // check: capture step (or 0), chk: 1 if this lane checks an owner
   uint32_t chk;
-  uint64_t mlo;
-  uint32_t y, yc, O;
+  uint64_t mlo;     // bytes of the capture step's word that precede the checked entry's CRC span
+  uint64_t wc;      // that word
+  uint32_t y, ya, cap, O;
 };
 
 // Rewrite (inject = true) or restore the 8 bytes [s, s+8) of a start in the staging buffer.
@@ -222,36 +277,47 @@ LDB_HD void rewrite8(uint8_t* wbuf, const ChainPriv& c, bool inject) {
 }
 
 // Lane scan of the G-chain: O_l = sum_{i <= l} shift(y_i, (l - i) slices) (Hillis-Steele, 6 steps).
+template <int I, class WP, class CPriv>
+LDB_HD void scan_step(WP& wp, const uint32_t* tab, CPriv cpriv) {
+  constexpr int off = I == 0 ? kZSOff : kSCOff + (I - 1) * 1024;
+  wp.template shfl_up<(1 << I)>([&](int l) { return cpriv(l).O; },
+                                [&](int l, uint32_t t, bool valid) { if (valid) cpriv(l).O ^= shift_tab(tab, off, t); });
+}
+
 template <class WP, class CPriv>
 LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv) {
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int d = 1 << i;
-    const int off = i == 0 ? kZSOff : kSCOff + (i - 1) * 1024;
-    wp.shfl_up(d, [&](int l) { return cpriv(l).O; },
-               [&](int l, uint32_t t, bool valid) { if (valid) cpriv(l).O ^= shift_tab(tab, off, t); });
-  }
+  scan_step<0>(wp, tab, cpriv);
+  scan_step<1>(wp, tab, cpriv);
+  scan_step<2>(wp, tab, cpriv);
+  scan_step<3>(wp, tab, cpriv);
+  scan_step<4>(wp, tab, cpriv);
+  scan_step<5>(wp, tab, cpriv);
 }
 
 // The chained fast path for one region. Returns false (buffer restored, state untouched) when
 // the region must go through region_process instead. On success writes *out, emits the
 // region's tuples and advances `st`.
-template <class WP, class CPriv, class Emit>
+// `release()` is called once the staging buffer is no longer read (the caller may start refilling
+// it); if the region must then fall back, `restage()` reloads the region into the buffer first.
+template <class WP, class CPriv, class Emit, class Free, class Restage>
 LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, RegionSum* out,
-                           CPriv cpriv, Emit emit) {
+                           CPriv cpriv, Emit emit, Free release, Restage restage) {
   if (!st.on) return false;
   if (v.rlen != (uint32_t)kW || v.R0 + (uint64_t)(kW + kHalo) > v.len || st.x < v.R0) return LDB_DECLINE(1);
   const uint64_t xr64 = st.x - v.R0;
   if (xr64 >= (uint64_t)kW) {
     // ---- covered region: the open entry runs through it; no header can start here
-    wp.each([&](int l) { ChainPriv& c = cpriv(l); c.O = crc_slice_from(v, l * kS, 0); });
+    const uint32_t Ishift = shift_tab_uniform(v.gsh, st.I);   // build_gshift table kGsW: one region
+    wp.each([&](int l) { ChainPriv& c = cpriv(l); c.O = crc_slice_raw2(v, l * kS); });
+    release();
     lane_scan(wp, v.tab, cpriv);
     const uint32_t raw = wp.from(kLanes - 1, [&](int l) { return cpriv(l).O; });
+    wp.stamp(16);
     RegionSum r;
     r.start = kNone64; r.exitp = 0; r.soff = 0; r.status = kCont; r.count = 0;
     r.rpre = raw; r.rout = 0; r.scrc = 0; r.sflag = 0;
     wp.single([&] { *out = r; });
-    st.I = shift_tab(v.gsh, 0, st.I) ^ raw;   // build_gshift table kGsW: shift by one region
+    st.I = Ishift ^ raw;
     return true;
   }
   const uint32_t xr = (uint32_t)xr64;
@@ -270,7 +336,34 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     }
     sh.s[l] = c.s;
   });
+  wp.stamp(10);
   if (wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) return LDB_DECLINE(2);
+  // ---- pointer round: a lane without a plausible first candidate that the nearest start below
+  // lands in decodes at that exit (typically a true start whose first candidate was a stored-crc
+  // byte <= 2); one batched pass instead of one link repair per lane
+  {
+    wp.each([&](int l) { sh.raw[l] = cpriv(l).s != kNone32 ? cpriv(l).X : kNone32; });   // exits
+    const uint64_t sts = wp.ballot([&](int l) { return cpriv(l).s != kNone32; });
+    auto target = [&](int l) -> uint32_t {
+      const uint64_t below = sts & ((1ull << l) - 1);
+      if (cpriv(l).s != kNone32 || !below) return kNone32;
+      const uint32_t X = sh.raw[63 - (int)__builtin_clzll(below)];
+      return X < (uint32_t)kW && (int)(X / kS) == l ? X : kNone32;
+    };
+    if (wp.ballot([&](int l) { return target(l) != kNone32; })) {
+      wp.each([&](int l) {
+        ChainPriv& c = cpriv(l);
+        const uint32_t X = target(l);
+        if (X != kNone32) {
+          Lean e;
+          if (decode_lean(v, (int)X, &e)) {
+            c.s = X; c.X = e.X; c.crc = e.crc; c.k = e.k; c.vv = e.vv; c.w1 = e.w1; c.hs = e.hs; c.stat = e.stat;
+          }
+        }
+      });
+      wp.each([&](int l) { sh.s[l] = cpriv(l).s; });
+    }
+  }
   // ---- links from the entry lane: each start's exit is the next start, no start in between
   uint64_t starts = 0;
   for (int it = 0;; ++it) {
@@ -303,6 +396,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     });
     if (m < kLanes && wp.from(m, [&](int l) { return cpriv(l).s; }) == kNone32) return LDB_DECLINE(6);
   }
+  wp.stamp(11);
   const int z = 63 - (int)__builtin_clzll(starts);
   const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).s; });
   if (sz + 8 > (uint32_t)kW) return LDB_DECLINE(7);   // the rewrite of the last start would spill past the region
@@ -324,22 +418,38 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     c.mlo = nb ? (~0ull >> (64 - 8 * nb)) : 0ull;
     if (c.s != kNone32) rewrite8(wbuf, c, true);
   });
+  wp.stamp(12);
   // ---- one CRC chain per lane, lane scan, owner checks
-  wp.each([&](int l) { ChainPriv& c = cpriv(l); crc_slice_cap(v, l * kS, c.kb, c.mlo, &c.y, &c.yc); });
+  wp.each([&](int l) { ChainPriv& c = cpriv(l); crc_slice_cap(v, l * kS, c.kb, &c.y, &c.ya, &c.cap, &c.wc); });
+#ifndef LDB_LATE_RELEASE
+  release();   // last read of the staging buffer on the success path
+#endif
+  wp.stamp(13);
   const uint32_t I0 = shift_tab(v.tab, kZSOff, st.I);
   wp.each([&](int l) { ChainPriv& c = cpriv(l); c.O = c.y ^ (l == 0 ? I0 : 0u); });
   lane_scan(wp, v.tab, cpriv);
   const uint32_t Iin = st.I;
-  wp.shfl_up(1, [&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
+  wp.template shfl_up<1>([&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
     ChainPriv& c = cpriv(l);
+    if (!c.chk) return;   // lanes without a check stay off the LDS (fewer bank conflicts)
     const uint32_t g = valid ? t : Iin;   // G at the slice start
-    c.y = shift_8n(v.tab, g, c.kb + 1) ^ c.yc;   // check value (reuses y)
+    const uint64_t w = c.wc & c.mlo;
+    // G at P = slice start + 8 (kb + 1) = shift(G at the chain start, P - chain start) ^ the chain's
+    // register at P; the second chain starts at byte 48, where G = shift48(G) ^ (first chain)
+    const bool second = c.kb >= (uint32_t)kSplit;
+    const uint32_t base = second ? shift_tab(v.tab, kVSOff + 2 * 1024, shift_tab(v.tab, kVSOff + 1024, g)) ^ c.ya : g;
+    const uint32_t n = second ? c.kb + 1 - kSplit : c.kb + 1;
+    c.y = shift_8n(v.tab, base, n) ^ crc_step8(v.tab, c.cap, (uint32_t)w, (uint32_t)(w >> 32));
   });
-  const int bad = wp.first([&](int l) { const ChainPriv& c = cpriv(l); return c.chk && c.y != 0u; });
+  const int bad = LDB_ABLATE ? -1 : wp.first([&](int l) { const ChainPriv& c = cpriv(l); return c.chk && c.y != 0u; });
+#ifdef LDB_LATE_RELEASE
+  if (bad < 0) release();
+#endif
   if (bad >= 0) {
-    wp.each([&](int l) { const ChainPriv& c = cpriv(l); if (c.s != kNone32) rewrite8(wbuf, c, false); });
+    restage();   // the buffer may already hold the next region: reload this one (original bytes)
     return LDB_DECLINE(8);
   }
+  wp.stamp(14);
   // ---- tuples and summary
   wp.each([&](int l) {
     const ChainPriv& c = cpriv(l);
@@ -347,7 +457,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     const uint32_t slot = (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
     const uint64_t pos = ((v.R0 + c.s) & 0xFFFFFFFFFFull) | ((uint64_t)(c.hs & 0x3F) << 40) |
                          ((uint64_t)(c.hs & 0x3F) << 46) | ((uint64_t)(c.stat & 0xFF) << 52);
-    emit(slot, pos, c.k, c.vv);
+    if (!(LDB_ABLATE & 4)) emit(slot, pos, c.k, c.vv);
   });
   RegionSum r;
   r.start = v.R0 + xr;
@@ -363,18 +473,19 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   st.x = r.exitp;
   st.I = r.rout;
   st.owner = r.scrc;
+  wp.stamp(15);
   return true;
 }
 
 // One region of a wavefront's run: the chained fast path when the chain state allows it,
 // otherwise region_process (speculative at the start of a run, entry forced after a fallback).
-template <class WP, class Priv, class CPriv, class Emit, class Free>
-LDB_HD void run_region(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, RegionSum* out, Priv priv,
-                       CPriv cpriv, Emit emit, Free buffer_free) {
-  if (region_chained(wp, v, wbuf, sh, st, out, cpriv, emit)) {
-    buffer_free();
-    return;
-  }
+// buffer_free(): the staging buffer is no longer read (start refilling it); restage(): wait for any
+// refill in flight and reload this region's bytes into the buffer. Returns true when the chained
+// fast path did the region.
+template <class WP, class Priv, class CPriv, class Emit, class Free, class Restage>
+LDB_HD bool run_region(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, RegionSum* out, Priv priv,
+                       CPriv cpriv, Emit emit, Free buffer_free, Restage restage) {
+  if (region_chained(wp, v, wbuf, sh, st, out, cpriv, emit, buffer_free, restage)) return true;
   uint32_t enter = kForceSpec;
   if (st.on && st.x >= v.R0) enter = st.x - v.R0 < (uint64_t)v.rlen ? (uint32_t)(st.x - v.R0) : kForceNone;
   region_process(wp, v, sh, enter, out, priv, emit, buffer_free);
@@ -385,6 +496,7 @@ LDB_HD void run_region(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainSt
   st.x = r.exitp;
   st.I = r.rout;
   st.owner = r.scrc;
+  return false;
 }
 
 }  // namespace ldb

@@ -15,8 +15,11 @@
 
 #if defined(__HIPCC__)
 #define LDB_HD __host__ __device__ __forceinline__
+// out-of-line on the GPU: the rare general path must not shape the hot path's register allocation
+#define LDB_HD_COLD __host__ __device__ __attribute__((noinline))
 #else
 #define LDB_HD inline
+#define LDB_HD_COLD inline
 #endif
 
 namespace ldb {

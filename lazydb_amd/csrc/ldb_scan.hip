@@ -38,6 +38,9 @@ namespace {
 #ifndef LDB_NB
 #define LDB_NB 1
 #endif
+#ifndef LDB_SCAN_BPERM
+#define LDB_SCAN_BPERM 0   // 1: lane shifts of the scan by ds_bpermute instead of DPP / permlane swaps
+#endif
 constexpr int kWPB = LDB_WPB;  // wavefronts per workgroup in k_scan_main
 constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
 #ifndef LDB_BLOCKS_PER_CU
@@ -46,7 +49,7 @@ constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
 constexpr int kG = kW / 1024 + 1;  // LDS-DMA instructions per region (5 x 1 KiB + the halo)
 
 // ---------------------------------------------------------------- wave policy (SIMT)
-constexpr int kStampSlots = 10;   // phase ids of region_process / k_scan_main (tools/stamps.py)
+constexpr int kStampSlots = 18;   // phase ids of region_process / region_chained / k_scan_main (tools/stamps.py)
 struct GpuWave {
   int lane;
 #ifdef LDB_STAMPS
@@ -110,13 +113,35 @@ struct GpuWave {
     if (lane == 0) f();
     sync();
   }
-  // put(lane, value of lane - d, lane >= d): DPP wave_shr for d = 1, ds_bpermute otherwise
-  template <class G, class P> __device__ void shfl_up(int d, G get, P put) {
+  // Lanes shifted up by 16: permlane16_swap gives rows (R0, R0, R2, R2) and (R1, R1, R3, R3);
+  // permlane32_swap of the latter puts R1 into row 2.
+  __device__ static uint32_t up16(uint32_t x, int lane) {
+    const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);
+    return (lane >> 4) == 2 ? b[0] : a[0];
+  }
+  // put(lane, value of lane - D, lane >= D), all in VALU (DPP / permlane swaps, no LDS):
+  // D = 1 wave_shr; D = 32 permlane32_swap; D = 16 up16; D = 2, 4, 8 row_shr inside a row and, for
+  // the first D lanes of a row, row_ror moved up one row.
+  template <int D, class G, class P> __device__ void shfl_up(G get, P put) {
     const uint32_t x = get(lane);
     uint32_t y;
-    if (d == 1) y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
-    else y = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - d) << 2, (int)x);
-    put(lane, y, lane >= d);
+    if constexpr (D == 1) {
+      y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+    } else if constexpr (LDB_SCAN_BPERM) {
+      y = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - D) << 2, (int)x);
+    } else if constexpr (D == 32) {
+      y = __builtin_amdgcn_permlane32_swap(x, x, false, false)[0];
+    } else if constexpr (D == 16) {
+      y = up16(x, lane);
+    } else {
+      static_assert(D == 2 || D == 4 || D == 8, "lane shift");
+      const uint32_t in_row = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + D, 0xf, 0xf, false);
+      const uint32_t wrap = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x120 + D, 0xf, 0xf, false);
+      const uint32_t prev_row = up16(wrap, lane);
+      y = (lane & 15) >= D ? in_row : prev_row;
+    }
+    put(lane, y, lane >= D);
   }
 };
 
@@ -130,7 +155,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
                : "memory");
 }
 template <int N>
@@ -184,7 +209,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
   if (blockIdx.x == 0) {  // control words of the later stages (stream-ordered after this kernel)
-    if (threadIdx.x < 4) p.ctr[threadIdx.x] = 0;
+    if (threadIdx.x < 3) p.ctr[threadIdx.x] = 0;   // ctr[3] (fast regions) is counted here: k_serial zeroes it
     if (threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
   }
   __syncthreads();
@@ -203,6 +228,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   GpuWave wp{lane};
   ChainState st;
   st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
+  uint32_t n_fast = 0;
   // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
   // has read it for the last time (buffer_free), so the DMA overlaps the summary, its stores and
   // the next region's wait.
@@ -213,11 +239,12 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     // ops only in this kernel). Younger than DMA(i) are at least: in steady state the region
     // summary store of iteration i-kNB (>= 1 instruction) and, for kNB > 1, the DMAs of regions
     // i+1 .. i+kNB-1 (kG instructions each; their summary stores are not counted: conservative).
-    if (i >= (uint64_t)kNB) {
-      wait_vm<(kNB - 1) * kG + 1>();
-    } else {
-      const uint64_t ahead = (count < (uint64_t)kNB ? count : (uint64_t)kNB) - 1 - i;   // prologue DMAs after i
-      if (kNB >= 3 && ahead >= 2) wait_vm<2 * kG>();
+    // Near the end of the run fewer DMAs were issued after DMA(i) (none past the run's last region).
+    {
+      const uint64_t left = count - 1 - i;
+      const uint64_t ahead = left < (uint64_t)(kNB - 1) ? left : (uint64_t)(kNB - 1);   // DMAs issued after DMA(i)
+      if (ahead == (uint64_t)(kNB - 1) && i >= (uint64_t)kNB) wait_vm<(kNB - 1) * kG + 1>();
+      else if (kNB >= 3 && ahead >= 2) wait_vm<2 * kG>();
       else if (kNB >= 2 && ahead >= 1) wait_vm<kG>();
       else wait_vm<0>();
     }
@@ -237,7 +264,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
     LanePriv q;
     ChainPriv cq;
-    run_region(
+    n_fast += run_region(
         wp, v, ring + slot * kBuf, wl->sh, st, &wl->rs, [&](int) -> LanePriv& { return q; },
         [&](int) -> ChainPriv& { return cq; },
         [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot_, pos, k, vv); },
@@ -246,12 +273,21 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every LDS read of this buffer is back
           GpuWave::sync();
           if (nx < count) stage_dma(p.img, p.len, rb + nx, ring_lds + slot * kBuf, lane);
+        },
+        [&] {
+          // rare (a failed in-wave check): drain every DMA in flight, reload this region, wait for it
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          GpuWave::sync();
+          stage_dma(p.img, p.len, r, ring_lds + slot * kBuf, lane);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          GpuWave::sync();
         });
     write_region_wave(p, r, &wl->rs, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
     wp.stamp(7);
   }
+  if (lane == 0 && n_fast) atomicAdd(&p.ctr[3], n_fast);
 #ifdef LDB_STAMPS
   if (lane == 0)
     for (int k = 0; k < kStampSlots; ++k) atomicAdd((unsigned long long*)&g_stamps[k], (unsigned long long)wp.acc[k]);
@@ -467,6 +503,8 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
     res.end_off = tp;
     res.n_repairs = p.ctr[2];
     res.n_regions = (uint32_t)p.nreg;
+    res.n_fast = p.ctr[3];
+    res.reserved_ = 0;
     if (n > p.cap) res.status = LDB_ERR_CAPACITY;
     if (p.ctr[1]) res.status = kOverflow;  // k_serial redoes the scan
     *p.result = res;
@@ -491,7 +529,10 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
 // One lane walks the chain exactly like index.go:84-95 (global memory, byte-wise CRC).
 __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   if (threadIdx.x != 0) return;
-  if (only_on_overflow && !p.ctr[1]) return;
+  if (only_on_overflow && !p.ctr[1]) {
+    p.ctr[3] = 0;   // last kernel of the pipeline: leave the fast-region counter zeroed for the next scan
+    return;
+  }
   struct G {
     const uint8_t* q;
     __device__ uint32_t operator()(int i) const { return q[i]; }
@@ -530,7 +571,10 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   res.end_off = off;
   res.n_repairs = 0;
   res.n_regions = (uint32_t)p.nreg;
+  res.n_fast = 0;
+  res.reserved_ = 0;
   *p.result = res;
+  p.ctr[3] = 0;
 }
 
 size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
@@ -614,6 +658,7 @@ int ensure_ws(ldb_ctx* c, uint64_t bytes) {
   c->ws = nullptr;
   c->ws_bytes = 0;
   if (hipMalloc(&c->ws, bytes) != hipSuccess) return LDB_ERR_NOMEM;
+  if (hipMemset(c->ws, 0, 256) != hipSuccess) return LDB_ERR_HIP;   // control words (layout: ctr first)
   c->ws_bytes = bytes;
   return LDB_OK;
 }

@@ -75,7 +75,7 @@ struct CpuWave {
   template <class F> uint64_t from64(int src, F f) { return (uint64_t)f(src); }
   template <class F> void single(F f) { f(); }
   // put(l, value of lane l - d, l >= d) for every lane, all reads before any write
-  template <class G, class P> void shfl_up(int d, G get, P put) {
+  template <int d, class G, class P> void shfl_up(G get, P put) {
     uint32_t t[kLanes];
     for (int l = 0; l < kLanes; ++l) t[l] = get(l);
     for (int l = 0; l < kLanes; ++l) { EMU_SET_LANE(l); put(l, l >= d ? t[l - d] : 0u, l >= d); }
@@ -123,14 +123,21 @@ struct Emu {
     LanePriv priv[kLanes];
     ChainPriv cpriv[kLanes];
     const uint32_t on = st.on;
-    run_region(wp, v, buf.data(), sh, st, &s, [&](int l) -> LanePriv& { return priv[l]; },
+    bool released = false;
+    const bool fast = run_region(wp, v, buf.data(), sh, st, &s, [&](int l) -> LanePriv& { return priv[l]; },
                [&](int l) -> ChainPriv& { return cpriv[l]; },
                [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
                  sc[slot].pos = pos;
                  sc[slot].k_size = k;
                  sc[slot].v_size = vv;
-               }, [] {});
-    if (on && (s.sflag & kOwnerOk || s.start == kNone64)) ++*n_fast;
+               }, [&] { released = true; }, [&] {
+                 // the GPU refills the buffer at release: model it with garbage, then reload
+                 if (released) for (auto& b : buf) b = 0xA5;
+                 stage(p, r);
+                 released = false;
+               });
+    if (fast) ++*n_fast;
+    (void)on;
     store_region(p, r, s);
     EMU_FOLD();
     return s;

@@ -33,7 +33,7 @@ def test_library_exports_header_symbols():
 
 def test_struct_layouts_match_header():
     from lazydb_amd import _native as N
-    assert C.sizeof(N.ScanResult) == 32
+    assert C.sizeof(N.ScanResult) == 40
     assert N.INDEX_TUPLE.itemsize == 16 and N.ENTRY_TUPLE.itemsize == 48
     assert N.INDEX_TUPLE == coracle.INDEX_TUPLE and N.ENTRY_TUPLE == coracle.ENTRY_TUPLE
 

@@ -109,3 +109,17 @@ def test_config2_1gib_full_parity(eng):
     ref, rt = coracle.scan(img)
     assert_same(res, tup, ref, rt)
     assert res.status == 2 and res.n_repairs == 0
+    # the chained fast path (ldb_chain.h) must carry the scan: a broken lane shuffle or check would
+    # only show up here, as every region silently falling back to the exact general routine
+    assert res.n_fast >= 0.9 * res.n_regions, (res.n_fast, res.n_regions)
+
+
+def test_config3_shape_fast_path(eng):
+    """BASELINE config 3 shape (Zipf values 16 B .. 64 KiB) at 256 MiB: parity and fast-path share."""
+    img, n, end = coracle.gen_log(256 << 20, 2, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
+    res, tup = eng.scan_dev(to_dev(img), cap=n + 16)
+    ref, rt = coracle.scan(img)
+    assert_same(res, tup, ref, rt)
+    # ~13 regions per wavefront run at this size; each run starts speculative (region_process)
+    # and stays so across covered regions until its first entry start
+    assert res.n_fast >= 0.6 * res.n_regions, (res.n_fast, res.n_regions)

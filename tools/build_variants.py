@@ -19,6 +19,14 @@ def build(name: str) -> str:
     m = re.fullmatch(r"(ab)?w(\d+)n(\d+)", name)
     if m:
         defs = [f"-DLDB_WPB={m.group(2)}", f"-DLDB_NB={m.group(3)}"] + (["-DLDB_CRC_AB=1"] if m.group(1) else [])
+    elif name == "bperm":
+        defs = ["-DLDB_SCAN_BPERM=1"]
+    elif name == "late":
+        defs = ["-DLDB_LATE_RELEASE=1"]
+    elif name == "bpermlate":
+        defs = ["-DLDB_SCAN_BPERM=1", "-DLDB_LATE_RELEASE=1"]
+    elif name.startswith("abl"):
+        defs = [f"-DLDB_ABLATE={int(name[3:])}"]
     elif name == "stamps":
         defs = ["-DLDB_STAMPS=1"]
     elif name == "stamps1":   # one wave per SIMD: phase stamps measure each wave's own critical path
