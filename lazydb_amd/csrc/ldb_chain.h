@@ -108,8 +108,8 @@ LDB_HD uint32_t shift_8n(const uint32_t* tab, uint32_t r, uint32_t n) {
 // (db.go:473-523 -> EncodeEntry): canonical varints, expiredAt/txID <= 5 bytes, txStat one byte
 // of value 0..2, key/value sizes <= 4 bytes with kSize >= 1. For such a header Go's decode is
 // the plain one below, EncodeEntry re-emits the same header length, and ReadLogEntry returns
-// the entry (no sentinel; the caller guarantees the 38-byte window is readable and this checks
-// that the key/value bytes end strictly before the file end, i.e. within both bound rules).
+// the entry (no sentinel; this checks that the 38-byte header window and the key/value bytes
+// are readable under the IOController's bound rule).
 // Returns false for everything else (the exact decoder in region_process handles it).
 struct Lean {
   uint32_t crc, stat, hs, k, vv;
@@ -175,7 +175,8 @@ LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   const uint32_t hs = 5 + e4;
   const uint32_t k = uk >> 1, vv = uv >> 1;
   const uint32_t X = (uint32_t)p + hs + k + vv;
-  ok = ok && v.R0 + (uint64_t)X < v.len;   // key/value read within both IOController bound rules
+  ok = ok && !read_eof(v.len, v.io, (int64_t)(v.R0 + (uint64_t)p + hs), k + vv);   // key/value read (log_file.go:130-139)
+  ok = ok && !read_eof(v.len, v.io, (int64_t)(v.R0 + (uint64_t)p), kMaxHeader);   // header window (log_file.go:117-122)
   o->crc = w[0];
   o->stat = stat;
   o->hs = hs;
@@ -186,11 +187,21 @@ LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   return ok;
 }
 
-// First header candidate of slice [B, B+kS): smallest p with byte p+4 <= 2 (a Status byte,
-// log_entry.go:9-16), or kNone32. Speculation only.
-LDB_HD uint32_t first_cand(const View& v, int B) {
+// The ReadLogEntry statuses a chain may end on inside the lean path (log_file.go:117-126): the
+// header window past the file end, or the all-zero sentinel (10 zero bytes decode as crc 0,
+// stat 0 and five one-byte zero varints). kCont: anything else (region_process decides).
+LDB_HD int32_t lean_terminal(const View& v, uint32_t p) {
+  if (read_eof(v.len, v.io, (int64_t)(v.R0 + (uint64_t)p), kMaxHeader)) return LDB_EOF_WINDOW;
+  const uint32_t a = vword(v, (int)p), b = vword(v, (int)p + 4), c = vword(v, (int)p + 8) & 0xFFFFu;
+  return (a | b | c) == 0u ? LDB_EOF_SENTINEL : kCont;
+}
+
+// First header candidate of slice [B, B+kS) at or after slice offset `from`: smallest p with
+// byte p+4 <= 2 (a Status byte, log_entry.go:9-16), or kNone32. Speculation only.
+LDB_HD uint32_t first_cand(const View& v, int B, uint32_t from = 0) {
   const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
   uint32_t best = 0xFFFFFFFFu;
+  const uint32_t lo = from << 3;   // bit index of position `from` in the (qd << 5 | byte bit) order
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     const Row16 q = row[k];
@@ -198,7 +209,10 @@ LDB_HD uint32_t first_cand(const View& v, int B) {
     for (int j = 0; j < 4; ++j) {
       const int qd = 4 * k + j - 1;   // dword qd + 1 of the slice holds the stat bytes of positions 4qd..4qd+3
       if (qd < 0 || qd >= kS / 4) continue;
-      const uint32_t m = small_bytes(q.w[j]);   // lowest flagged byte is exact
+      uint32_t m = small_bytes(q.w[j]);   // lowest flagged byte is exact
+      // drop positions before `from` (only their flags can be borrow artefacts of a lower hit)
+      const int rel = (int)lo - (qd << 5);
+      m = rel <= 0 ? m : (rel >= 32 ? 0u : (m & (0xFFFFFFFFu << rel)));
       const uint32_t bit = m ? (uint32_t)__builtin_ctz(m) : 0xFFFFFFFFu;
       const uint32_t c = bit | ((uint32_t)qd << 5);
       best = c < best ? c : best;
@@ -214,40 +228,50 @@ LDB_HD uint32_t first_cand(const View& v, int B) {
 constexpr int kSplit = 6;   // steps in the first chain
 static_assert(kS == 80 && kSplit == 6, "slice split: 48 + 32 bytes (kVSOff shift-by-32 joins them)");
 
-LDB_HD void crc_slice_cap(const View& v, int B, uint32_t kb, uint32_t* y, uint32_t* ya, uint32_t* cap, uint64_t* wc) {
+struct SliceRows { Row16 q[kS / 16]; };
+
+LDB_HD SliceRows load_rows(const View& v, int B) {
   const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
-  uint32_t ra = 0, rb = 0, c = 0;
-  uint64_t cw = 0;
-  Row16 q[kS / 16];
+  SliceRows r;
 #pragma unroll
-  for (int k2 = 0; k2 < kS / 16; ++k2) q[k2] = row[k2];
+  for (int k2 = 0; k2 < kS / 16; ++k2) r.q[k2] = row[k2];
+  return r;
+}
+
+// kb == 10 (lane 63, a start in the region's last 4 bytes): the capture is after the whole slice,
+// over the 8 bytes past it (w10, from the staging buffer's halo).
+LDB_HD void crc_slice_cap(const uint32_t* tab, const SliceRows& rows, uint32_t kb, uint32_t* y, uint32_t* ya,
+                          uint32_t* cap, uint64_t* wc, uint64_t w10 = 0) {
+  const Row16* q = rows.q;
+  uint32_t ra = 0, rb = 0, c = 0;
+  uint64_t cw = w10;
 #pragma unroll
   for (int k = 0; k < kSplit; ++k) {   // interleaved: step k of chain A, step kSplit + k of chain B
     {
       const uint64_t w = ((uint64_t)q[k >> 1].w[2 * (k & 1) + 1] << 32) | q[k >> 1].w[2 * (k & 1)];
       c = (uint32_t)k == kb ? ra : c;
       cw = (uint32_t)k == kb ? w : cw;
-      ra = (LDB_ABLATE & 1) ? ((ra << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(v.tab, ra, (uint32_t)w, (uint32_t)(w >> 32));
+      ra = (LDB_ABLATE & 1) ? ((ra << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(tab, ra, (uint32_t)w, (uint32_t)(w >> 32));
     }
     const int kbb = kSplit + k;
     if (kbb < kS / 8) {
       const uint64_t w = ((uint64_t)q[kbb >> 1].w[2 * (kbb & 1) + 1] << 32) | q[kbb >> 1].w[2 * (kbb & 1)];
       c = (uint32_t)kbb == kb ? rb : c;
       cw = (uint32_t)kbb == kb ? w : cw;
-      rb = (LDB_ABLATE & 1) ? ((rb << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(v.tab, rb, (uint32_t)w, (uint32_t)(w >> 32));
+      rb = (LDB_ABLATE & 1) ? ((rb << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(tab, rb, (uint32_t)w, (uint32_t)(w >> 32));
     }
   }
   *ya = ra;
-  *y = shift_tab(v.tab, kVSOff + 2 * 1024, ra) ^ rb;
-  *cap = c;
+  *y = shift_tab(tab, kVSOff + 2 * 1024, ra) ^ rb;
+  *cap = kb == (uint32_t)(kS / 8) ? rb : c;   // chain B's register after the slice
   *wc = cw;
 }
 
 // Raw register over the whole slice (two chains as above).
-LDB_HD uint32_t crc_slice_raw2(const View& v, int B) {
+LDB_HD uint32_t crc_slice_raw2(const uint32_t* tab, const SliceRows& rows) {
   uint32_t y, ya, cap;
   uint64_t wc;
-  crc_slice_cap(v, B, 0, &y, &ya, &cap, &wc);
+  crc_slice_cap(tab, rows, 0, &y, &ya, &cap, &wc);
   return y;
 }
 
@@ -284,60 +308,127 @@ LDB_HD void scan_step(WP& wp, const uint32_t* tab, CPriv cpriv) {
                                 [&](int l, uint32_t t, bool valid) { if (valid) cpriv(l).O ^= shift_tab(tab, off, t); });
 }
 
-template <class WP, class CPriv>
-LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv) {
-  scan_step<0>(wp, tab, cpriv);
-  scan_step<1>(wp, tab, cpriv);
-  scan_step<2>(wp, tab, cpriv);
-  scan_step<3>(wp, tab, cpriv);
-  scan_step<4>(wp, tab, cpriv);
-  scan_step<5>(wp, tab, cpriv);
+// Segmented scan: lanes below `seg` and lanes from `seg` on are combined separately (seg = 0:
+// one segment).
+template <int I, class WP, class CPriv>
+LDB_HD void scan_step_seg(WP& wp, const uint32_t* tab, CPriv cpriv, int seg) {
+  constexpr int off = I == 0 ? kZSOff : kSCOff + (I - 1) * 1024;
+  constexpr int d = 1 << I;
+  wp.template shfl_up<d>([&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
+    if (valid && (l < seg || l - d >= seg)) cpriv(l).O ^= shift_tab(tab, off, t);
+  });
 }
 
-// The chained fast path for one region. Returns false (buffer restored, state untouched) when
-// the region must go through region_process instead. On success writes *out, emits the
-// region's tuples and advances `st`.
+template <class WP, class CPriv>
+LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv, int seg = 0) {
+  scan_step_seg<0>(wp, tab, cpriv, seg);
+  scan_step_seg<1>(wp, tab, cpriv, seg);
+  scan_step_seg<2>(wp, tab, cpriv, seg);
+  scan_step_seg<3>(wp, tab, cpriv, seg);
+  scan_step_seg<4>(wp, tab, cpriv, seg);
+  scan_step_seg<5>(wp, tab, cpriv, seg);
+}
+
+// The lean path for one region, in one of two modes:
+//   chained (st.on): the chain enters at st.x with the CRC state st.I / st.owner; the owner of the
+//     region's first start is CRC-checked here (kOwnerOk);
+//   speculative (!st.on; a run's first region, or after region_process): every lane speculates,
+//     the first plausible start L0 is taken as the chain's entry. Its owner is unknown, so its
+//     stored-crc field is rewritten to 0 and the region reports the A-form prefix register
+//     rpre = shift(raw([R0, s_L0)), end of L0's slice - s_L0) for k_combine (as region_process
+//     does); the lane scan is segmented at L0 so the G-chain starts clean there. k_link / k_repair
+//     verify the speculative entry like any region_process result.
+// Returns false (buffer restored, state untouched) when the region must go through region_process.
+// On success stores the summary, emits the region's tuples and advances `st` to chained mode.
 // `release()` is called once the staging buffer is no longer read (the caller may start refilling
 // it); if the region must then fall back, `restage()` reloads the region into the buffer first.
-template <class WP, class CPriv, class Emit, class Free, class Restage>
-LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, RegionSum* out,
-                           CPriv cpriv, Emit emit, Free release, Restage restage) {
-  if (!st.on) return false;
-  if (v.rlen != (uint32_t)kW || v.R0 + (uint64_t)(kW + kHalo) > v.len || st.x < v.R0) return LDB_DECLINE(1);
-  const uint64_t xr64 = st.x - v.R0;
-  if (xr64 >= (uint64_t)kW) {
-    // ---- covered region: the open entry runs through it; no header can start here
-    const uint32_t Ishift = shift_tab_uniform(v.gsh, st.I);   // build_gshift table kGsW: one region
-    wp.each([&](int l) { ChainPriv& c = cpriv(l); c.O = crc_slice_raw2(v, l * kS); });
-    release();
+// `store(r)` writes the region summary (called by every lane with the same r).
+template <class WP, class CPriv, class Emit, class Free, class Restage, class Store>
+LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, CPriv cpriv, Emit emit,
+                           Free release, Restage restage, Store store) {
+  const bool spec = !st.on;
+  if (!spec && st.x < v.R0) return LDB_DECLINE(1);
+  // covered region: raw register of the whole region (rpre); chained mode also advances st.I
+  auto covered = [&](bool chained) {
+    const uint32_t Ishift = chained ? shift_tab_uniform(v.gsh, st.I) : 0u;   // build_gshift kGsW: one region
+    // the slice's rows go to registers and the buffer is released at once: the next region's DMA
+    // overlaps this region's CRC chains, scan and summary
+    wp.each([&](int l) {
+      const SliceRows rows = load_rows(v, l * kS);
+      release();
+      cpriv(l).O = crc_slice_raw2(v.tab, rows);
+    });
     lane_scan(wp, v.tab, cpriv);
     const uint32_t raw = wp.from(kLanes - 1, [&](int l) { return cpriv(l).O; });
     wp.stamp(16);
     RegionSum r;
     r.start = kNone64; r.exitp = 0; r.soff = 0; r.status = kCont; r.count = 0;
     r.rpre = raw; r.rout = 0; r.scrc = 0; r.sflag = 0;
-    wp.single([&] { *out = r; });
-    st.I = Ishift ^ raw;
-    return true;
+    // the file ends in the region: raw register of [R0, len) (rare). The buffer is still intact
+    // although released: a partial region is the file's last, the last of its run (no refill).
+    if (v.rlen < (uint32_t)kW) {
+      const int q = (int)(v.rlen / kS), n = (int)(v.rlen % kS);
+      uint32_t reg = q > 0 ? wp.from(q - 1, [&](int l) { return cpriv(l).O; }) : 0u;
+      if (n) reg = multmodp(v.xw[n], reg);
+      uint32_t part = 0;
+      for (int i = 0; i < n; ++i) part = crc_byte(v.tab + kT8Off, part, vbyte(v, q * kS + i));
+      r.rpre = reg ^ part;
+    }
+    store(r);
+    if (chained) st.I = Ishift ^ raw;
+  };
+  uint32_t xr = 0;
+  int lt = -1;
+  if (!spec) {
+    const uint64_t xr64 = st.x - v.R0;
+    if (xr64 >= (uint64_t)kW) {   // the open entry runs through the region: no header can start here
+      covered(true);
+      return true;
+    }
+    xr = (uint32_t)xr64;
+    lt = (int)(xr / kS);
   }
-  const uint32_t xr = (uint32_t)xr64;
-  const int lt = (int)(xr / kS);
-  // ---- speculation: the entry lane decodes at x, later lanes at their first candidate
+  // ---- speculation: the entry lane decodes at x, later lanes (all lanes when speculative) at
+  // their first candidate
+  // chained: each lane decodes its first candidate (the pointer round recovers true starts behind
+  // a false candidate); speculative: lanes keep trying their next candidate until one decodes as
+  // a plausible header, since the region's entry lane L0 has no pointer to recover from
   wp.each([&](int l) {
     ChainPriv& c = cpriv(l);
     c.s = kNone32;
     c.chk = 0;
-    const uint32_t p = l < lt ? kNone32 : (l == lt ? xr : first_cand(v, l * kS));
-    if (p != kNone32) {
+    c.X = l == lt ? xr : (l > lt ? first_cand(v, l * kS) : kNone32);   // candidate (X reused)
+  });
+  for (int it = 0; it < (spec ? 6 : 1); ++it) {
+    wp.each([&](int l) {
+      ChainPriv& c = cpriv(l);
+      const uint32_t p = c.s == kNone32 ? c.X : kNone32;
+      if (p == kNone32) return;
       Lean e;
       if (decode_lean(v, (int)p, &e)) {
         c.s = p; c.X = e.X; c.crc = e.crc; c.k = e.k; c.vv = e.vv; c.w1 = e.w1; c.hs = e.hs; c.stat = e.stat;
+      } else {
+        const uint32_t nxt = p + 1 - (uint32_t)(l * kS);
+        c.X = (spec && nxt < (uint32_t)kS) ? first_cand(v, l * kS, nxt) : kNone32;
       }
-    }
-    sh.s[l] = c.s;
-  });
+    });
+    if (!spec || !wp.ballot([&](int l) { return cpriv(l).s == kNone32 && cpriv(l).X != kNone32; })) break;
+  }
+  wp.each([&](int l) { sh.s[l] = cpriv(l).s; });
   wp.stamp(10);
-  if (wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) return LDB_DECLINE(2);
+  // A chain may end inside the region on a terminal status (lean_terminal): tpos / tstat. Its last
+  // entry's owner check then runs at a check-only "pseudo start" at tpos (rewritten like a start,
+  // no tuple, not in `starts`).
+  uint32_t tpos = kNone32;
+  int32_t tstat = kCont;
+  uint64_t starts = 0;
+  if (!spec && wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) {
+    tstat = lean_terminal(v, xr);
+    if (tstat == kCont) return LDB_DECLINE(2);
+    tpos = xr;   // the chain enters on its terminal: nothing in the region is on it
+    wp.each([&](int l) { cpriv(l).s = kNone32; sh.s[l] = kNone32; });
+  }
+  if (tpos == kNone32) {
   // ---- pointer round: a lane without a plausible first candidate that the nearest start below
   // lands in decodes at that exit (typically a true start whose first candidate was a stored-crc
   // byte <= 2); one batched pass instead of one link repair per lane
@@ -365,7 +456,6 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     }
   }
   // ---- links from the entry lane: each start's exit is the next start, no start in between
-  uint64_t starts = 0;
   for (int it = 0;; ++it) {
     starts = wp.ballot([&](int l) { return cpriv(l).s != kNone32; });
     const uint64_t sts = starts;
@@ -394,25 +484,57 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       }
       sh.s[l] = c.s;
     });
-    if (m < kLanes && wp.from(m, [&](int l) { return cpriv(l).s; }) == kNone32) return LDB_DECLINE(6);
+    if (m < kLanes && wp.from(m, [&](int l) { return cpriv(l).s; }) == kNone32) {
+      // the verified chain from j ends at Xj unless a valid entry the lean decode rejects starts there
+      tstat = lean_terminal(v, Xj);
+      if (tstat == kCont) return LDB_DECLINE(6);
+      tpos = Xj;
+      wp.each([&](int l) {
+        if (l > j) cpriv(l).s = kNone32;
+        sh.s[l] = cpriv(l).s;
+      });
+      starts = wp.ballot([&](int l) { return cpriv(l).s != kNone32; });
+      break;
+    }
   }
+  }   // tpos == kNone32
   wp.stamp(11);
-  const int z = 63 - (int)__builtin_clzll(starts);
+  if (!starts && tpos == kNone32) {   // speculative, no plausible header anywhere: a covered region
+    covered(false);
+    return true;
+  }
+  if (tpos != kNone32) {   // the pseudo start (see above)
+    const int mt = (int)(tpos / kS);
+    wp.each([&](int l) {
+      ChainPriv& c = cpriv(l);
+      if (l == mt) { c.s = tpos; c.X = tpos; c.crc = 0; c.w1 = 0; }
+      sh.s[l] = c.s;
+    });
+  }
+  const int L0 = spec ? (int)__builtin_ctzll(starts) : lt;
+  const uint32_t sL0 = wp.from(L0, [&](int l) { return cpriv(l).s; });
+  const int z = starts ? 63 - (int)__builtin_clzll(starts) : L0;
   const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).s; });
-  if (sz + 8 > (uint32_t)kW) return LDB_DECLINE(7);   // the rewrite of the last start would spill past the region
+  // The last start's 8-byte rewrite may run past the region end (into the staged halo):
+  //   kW - sz in (4, 8): its CRC-init bytes straddle the end; the true init-based register at the
+  //     region end is the G-chain's ^ (~0 >> 8 * (bytes of the init inside the region));
+  //   kW - sz <= 4: its CRC span starts at/after the region end (region_process's kSkip case,
+  //     k_combine finishes it); its owner is checked in lane 63 over the halo (capture step 10).
+  const uint32_t tail = (uint32_t)kW - sz;
   // ---- owners, check assignment, buffer rewrite
   wp.each([&](int l) { sh.want[l] = ~cpriv(l).crc; });
-  const uint32_t want_x = ~st.owner;
+  const uint32_t want_x = spec ? 0u : ~st.owner;   // speculative: the entry's stored crc field becomes 0
   wp.each([&](int l) {
     ChainPriv& c = cpriv(l);
     const uint64_t below = starts & ((1ull << l) - 1);
     c.wo = below ? sh.want[63 - (int)__builtin_clzll(below)] : want_x;
     const uint32_t B = (uint32_t)(l * kS);
     uint32_t cs = kNone32;
-    if (c.s != kNone32 && c.s + 4 < B + kS) cs = c.s;
+    if (c.s != kNone32 && (c.s + 4 < B + kS || l == kLanes - 1)) cs = c.s;   // lane 63: P may be past E (halo)
     else if (l > 0 && sh.s[l - 1] != kNone32 && sh.s[l - 1] + 4 >= B) cs = sh.s[l - 1];
-    c.chk = cs != kNone32;
-    const uint32_t rel = cs != kNone32 ? cs + 4 - B : 0u;   // [0, kS)
+    // speculative: L0's owner is checked by k_combine (rpre); its capture only yields the prefix
+    c.chk = cs != kNone32 && !(spec && cs == sL0);
+    const uint32_t rel = cs != kNone32 ? cs + 4 - B : 0u;   // [0, kS + 4): kb == 10 only in lane 63
     c.kb = rel >> 3;
     const uint32_t nb = rel & 7u;
     c.mlo = nb ? (~0ull >> (64 - 8 * nb)) : 0ull;
@@ -420,14 +542,37 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   });
   wp.stamp(12);
   // ---- one CRC chain per lane, lane scan, owner checks
-  wp.each([&](int l) { ChainPriv& c = cpriv(l); crc_slice_cap(v, l * kS, c.kb, &c.y, &c.ya, &c.cap, &c.wc); });
+  wp.each([&](int l) {
+    ChainPriv& c = cpriv(l);
+    const SliceRows rows = load_rows(v, l * kS);   // the (rewritten) slice, the buffer's last read
+    const uint64_t w10 = (l == kLanes - 1 && c.kb == (uint32_t)(kS / 8))
+                             ? (((uint64_t)vword(v, kW + 4) << 32) | vword(v, kW)) : 0ull;   // halo
 #ifndef LDB_LATE_RELEASE
-  release();   // last read of the staging buffer on the success path
+    release();
 #endif
+    crc_slice_cap(v.tab, rows, c.kb, &c.y, &c.ya, &c.cap, &c.wc, w10);
+  });
   wp.stamp(13);
-  const uint32_t I0 = shift_tab(v.tab, kZSOff, st.I);
-  wp.each([&](int l) { ChainPriv& c = cpriv(l); c.O = c.y ^ (l == 0 ? I0 : 0u); });
-  lane_scan(wp, v.tab, cpriv);
+  uint32_t chainA = 0;   // speculative: shift(raw([B_L0, s_L0)), E_L0 - s_L0), lane L0's prefix contribution
+  if (spec) {
+    chainA = wp.from(L0, [&](int l) {
+      const ChainPriv& c = cpriv(l);
+      if (c.s + 4 >= (uint32_t)(l * kS + kS)) return c.y;   // [s, E) is the zeroed crc field: y is the prefix
+      const uint64_t w = c.wc & c.mlo;
+      const uint32_t loc = crc_step8(v.tab, c.cap, (uint32_t)w, (uint32_t)(w >> 32));   // chain-local, at P
+      const bool second = c.kb >= (uint32_t)kSplit;
+      const uint32_t at_p = second ? (shift_8n(v.tab, c.ya, c.kb + 1 - kSplit) ^ loc) : loc;   // slice-local
+      return shift_8n(v.tab, at_p, (uint32_t)(kS / 8 - 1) - c.kb);   // from P to the slice end
+    });
+  }
+  const uint32_t I0 = spec ? 0u : shift_tab(v.tab, kZSOff, st.I);
+  wp.each([&](int l) {
+    ChainPriv& c = cpriv(l);
+    c.O = c.y ^ (l == 0 ? I0 : 0u) ^ (spec && l == L0 ? chainA : 0u);
+  });
+  lane_scan(wp, v.tab, cpriv, spec ? L0 : 0);
+  uint32_t rpre = 0;
+  if (spec) rpre = (L0 > 0 ? shift_tab(v.tab, kZSOff, wp.from(L0 - 1, [&](int l) { return cpriv(l).O; })) : 0u) ^ chainA;
   const uint32_t Iin = st.I;
   wp.template shfl_up<1>([&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
     ChainPriv& c = cpriv(l);
@@ -453,23 +598,38 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   // ---- tuples and summary
   wp.each([&](int l) {
     const ChainPriv& c = cpriv(l);
-    if (c.s == kNone32) return;
+    if (!((starts >> l) & 1u)) return;   // no entry (or the pseudo start)
     const uint32_t slot = (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
     const uint64_t pos = ((v.R0 + c.s) & 0xFFFFFFFFFFull) | ((uint64_t)(c.hs & 0x3F) << 40) |
                          ((uint64_t)(c.hs & 0x3F) << 46) | ((uint64_t)(c.stat & 0xFF) << 52);
     if (!(LDB_ABLATE & 4)) emit(slot, pos, c.k, c.vv);
   });
   RegionSum r;
-  r.start = v.R0 + xr;
+  r.start = v.R0 + sL0;
+  if (tpos != kNone32) {   // the chain ends here (status at tpos, as region_process reports it)
+    r.status = tstat;
+    r.count = (uint32_t)__builtin_popcountll(starts);
+    r.exitp = v.R0 + tpos;
+    r.soff = 0; r.scrc = 0; r.rout = 0;
+    r.rpre = rpre;
+    r.sflag = spec ? 0u : kOwnerOk;
+    store(r);
+    st.on = 0;
+    wp.stamp(15);
+    return true;
+  }
   r.status = kCont;
   r.count = (uint32_t)__builtin_popcountll(starts);
   r.exitp = v.R0 + wp.from(z, [&](int l) { return cpriv(l).X; });
   r.soff = v.R0 + sz;
   r.scrc = wp.from(z, [&](int l) { return cpriv(l).crc; });
   r.rout = wp.from(kLanes - 1, [&](int l) { return cpriv(l).O; });
-  r.rpre = 0;
-  r.sflag = kStraddle | kOwnerOk;
-  wp.single([&] { *out = r; });
+  if (tail > 4 && tail < 8) r.rout ^= 0xFFFFFFFFu >> (8 * (tail - 4));
+  r.rpre = rpre;
+  r.sflag = spec ? kStraddle : (kStraddle | kOwnerOk);
+  if (tail <= 4) { r.sflag |= kSkip; r.rout = 0; }
+  store(r);
+  st.on = tail > 4 ? 1u : 0u;   // after a kSkip straddler the next region starts speculative
   st.x = r.exitp;
   st.I = r.rout;
   st.owner = r.scrc;
@@ -482,10 +642,12 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
 // buffer_free(): the staging buffer is no longer read (start refilling it); restage(): wait for any
 // refill in flight and reload this region's bytes into the buffer. Returns true when the chained
 // fast path did the region.
-template <class WP, class Priv, class CPriv, class Emit, class Free, class Restage>
+// The fast path stores its summary with store(r); after region_process it is in *out (the caller
+// stores it).
+template <class WP, class Priv, class CPriv, class Emit, class Free, class Restage, class Store>
 LDB_HD bool run_region(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, RegionSum* out, Priv priv,
-                       CPriv cpriv, Emit emit, Free buffer_free, Restage restage) {
-  if (region_chained(wp, v, wbuf, sh, st, out, cpriv, emit, buffer_free, restage)) return true;
+                       CPriv cpriv, Emit emit, Free buffer_free, Restage restage, Store store) {
+  if (region_chained(wp, v, wbuf, sh, st, cpriv, emit, buffer_free, restage, store)) return true;
   uint32_t enter = kForceSpec;
   if (st.on && st.x >= v.R0) enter = st.x - v.R0 < (uint64_t)v.rlen ? (uint32_t)(st.x - v.R0) : kForceNone;
   region_process(wp, v, sh, enter, out, priv, emit, buffer_free);

@@ -28,7 +28,8 @@ struct Pipe {
   ldb_index_tuple* scratch;   // nreg * kRegionCap
   // control
   int64_t* fail_src;          // regions whose outgoing link failed (-1: region 0 does not start at 0)
-  uint32_t* ctr;              // [0] fail count, [1] overflow, [2] repairs, [3] first terminal region (min)
+  uint32_t* defer;            // regions k_scan_main left to k_fallback (region_process)
+  uint32_t* ctr;              // [0] fail count, [1] overflow, [2] repairs, [3] fast regions, [4] deferred
   uint64_t* tpos;             // [0] min terminal position, [1] its status (packed with position)
   uint64_t* blk;              // per kBlkRegions-region block: count sum (k_combine)
   void* out;

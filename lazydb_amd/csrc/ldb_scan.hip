@@ -198,6 +198,28 @@ __device__ __forceinline__ void write_region_wave(const Pipe& p, uint64_t r, con
   }
 }
 
+// Global -> LDS copy of the table block: 16-B loads, kBatch of them in flight per thread before
+// the stores (one global round trip per batch, not per word).
+static_assert(kTabWords % 4 == 0, "table block is a whole number of 16-B words");
+__device__ __forceinline__ void copy_tables(uint32_t* tab, const uint32_t* gtab) {
+  constexpr int kQ = kTabWords / 4, kBatch = 8;
+  const uint4* g = reinterpret_cast<const uint4*>(gtab);
+  uint4* t = reinterpret_cast<uint4*>(tab);
+  for (int i0 = 0; i0 < kQ; i0 += kBatch * (int)blockDim.x) {
+    uint4 x[kBatch];
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int i = i0 + b * (int)blockDim.x + (int)threadIdx.x;
+      if (i < kQ) x[b] = g[i];
+    }
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int i = i0 + b * (int)blockDim.x + (int)threadIdx.x;
+      if (i < kQ) t[i] = x[b];
+    }
+  }
+}
+
 #ifdef LDB_STAMPS
 __device__ uint64_t g_stamps[kStampSlots];
 #endif
@@ -207,7 +229,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   // folds the table base into the ds_read offset field
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
+  copy_tables(tab, p.gtab);
   if (blockIdx.x == 0) {  // control words of the later stages (stream-ordered after this kernel)
     if (threadIdx.x < 3) p.ctr[threadIdx.x] = 0;   // ctr[3] (fast regions) is counted here: k_serial zeroes it
     if (threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
@@ -262,27 +284,58 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     v.len = p.len;
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    LanePriv q;
     ChainPriv cq;
-    n_fast += run_region(
-        wp, v, ring + slot * kBuf, wl->sh, st, &wl->rs, [&](int) -> LanePriv& { return q; },
-        [&](int) -> ChainPriv& { return cq; },
+#if LDB_ABLATE >= 16
+    {   // timing skeletons (results invalid): 16 = DMA only, 32 = + slice CRC, 64 = + lane scan
+      uint32_t acc = 0;
+      if (LDB_ABLATE >= 32) {
+        const SliceRows rows = load_rows(v, lane * kS);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GpuWave::sync();
+        if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
+        cq.O = crc_slice_raw2(v.tab, rows);
+        if (LDB_ABLATE >= 64) lane_scan(wp, v.tab, [&](int) -> ChainPriv& { return cq; });
+        acc = wp.from(kLanes - 1, [&](int) { return cq.O; });
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GpuWave::sync();
+        if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
+      }
+      RegionSum s;
+      s.start = kNone64; s.exitp = 0; s.soff = 0; s.status = kCont; s.count = 0; s.rpre = acc; s.rout = 0;
+      s.scrc = 0; s.sflag = 0;
+      if (lane == 0) p.rs[r] = s;
+      n_fast += 1;
+      continue;
+    }
+#endif
+    bool released = false;
+    const bool fast = region_chained(
+        wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },
         [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot_, pos, k, vv); },
-        [&] {
+        [&] {   // the buffer's last read is behind us: stage the run's region i + kNB into it
           const uint64_t nx = i + kNB;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every LDS read of this buffer is back
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           GpuWave::sync();
           if (nx < count) stage_dma(p.img, p.len, rb + nx, ring_lds + slot * kBuf, lane);
+          released = true;
         },
-        [&] {
-          // rare (a failed in-wave check): drain every DMA in flight, reload this region, wait for it
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          GpuWave::sync();
-          stage_dma(p.img, p.len, r, ring_lds + slot * kBuf, lane);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          GpuWave::sync();
+        [] {},   // a deferred region is re-read from global memory by k_fallback
+        [&](const RegionSum& s) {   // straight from registers: one lane, three 16-B stores
+          if (lane == 0) p.rs[r] = s;
         });
-    write_region_wave(p, r, &wl->rs, lane);
+    if (fast) {
+      ++n_fast;
+    } else {
+      // leave the region to k_fallback (the exact general routine); the run goes on speculatively
+      if (!released) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GpuWave::sync();
+        if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
+      }
+      if (lane == 0) p.defer[atomicAdd(&p.ctr[4], 1u)] = (uint32_t)r;
+      st.on = 0;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
     wp.stamp(7);
@@ -292,6 +345,53 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   if (lane == 0)
     for (int k = 0; k < kStampSlots; ++k) atomicAdd((unsigned long long*)&g_stamps[k], (unsigned long long)wp.acc[k]);
 #endif
+}
+
+// ---------------------------------------------------------------- k_fallback
+// The regions k_scan_main deferred, each through region_process (speculative entry, exactly as
+// the pre-chain pipeline did every region); k_link / k_repair / k_combine then verify them like
+// any other region. Staging is synchronous (rare regions).
+constexpr int kFbWaves = 4;
+__global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p) {
+  const uint32_t n = p.ctr[4];
+  if ((uint64_t)blockIdx.x * kFbWaves >= n) return;   // no deferred region for this block
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  copy_tables(tab, p.gtab);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  WaveLds* wl = reinterpret_cast<WaveLds*>(smem + wave * (sizeof(WaveLds) + kBuf));
+  uint8_t* buf = smem + wave * (sizeof(WaveLds) + kBuf) + sizeof(WaveLds);
+  GpuWave wp{lane};
+  for (uint32_t d = blockIdx.x * kFbWaves + wave; d < n; d += gridDim.x * kFbWaves) {
+    const uint64_t r = p.defer[d];
+    const uint64_t R0 = r * (uint64_t)kW;
+    for (int k = lane; k < (kW + kHalo) / 16; k += 64) {
+      const uint64_t off = R0 + (uint64_t)k * 16;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (off < p.len) x = *reinterpret_cast<const uint4*>(p.img + off);
+      *reinterpret_cast<uint4*>(buf + kPre + k * 16) = x;
+    }
+    GpuWave::sync();
+    View v;
+    v.buf = buf;
+    v.tab = tab;
+    v.xw = p.xw;
+    v.gsh = p.gsh;
+    v.R0 = R0;
+    v.rlen = region_len(p, r);
+    v.len = p.len;
+    v.io = p.io;
+    ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
+    LanePriv q;
+    region_process(
+        wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LanePriv& { return q; },
+        [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); }, [] {});
+    write_region_wave(p, r, &wl->rs, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    GpuWave::sync();
+  }
 }
 
 // ---------------------------------------------------------------- k_link
@@ -330,7 +430,7 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
   // folds the table base into the ds_read offset field
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = p.gtab[i];
+  copy_tables(tab, p.gtab);
   WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
   uint8_t* buf = smem + sizeof(WaveLds);
   __syncthreads();
@@ -530,7 +630,8 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
 __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   if (threadIdx.x != 0) return;
   if (only_on_overflow && !p.ctr[1]) {
-    p.ctr[3] = 0;   // last kernel of the pipeline: leave the fast-region counter zeroed for the next scan
+    p.ctr[3] = 0;   // last kernel of the pipeline: leave the counters k_scan_main adds to zeroed
+    p.ctr[4] = 0;
     return;
   }
   struct G {
@@ -575,10 +676,12 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   res.reserved_ = 0;
   *p.result = res;
   p.ctr[3] = 0;
+  p.ctr[4] = 0;
 }
 
 size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
 size_t repair_lds_bytes() { return sizeof(WaveLds) + kBuf; }
+size_t fallback_lds_bytes() { return kFbWaves * (sizeof(WaveLds) + kBuf); }
 
 }  // namespace
 
@@ -627,7 +730,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -642,11 +745,12 @@ WsLayout layout(uint64_t len) {
     return at;
   };
   // control words first (one memset covers ctr, tpos, blk)
-  L.o_ctr = take(16);
+  L.o_ctr = take(32);
   L.o_tpos = take(16);
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1));
+  L.o_defer = take(4 * L.nreg);
   L.o_scratch = take(sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg);
   L.total = o;
   return L;
@@ -678,6 +782,7 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.rs = reinterpret_cast<RegionSum*>(w + L.o_rs);
   p.scratch = reinterpret_cast<ldb_index_tuple*>(w + L.o_scratch);
   p.fail_src = reinterpret_cast<int64_t*>(w + L.o_fail);
+  p.defer = reinterpret_cast<uint32_t*>(w + L.o_defer);
   p.ctr = reinterpret_cast<uint32_t*>(w + L.o_ctr);
   p.tpos = reinterpret_cast<uint64_t*>(w + L.o_tpos);
   p.blk = reinterpret_cast<uint64_t*>(w + L.o_blk);
@@ -702,7 +807,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   const Pipe p = make_pipe(c, L, d_img, len, fid, io, kind, d_out, cap, d_res);
   if (serial || len < (uint64_t)kMaxHeader) {
     // control words for k_serial (the parallel pipeline has k_scan_main initialise them)
-    LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 16, s));
+    LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
     LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 0);
     return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
@@ -732,6 +837,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   hipLaunchKernelGGL(k_scan_main, dim3(grid), dim3(64 * kWPB), main_lds_bytes(), s, p);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   const int g256 = (int)((L.nreg + 255) / 256);
+  hipLaunchKernelGGL(k_fallback, dim3(c->n_cu), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p);
   hipLaunchKernelGGL(k_link, dim3(g256), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_repair, dim3(1), dim3(64), repair_lds_bytes(), s, p);
   hipLaunchKernelGGL(k_combine, dim3(g256), dim3(256), 0, s, p);
@@ -792,7 +898,9 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
   if (hipFuncSetAttribute((const void*)k_scan_main, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)main_lds_bytes()) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_repair, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)repair_lds_bytes()) != hipSuccess) {
+                          (int)repair_lds_bytes()) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_fallback, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)fallback_lds_bytes()) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }

@@ -113,34 +113,26 @@ struct Emu {
     v.io = p.io;
     return v;
   }
-  // one region of a wavefront's run (k_scan_main): chained fast path or region_process
-  RegionSum run_chained(const Pipe& p, uint64_t r, ChainState& st, uint32_t* n_fast) {
+  // one region of a wavefront's run (k_scan_main): the lean path, or deferred to k_fallback
+  bool run_chained(const Pipe& p, uint64_t r, ChainState& st) {
     stage(p, r);
     const View v = view(p, r);
-    RegionSum s;
     CpuWave wp;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    LanePriv priv[kLanes];
     ChainPriv cpriv[kLanes];
-    const uint32_t on = st.on;
     bool released = false;
-    const bool fast = run_region(wp, v, buf.data(), sh, st, &s, [&](int l) -> LanePriv& { return priv[l]; },
-               [&](int l) -> ChainPriv& { return cpriv[l]; },
-               [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
-                 sc[slot].pos = pos;
-                 sc[slot].k_size = k;
-                 sc[slot].v_size = vv;
-               }, [&] { released = true; }, [&] {
-                 // the GPU refills the buffer at release: model it with garbage, then reload
-                 if (released) for (auto& b : buf) b = 0xA5;
-                 stage(p, r);
-                 released = false;
-               });
-    if (fast) ++*n_fast;
-    (void)on;
-    store_region(p, r, s);
+    const bool fast = region_chained(
+        wp, v, buf.data(), sh, st, [&](int l) -> ChainPriv& { return cpriv[l]; },
+        [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
+          sc[slot].pos = pos;
+          sc[slot].k_size = k;
+          sc[slot].v_size = vv;
+        },
+        [&] { released = true; }, [] {}, [&](const RegionSum& rs) { store_region(p, r, rs); });
+    if (!fast) st.on = 0;
+    (void)released;
     EMU_FOLD();
-    return s;
+    return fast;
   }
   RegionSum run(const Pipe& p, uint64_t r, uint32_t enter) {
     stage(p, r);
@@ -206,11 +198,16 @@ extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t 
   if (run_len == 0) {
     for (uint64_t r = 0; r < nreg; ++r) emu.run(p, r, kForceSpec);
   } else {
-    for (uint64_t r0 = 0; r0 < nreg; r0 += run_len) {
+    std::vector<uint64_t> deferred;
+    for (uint64_t r0 = 0; r0 < nreg; r0 += run_len) {   // k_scan_main
       ChainState st;
       st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
-      for (uint64_t r = r0; r < nreg && r < r0 + run_len; ++r) emu.run_chained(p, r, st, &n_fast);
+      for (uint64_t r = r0; r < nreg && r < r0 + run_len; ++r) {
+        if (emu.run_chained(p, r, st)) ++n_fast;
+        else deferred.push_back(r);
+      }
     }
+    for (uint64_t r : deferred) emu.run(p, r, kForceSpec);   // k_fallback
   }
   // k_link
   for (uint64_t r = 0; r < nreg; ++r) {

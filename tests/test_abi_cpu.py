@@ -173,3 +173,31 @@ def test_emulated_chained_path(seed):
             res, tup, st = emu_scan(im, io, 64)
             ref, rt = coracle.scan(im, io)
             assert_same(res, tup, ref, rt)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_emulated_file_end(seed):
+    """End of file on the chained fast path (ldb_chain.h lean_terminal / covered tail region): logs
+    cut at many lengths (inside entries: EOF_KV, window EOF, CRC errors once zero padding follows)
+    and clean ends (exactly at the last entry, or zero padding: EOF_WINDOW / sentinel / a covered
+    zero tail region), both IOController bound rules; every result must be the oracle's, and clean
+    ends must stay on the fast path for every region (except the mmap rule's EOF_KV on an entry
+    that ends exactly at the file end, log_file.go:130-139, which region_process reports)."""
+    base, n, end = coracle.gen_log(60_000 + 1000 * seed, 7 + seed, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=64)
+    rng = random.Random(seed)
+    for cut in [rng.randrange(end - 400, end) for _ in range(6)] + [rng.randrange(5000, end) for _ in range(4)]:
+        for pad in (0, 10, 38, 200):
+            img = np.concatenate([base[:cut], np.zeros(pad, np.uint8)])
+            for io in (0, 1):
+                res, tup, st = emu_scan(img, io, 64)
+                ref, rt = coracle.scan(img, io)
+                assert_same(res, tup, ref, rt)
+    for pad in (0, 10, 37, 38, 40, 64, 4000):
+        img = np.concatenate([base[:end], np.zeros(pad, np.uint8)])
+        nreg = (img.size + 5119) // 5120
+        for io in (0, 1):
+            res, tup, st = emu_scan(img, io, 64)
+            ref, rt = coracle.scan(img, io)
+            assert_same(res, tup, ref, rt)
+            if not (pad == 0 and io == 1):
+                assert int(st[2]) == nreg, (pad, io, int(st[2]), nreg)
