@@ -176,7 +176,9 @@ LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   const uint32_t k = uk >> 1, vv = uv >> 1;
   const uint32_t X = (uint32_t)p + hs + k + vv;
   ok = ok && !read_eof(v.len, v.io, (int64_t)(v.R0 + (uint64_t)p + hs), k + vv);   // key/value read (log_file.go:130-139)
+#ifndef LDB_NO_WINCHK   // timing variant only (results invalid near the file end)
   ok = ok && !read_eof(v.len, v.io, (int64_t)(v.R0 + (uint64_t)p), kMaxHeader);   // header window (log_file.go:117-122)
+#endif
   o->crc = w[0];
   o->stat = stat;
   o->hs = hs;
@@ -469,7 +471,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       return (between & sts) != 0 || (m < kLanes && sh.s[m] != c.X);
     });
     if (j < 0) break;
-    if (it == 3) return LDB_DECLINE(5);
+    if (it == 8) return LDB_DECLINE(5);   // one false candidate repaired per pass
     const uint32_t Xj = wp.from(j, [&](int l) { return cpriv(l).X; });
     const int m = Xj >= (uint32_t)kW ? kLanes : (int)(Xj / kS);
     wp.each([&](int l) {

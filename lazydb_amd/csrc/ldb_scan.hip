@@ -210,7 +210,7 @@ __device__ __forceinline__ void copy_tables(uint32_t* tab, const uint32_t* gtab)
 #pragma unroll
     for (int b = 0; b < kBatch; ++b) {
       const int i = i0 + b * (int)blockDim.x + (int)threadIdx.x;
-      if (i < kQ) x[b] = g[i];
+      x[b] = g[i < kQ ? i : kQ - 1];   // unconditional (clamped): the batch stays in registers
     }
 #pragma unroll
     for (int b = 0; b < kBatch; ++b) {

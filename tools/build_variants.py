@@ -27,6 +27,23 @@ def build(name: str) -> str:
         defs = ["-DLDB_SCAN_BPERM=1", "-DLDB_LATE_RELEASE=1"]
     elif name.startswith("abl"):
         defs = [f"-DLDB_ABLATE={int(name[3:])}"]
+    elif name == "nowin":
+        defs = ["-DLDB_NO_WINCHK=1"]
+    elif name.startswith("git_"):   # the library as of a commit (A/B timing on one box)
+        import tempfile
+        rev = name[4:]
+        tmp = tempfile.mkdtemp()
+        for d in ("lazydb_amd/csrc", "include"):
+            os.makedirs(os.path.join(tmp, d), exist_ok=True)
+            for f in subprocess.run(["git", "-C", ROOT, "ls-tree", "--name-only", f"{rev}:{d}"], check=True,
+                                    capture_output=True, text=True).stdout.split():
+                with open(os.path.join(tmp, d, f), "wb") as fh:
+                    fh.write(subprocess.run(["git", "-C", ROOT, "show", f"{rev}:{d}/{f}"], check=True,
+                                            capture_output=True).stdout)
+        out = os.path.join(OUT, f"var_{name}.so")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                        "-Wno-unused-function", "-o", out, os.path.join(tmp, "lazydb_amd/csrc/ldb_scan.hip")], check=True)
+        return out
     elif name == "stamps":
         defs = ["-DLDB_STAMPS=1"]
     elif name == "stamps1":   # one wave per SIMD: phase stamps measure each wave's own critical path
