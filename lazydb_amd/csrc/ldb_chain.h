@@ -344,7 +344,10 @@ LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv, int seg = 0) {
 // On success stores the summary, emits the region's tuples and advances `st` to chained mode.
 // `release()` is called once the staging buffer is no longer read (the caller may start refilling
 // it); if the region must then fall back, `restage()` reloads the region into the buffer first.
-// `store(r)` writes the region summary (called by every lane with the same r).
+// On success `emit(valid, slot, pos, k, v)` is called exactly once per lane (valid: the lane's
+// tuple; a covered region calls it with valid = false everywhere), then `store(r)` writes the
+// region summary (called by every lane with the same r): a fixed number of store instructions per
+// region, which the GPU caller's counted vmcnt wait relies on (ldb_scan.hip).
 template <class WP, class CPriv, class Emit, class Free, class Restage, class Store>
 LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, CPriv cpriv, Emit emit,
                            Free release, Restage restage, Store store) {
@@ -360,6 +363,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       release();
       cpriv(l).O = crc_slice_raw2(v.tab, rows);
     });
+    wp.each([&](int) { emit(false, 0u, 0ull, 0u, 0u); });   // no tuples (the fixed store count)
     lane_scan(wp, v.tab, cpriv);
     const uint32_t raw = wp.from(kLanes - 1, [&](int l) { return cpriv(l).O; });
     wp.stamp(16);
@@ -600,11 +604,11 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   // ---- tuples and summary
   wp.each([&](int l) {
     const ChainPriv& c = cpriv(l);
-    if (!((starts >> l) & 1u)) return;   // no entry (or the pseudo start)
+    const bool valid = ((starts >> l) & 1u) && !(LDB_ABLATE & 4);   // an entry (not the pseudo start)
     const uint32_t slot = (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
     const uint64_t pos = ((v.R0 + c.s) & 0xFFFFFFFFFFull) | ((uint64_t)(c.hs & 0x3F) << 40) |
                          ((uint64_t)(c.hs & 0x3F) << 46) | ((uint64_t)(c.stat & 0xFF) << 52);
-    if (!(LDB_ABLATE & 4)) emit(slot, pos, c.k, c.vv);
+    emit(valid, slot, pos, c.k, c.vv);
   });
   RegionSum r;
   r.start = v.R0 + sL0;

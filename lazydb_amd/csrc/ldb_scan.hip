@@ -198,13 +198,40 @@ __device__ __forceinline__ void write_region_wave(const Pipe& p, uint64_t r, con
   }
 }
 
+// Range-checked buffer stores: one buffer_store_dwordx4 per call whatever the lanes' offsets;
+// a lane whose voffset is kDrop (past the descriptor's size) writes nothing. k_scan_main issues a
+// fixed number of them per region, so its counted vmcnt wait retires the next region's DMA
+// without waiting for the stores issued after it.
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kDrop = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;   // wave-uniform
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t x, uint32_t y, uint32_t z,
+                                        uint32_t w) {
+  const v4u32 d = {x, y, z, w};
+  __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, 0, 0);
+}
+// A 48-B region summary from wave-uniform values: lanes 0-2 store 16 B each (one instruction).
+__device__ __forceinline__ void store_summary(const Pipe& p, uint64_t r, const RegionSum& s, int lane) {
+  uint32_t w[12];
+  __builtin_memcpy(w, &s, sizeof(w));
+  uint32_t d[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) d[j] = lane == 0 ? w[j] : (lane == 1 ? w[4 + j] : w[8 + j]);
+  store16(rsrc_of(p.rs + r, (uint32_t)sizeof(RegionSum)), lane < 3 ? (uint32_t)lane * 16u : kDrop, d[0], d[1], d[2], d[3]);
+}
+constexpr int kStoresPerRegion = 2;   // lean path: tuples + summary (both always issued)
+
 // Global -> LDS copy of the table block: 16-B loads, kBatch of them in flight per thread before
 // the stores (one global round trip per batch, not per word).
 static_assert(kTabWords % 4 == 0, "table block is a whole number of 16-B words");
 __device__ __forceinline__ void copy_tables(uint32_t* tab, const uint32_t* gtab) {
   constexpr int kQ = kTabWords / 4, kBatch = 8;
-  const uint4* g = reinterpret_cast<const uint4*>(gtab);
-  uint4* t = reinterpret_cast<uint4*>(tab);
+  const uint4* __restrict__ g = reinterpret_cast<const uint4*>(gtab);   // no aliasing: all loads before the stores
+  uint4* __restrict__ t = reinterpret_cast<uint4*>(tab);
   for (int i0 = 0; i0 < kQ; i0 += kBatch * (int)blockDim.x) {
     uint4 x[kBatch];
 #pragma unroll
@@ -212,6 +239,7 @@ __device__ __forceinline__ void copy_tables(uint32_t* tab, const uint32_t* gtab)
       const int i = i0 + b * (int)blockDim.x + (int)threadIdx.x;
       x[b] = g[i < kQ ? i : kQ - 1];   // unconditional (clamped): the batch stays in registers
     }
+    asm volatile("" ::: "memory");   // keep the whole batch of loads in flight before the stores
 #pragma unroll
     for (int b = 0; b < kBatch; ++b) {
       const int i = i0 + b * (int)blockDim.x + (int)threadIdx.x;
@@ -258,14 +286,15 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     if ((uint64_t)b < count) stage_dma(p.img, p.len, rb + (uint64_t)b, ring_lds + b * kBuf, lane);
   for (uint64_t i = 0; i < count; ++i) {
     // Wait for region i's DMA: vmcnt(N) retires all but the N youngest VM ops (issue order, global
-    // ops only in this kernel). Younger than DMA(i) are at least: in steady state the region
-    // summary store of iteration i-kNB (>= 1 instruction) and, for kNB > 1, the DMAs of regions
-    // i+1 .. i+kNB-1 (kG instructions each; their summary stores are not counted: conservative).
+    // ops only in this kernel). Younger than DMA(i) are, in steady state, the kStoresPerRegion
+    // buffer stores of iteration i-kNB (a lean region always issues exactly those after its
+    // release; a deferred region drains vmcnt on its atomic) and, for kNB > 1, the DMAs of regions
+    // i+1 .. i+kNB-1 (kG instructions each; their stores are not counted: conservative).
     // Near the end of the run fewer DMAs were issued after DMA(i) (none past the run's last region).
     {
       const uint64_t left = count - 1 - i;
       const uint64_t ahead = left < (uint64_t)(kNB - 1) ? left : (uint64_t)(kNB - 1);   // DMAs issued after DMA(i)
-      if (ahead == (uint64_t)(kNB - 1) && i >= (uint64_t)kNB) wait_vm<(kNB - 1) * kG + 1>();
+      if (ahead == (uint64_t)(kNB - 1) && i >= (uint64_t)kNB) wait_vm<(kNB - 1) * kG + kStoresPerRegion>();
       else if (kNB >= 3 && ahead >= 2) wait_vm<2 * kG>();
       else if (kNB >= 2 && ahead >= 1) wait_vm<kG>();
       else wait_vm<0>();
@@ -284,6 +313,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     v.len = p.len;
     v.io = p.io;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
+    const __amdgpu_buffer_rsrc_t sc_rs = rsrc_of(sc, (uint32_t)(kRegionCap * sizeof(ldb_index_tuple)));
     ChainPriv cq;
 #if LDB_ABLATE >= 16
     {   // timing skeletons (results invalid): 16 = DMA only, 32 = + slice CRC, 64 = + lane scan
@@ -312,7 +342,9 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
     bool released = false;
     const bool fast = region_chained(
         wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },
-        [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot_, pos, k, vv); },
+        [&](bool valid, uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
+          store16(sc_rs, valid ? slot_ * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
+        },
         [&] {   // the buffer's last read is behind us: stage the run's region i + kNB into it
           const uint64_t nx = i + kNB;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -321,9 +353,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
           released = true;
         },
         [] {},   // a deferred region is re-read from global memory by k_fallback
-        [&](const RegionSum& s) {   // straight from registers: one lane, three 16-B stores
-          if (lane == 0) p.rs[r] = s;
-        });
+        [&](const RegionSum& s) { store_summary(p, r, s, lane); });
     if (fast) {
       ++n_fast;
     } else {

@@ -123,7 +123,8 @@ struct Emu {
     bool released = false;
     const bool fast = region_chained(
         wp, v, buf.data(), sh, st, [&](int l) -> ChainPriv& { return cpriv[l]; },
-        [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
+        [&](bool valid, uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) {
+          if (!valid) return;
           sc[slot].pos = pos;
           sc[slot].k_size = k;
           sc[slot].v_size = vv;
