@@ -150,6 +150,11 @@ int ldb_scan_file_dev_serial(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len,
  * for the recorded events). enable: 1 on + reset, 0 off + reset, -1 query only. */
 int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n);
 
+/* Practical HBM-read ceiling for the roofline report: a read-only XOR
+ * reduction over the device image d_image[0, len), 16-B loads, `iters` timed launches after one
+ * warm-up, on the context's device and its own stream. *gbps = len / average launch time / 1e9. */
+int ldb_read_ceiling(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, int iters, double* gbps);
+
 #ifdef __cplusplus
 }
 #endif

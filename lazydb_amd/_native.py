@@ -67,6 +67,9 @@ def lib():
         for fn in ("ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve", "ldb_scan_file_dev",
                    "ldb_scan_file_dev_serial", "ldb_scan_file", "ldb_scan_files_dev", "ldb_kernel_timing"):
             getattr(L, fn).restype = i32
+        if hasattr(L, "ldb_read_ceiling"):   # absent from A/B builds of older revisions (tools/build_variants.py)
+            L.ldb_read_ceiling.argtypes = [vp, vp, u64, i32, C.POINTER(C.c_double)]
+            L.ldb_read_ceiling.restype = i32
         if L.ldb_abi_version() != 1:
             raise LdbError("liblazydb_gpu ABI version mismatch")
         _lib = L
@@ -75,7 +78,7 @@ def lib():
 
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
-           "ldb_scan_file_dev_serial", "ldb_kernel_timing")
+           "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_read_ceiling")
 
 
 def status_str(s: int) -> str:

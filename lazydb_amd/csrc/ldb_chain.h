@@ -344,10 +344,13 @@ LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv, int seg = 0) {
 // On success stores the summary, emits the region's tuples and advances `st` to chained mode.
 // `release()` is called once the staging buffer is no longer read (the caller may start refilling
 // it); if the region must then fall back, `restage()` reloads the region into the buffer first.
-// On success `emit(valid, slot, pos, k, v)` is called exactly once per lane (valid: the lane's
-// tuple; a covered region calls it with valid = false everywhere), then `store(r)` writes the
-// region summary (called by every lane with the same r): a fixed number of store instructions per
-// region, which the GPU caller's counted vmcnt wait relies on (ldb_scan.hip).
+// Once the region's starts are final, `emit(valid, slot, pos, k, v)` is called exactly once per
+// lane (valid: the lane's tuple), before the CRC work and before `release()`: the tuple fields die
+// early, and a region that then declines is redone by region_process, which rewrites its slots
+// (k_compact reads only as many as the final summary counts). A covered region emits nothing. On
+// success `store(r)` writes the region summary (called by every lane with the same r) after
+// `release()`: one store instruction per region after the next region's DMA, which the GPU
+// caller's counted vmcnt wait relies on (ldb_scan.hip).
 template <class WP, class CPriv, class Emit, class Free, class Restage, class Store>
 LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, CPriv cpriv, Emit emit,
                            Free release, Restage restage, Store store) {
@@ -363,7 +366,6 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       release();
       cpriv(l).O = crc_slice_raw2(v.tab, rows);
     });
-    wp.each([&](int) { emit(false, 0u, 0ull, 0u, 0u); });   // no tuples (the fixed store count)
     lane_scan(wp, v.tab, cpriv);
     const uint32_t raw = wp.from(kLanes - 1, [&](int l) { return cpriv(l).O; });
     wp.stamp(16);
@@ -521,6 +523,15 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   const uint32_t sL0 = wp.from(L0, [&](int l) { return cpriv(l).s; });
   const int z = starts ? 63 - (int)__builtin_clzll(starts) : L0;
   const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).s; });
+  // ---- tuples (see emit above)
+  wp.each([&](int l) {
+    const ChainPriv& c = cpriv(l);
+    const bool valid = ((starts >> l) & 1u) && !(LDB_ABLATE & 4);   // an entry (not the pseudo start)
+    const uint32_t slot = (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
+    const uint64_t pos = ((v.R0 + c.s) & 0xFFFFFFFFFFull) | ((uint64_t)(c.hs & 0x3F) << 40) |
+                         ((uint64_t)(c.hs & 0x3F) << 46) | ((uint64_t)(c.stat & 0xFF) << 52);
+    emit(valid, slot, pos, c.k, c.vv);
+  });
   // The last start's 8-byte rewrite may run past the region end (into the staged halo):
   //   kW - sz in (4, 8): its CRC-init bytes straddle the end; the true init-based register at the
   //     region end is the G-chain's ^ (~0 >> 8 * (bytes of the init inside the region));
@@ -601,15 +612,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     return LDB_DECLINE(8);
   }
   wp.stamp(14);
-  // ---- tuples and summary
-  wp.each([&](int l) {
-    const ChainPriv& c = cpriv(l);
-    const bool valid = ((starts >> l) & 1u) && !(LDB_ABLATE & 4);   // an entry (not the pseudo start)
-    const uint32_t slot = (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
-    const uint64_t pos = ((v.R0 + c.s) & 0xFFFFFFFFFFull) | ((uint64_t)(c.hs & 0x3F) << 40) |
-                         ((uint64_t)(c.hs & 0x3F) << 46) | ((uint64_t)(c.stat & 0xFF) << 52);
-    emit(valid, slot, pos, c.k, c.vv);
-  });
+  // ---- summary
   RegionSum r;
   r.start = v.R0 + sL0;
   if (tpos != kNone32) {   // the chain ends here (status at tpos, as region_process reports it)

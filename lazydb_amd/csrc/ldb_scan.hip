@@ -223,7 +223,7 @@ __device__ __forceinline__ void store_summary(const Pipe& p, uint64_t r, const R
   for (int j = 0; j < 4; ++j) d[j] = lane == 0 ? w[j] : (lane == 1 ? w[4 + j] : w[8 + j]);
   store16(rsrc_of(p.rs + r, (uint32_t)sizeof(RegionSum)), lane < 3 ? (uint32_t)lane * 16u : kDrop, d[0], d[1], d[2], d[3]);
 }
-constexpr int kStoresPerRegion = 2;   // lean path: tuples + summary (both always issued)
+constexpr int kStoresPerRegion = 1;   // lean path: the summary (tuples are stored before the release)
 
 // Global -> LDS copy of the table block: 16-B loads, kBatch of them in flight per thread before
 // the stores (one global round trip per batch, not per word).
@@ -287,8 +287,8 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   for (uint64_t i = 0; i < count; ++i) {
     // Wait for region i's DMA: vmcnt(N) retires all but the N youngest VM ops (issue order, global
     // ops only in this kernel). Younger than DMA(i) are, in steady state, the kStoresPerRegion
-    // buffer stores of iteration i-kNB (a lean region always issues exactly those after its
-    // release; a deferred region drains vmcnt on its atomic) and, for kNB > 1, the DMAs of regions
+    // buffer stores of iteration i-kNB (a finished lean region always issues exactly those after
+    // its release; a deferred region drains vmcnt on its atomic) and, for kNB > 1, the DMAs of regions
     // i+1 .. i+kNB-1 (kG instructions each; their stores are not counted: conservative).
     // Near the end of the run fewer DMAs were issued after DMA(i) (none past the run's last region).
     {
@@ -709,6 +709,23 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   p.ctr[4] = 0;
 }
 
+// Read-only reduction over the image (ldb_read_ceiling): four 16-B loads in flight per thread.
+__global__ __launch_bounds__(256) void k_read_reduce(const uint4* __restrict__ p, uint64_t n16, uint32_t* sink) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  uint32_t acc = 0;
+  uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 x0 = p[i], x1 = p[i + stride], x2 = p[i + 2 * stride], x3 = p[i + 3 * stride];
+    acc ^= x0.x ^ x0.y ^ x0.z ^ x0.w ^ x1.x ^ x1.y ^ x1.z ^ x1.w ^ x2.x ^ x2.y ^ x2.z ^ x2.w ^ x3.x ^ x3.y ^ x3.z ^ x3.w;
+  }
+  for (; i < n16; i += stride) {
+    const uint4 x = p[i];
+    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+  }
+  acc = __reduce_xor_sync(~0ull, acc);
+  if ((threadIdx.x & 63) == 0) atomicXor(&sink[blockIdx.x], acc);
+}
+
 size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
 size_t repair_lds_bytes() { return sizeof(WaveLds) + kBuf; }
 size_t fallback_lds_bytes() { return kFbWaves * (sizeof(WaveLds) + kBuf); }
@@ -1045,6 +1062,37 @@ int ldb_debug_stamps(uint64_t* out, int reset) {
   return LDB_OK;
 }
 #endif
+
+int ldb_read_ceiling(ldb_ctx* c, const uint8_t* d_image, uint64_t len, int iters, double* gbps) {
+  if (!c || !gbps || (len && !d_image) || iters < 1 || (uintptr_t)d_image % 16) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  *gbps = 0.0;
+  const uint64_t n16 = len / 16;
+  if (!n16) return LDB_OK;
+  hipStream_t s;
+  hipEvent_t a, b;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return LDB_ERR_HIP;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  uint32_t* d_sink = nullptr;
+  const unsigned grid = (unsigned)c->n_cu * 8;
+  int rc = hipMalloc(&d_sink, grid * sizeof(uint32_t)) == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+  if (rc == LDB_OK) {
+    hipLaunchKernelGGL(k_read_reduce, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(d_image), n16, d_sink);
+    (void)hipEventRecord(a, s);
+    for (int i = 0; i < iters; ++i)
+      hipLaunchKernelGGL(k_read_reduce, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(d_image), n16, d_sink);
+    (void)hipEventRecord(b, s);
+    float ms = 0.f;
+    if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess || ms <= 0.f) rc = LDB_ERR_HIP;
+    else *gbps = (double)(n16 * 16) / ((double)ms / iters * 1e-3) / 1e9;
+  }
+  if (d_sink) (void)hipFree(d_sink);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipStreamDestroy(s);
+  return rc;
+}
 
 int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n) {
   if (!c) return LDB_ERR_ARG;

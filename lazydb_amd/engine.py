@@ -88,6 +88,12 @@ class Engine:
                                       out.ctypes.data, cap, C.byref(res)), "ldb_scan_file")
         return res, out[: min(res.n_entries, cap)]
 
+    def read_ceiling(self, d_img, iters: int = 20) -> float:
+        """GB/s of a read-only reduction over the device image (the practical HBM-read ceiling)."""
+        g = C.c_double()
+        N.check(N.lib().ldb_read_ceiling(self.ctx, d_img.data_ptr(), d_img.numel(), iters, C.byref(g)), "read_ceiling")
+        return g.value
+
     def timing(self, enable: int = -1):
         a, b, n = C.c_double(), C.c_double(), C.c_uint64()
         N.check(N.lib().ldb_kernel_timing(self.ctx, enable, C.byref(a), C.byref(b), C.byref(n)), "timing")
