@@ -132,7 +132,23 @@ LDB_HD uint32_t win_word(const uint32_t* w, uint32_t b) {
   return funnel(hi, lo, b & 3u);
 }
 
-LDB_HD uint32_t ctz_or(uint32_t x, uint32_t dflt) { return x ? (uint32_t)__builtin_ctz(x) : dflt; }
+// Index of the lowest set bit, 0xFFFFFFFF for 0: v_ffbl_b32 as is (__builtin_ctz(0) is undefined,
+// so the compiler adds a compare and select around it).
+LDB_HD uint32_t ffbl_raw(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu;
+#endif
+}
+
+// dflt <= 32 (a bit count): min(ffbl, dflt) is the lowest set bit or dflt
+LDB_HD uint32_t ctz_or(uint32_t x, uint32_t dflt) {
+  const uint32_t b = ffbl_raw(x);
+  return b < dflt ? b : dflt;
+}
 
 // varint payload of a canonical field of n in [1, 4] bytes held little-endian in b;
 // *canon = minimal encoding (n == 1 or last byte nonzero)
@@ -215,8 +231,7 @@ LDB_HD uint32_t first_cand(const View& v, int B, uint32_t from = 0) {
       // drop positions before `from` (only their flags can be borrow artefacts of a lower hit)
       const int rel = (int)lo - (qd << 5);
       m = rel <= 0 ? m : (rel >= 32 ? 0u : (m & (0xFFFFFFFFu << rel)));
-      const uint32_t bit = m ? (uint32_t)__builtin_ctz(m) : 0xFFFFFFFFu;
-      const uint32_t c = bit | ((uint32_t)qd << 5);
+      const uint32_t c = ffbl_raw(m) | ((uint32_t)qd << 5);   // no hit: 0xFFFFFFFF
       best = c < best ? c : best;
     }
   }
