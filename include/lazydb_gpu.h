@@ -155,6 +155,86 @@ int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg
  * warm-up, on the context's device and its own stream. *gbps = len / average launch time / 1e9. */
 int ldb_read_ceiling(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, int iters, double* gbps);
 
+/* ---- merge / GC: last-writer-wins liveness and the compacted entry stream ------------------
+ * Replaces, for the string value type, the scan + liveness + rewrite body of
+ *   db.go:370-427  (*LazyDB).Merge       per target file: ReadLogEntry loop, drop SDelete (:403),
+ *                                        drop ExpiredAt != 0 && <= now (:406-409), mergeStr (:413)
+ *   db.go:243-265  mergeStr              live iff index[key] == (fid, offset) (:255)
+ *   db.go:473-523  writeLogEntry         EncodeEntry + rollover to fid+1 when Offset+size > MaxLogFileSize
+ *   index.go:15-26 buildStrIndex         the index those checks read: Put per record, Delete on SDelete,
+ *                                        applied in (fid, offset) order (index.go:68-95)
+ * and the per-record liveness that lets a replay do one Put per live key. */
+
+/* One log file of the value type, in ascending fid order (index.go:68 sorts fids). */
+typedef struct ldb_merge_file {
+  const uint8_t* d_image;  /* device image of the file, `len` bytes (the IOController bound) */
+  uint64_t len;
+  uint32_t fid;
+  uint32_t is_target;      /* 1: in the compaction candidate list (discard.go:192-230 getCCL) */
+} ldb_merge_file;
+
+/* The ValuePos a rewritten record gets (db.go:516-520), plus where it came from, so the caller can
+ * update its index (db.go:260 updateIndexTree) without re-reading the key. */
+typedef struct ldb_merge_pos {
+  uint64_t offset;      /* offset in the output log file */
+  uint32_t fid;         /* output log file (active fid, or a rollover successor) */
+  uint32_t entry_size;  /* len(EncodeEntry(entry)) */
+  uint64_t src_offset;  /* offset of the record in its input file */
+  uint32_t src_file;    /* index of the input file in the ldb_merge_file array */
+  uint32_t reserved_;
+} ldb_merge_pos;
+
+/* A run of the compacted stream that goes to one log file: stream[stream_off, +n_bytes) is written at
+ * file_off of log file `fid`. Segments are in stream order; a rollover starts a new segment. */
+typedef struct ldb_merge_segment {
+  uint32_t fid;
+  uint32_t reserved_;
+  uint64_t file_off;
+  uint64_t stream_off;
+  uint64_t n_bytes;
+} ldb_merge_segment;
+
+/* Per input file: its replay scan result and its live records (the index's final values). */
+typedef struct ldb_merge_file_stat {
+  int32_t status;       /* scan status of the file (ldb_scan_result.status) */
+  uint32_t fid;
+  uint64_t n_entries;
+  uint64_t end_off;
+  uint64_t live_count;  /* records that are the final index value of their key */
+  uint64_t live_bytes;  /* their EncodeEntry sizes; total - live = the stale bytes discard.go tracks */
+} ldb_merge_file_stat;
+
+typedef struct ldb_merge_result {
+  int32_t status;       /* LDB_OK; a file's fatal scan status (then bad_file is set); LDB_ERR_CAPACITY */
+  int32_t bad_file;     /* -1, or the first input file whose replay scan failed (index.go:90 Fatalf) */
+  uint64_t n_records;   /* records replayed over all files */
+  uint64_t n_live;      /* records that are the final index value of their key */
+  uint64_t n_emit;      /* records rewritten by the merge (live, in a target file, not expired) */
+  uint64_t emit_bytes;  /* bytes of the compacted stream */
+  uint32_t end_fid;     /* the active file after the merge (rollovers advance it) */
+  uint32_t n_segments;
+  uint64_t end_off;     /* its append offset (LogFile.Offset) */
+} ldb_merge_result;
+
+/* Merge the target files of one value type.  Synchronous; all work runs on `stream` of the context's
+ * device.  files: host array of n_files descriptors, ascending fid; the active file (active_fid, append
+ * offset active_off) may be among them but must not be a target.  The compacted stream goes to
+ * d_stream (device, stream_cap bytes), the new positions to d_pos (device, pos_cap entries), the
+ * segments to h_segs (host, seg_cap), per-record liveness (1 byte per replayed record, file order,
+ * files concatenated) to d_live (device, live_cap; may be NULL), per-file stats to h_stats (host,
+ * n_files; may be NULL).  With no target file this is the replay pre-resolution alone (f1).
+ * LDB_ERR_CAPACITY: some output was too small; h_result holds the sizes needed. */
+int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type, uint32_t active_fid,
+                        uint64_t active_off, uint64_t max_file_size, int64_t now, uint8_t* d_stream,
+                        uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap, ldb_merge_segment* h_segs,
+                        uint32_t seg_cap, uint8_t* d_live, uint64_t live_cap, ldb_merge_file_stat* h_stats,
+                        ldb_merge_result* h_result, void* stream);
+
+/* Timing hook for bench.py: device time (ms) of the last ldb_merge_files_dev call, split into the
+ * replay scans, the liveness resolution (hash + last-writer-wins) and the compaction (prefix sums,
+ * rollover packing, stream copy), measured with HIP events on the merge stream. */
+int ldb_merge_timing(ldb_ctx* ctx, double* scan_ms, double* live_ms, double* compact_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,28 @@ class ScanResult(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class MergeFile(C.Structure):
+    _fields_ = [("d_image", C.c_void_p), ("len", C.c_uint64), ("fid", C.c_uint32), ("is_target", C.c_uint32)]
+
+
+class MergeResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("bad_file", C.c_int32), ("n_records", C.c_uint64), ("n_live", C.c_uint64),
+                ("n_emit", C.c_uint64), ("emit_bytes", C.c_uint64), ("end_fid", C.c_uint32),
+                ("n_segments", C.c_uint32), ("end_off", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+MERGE_POS = np.dtype([("offset", "<u8"), ("fid", "<u4"), ("entry_size", "<u4"), ("src_offset", "<u8"),
+                      ("src_file", "<u4"), ("reserved_", "<u4")])
+MERGE_SEGMENT = np.dtype([("fid", "<u4"), ("reserved_", "<u4"), ("file_off", "<u8"), ("stream_off", "<u8"),
+                          ("n_bytes", "<u8")])
+MERGE_FILE_STAT = np.dtype([("status", "<i4"), ("fid", "<u4"), ("n_entries", "<u8"), ("end_off", "<u8"),
+                            ("live_count", "<u8"), ("live_bytes", "<u8")])
+assert C.sizeof(MergeFile) == 24 and C.sizeof(MergeResult) == 56
+assert MERGE_POS.itemsize == 32 and MERGE_SEGMENT.itemsize == 32 and MERGE_FILE_STAT.itemsize == 40
+
 RESULT_BYTES = C.sizeof(ScanResult)
 assert RESULT_BYTES == 40
 
@@ -70,6 +92,12 @@ def lib():
         if hasattr(L, "ldb_read_ceiling"):   # absent from A/B builds of older revisions (tools/build_variants.py)
             L.ldb_read_ceiling.argtypes = [vp, vp, u64, i32, C.POINTER(C.c_double)]
             L.ldb_read_ceiling.restype = i32
+        if hasattr(L, "ldb_merge_files_dev"):   # absent from A/B builds of older revisions
+            L.ldb_merge_files_dev.argtypes = [vp, i32, vp, i32, u32, u64, u64, C.c_int64, vp, u64, vp, u64, vp, u32,
+                                              vp, u64, vp, C.POINTER(MergeResult), vp]
+            L.ldb_merge_files_dev.restype = i32
+            L.ldb_merge_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+            L.ldb_merge_timing.restype = i32
         if L.ldb_abi_version() != 1:
             raise LdbError("liblazydb_gpu ABI version mismatch")
         _lib = L
@@ -78,7 +106,8 @@ def lib():
 
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
-           "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_read_ceiling")
+           "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_read_ceiling", "ldb_merge_files_dev",
+           "ldb_merge_timing")
 
 
 def status_str(s: int) -> str:

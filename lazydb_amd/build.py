@@ -6,7 +6,7 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "ldb_scan.hip")
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("ldb_scan.hip", "ldb_merge.hip")]
 OUT = os.path.join(HERE, "_lib", "liblazydb_gpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -24,7 +24,7 @@ def build_lib(force: bool = False) -> str:
     if force or _stale(OUT, deps):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-               "-Wno-unused-function", "-o", OUT, SRC]
+               "-Wno-unused-function", "-o", OUT, *SRCS]
         subprocess.run(cmd, check=True)
     return OUT
 

@@ -1,0 +1,727 @@
+// ldb_merge.hip — merge/GC engine: last-writer-wins liveness over the replayed records of one value
+// type, and the compacted entry stream of the target files.
+//
+// Reference semantics restated (kakosute/lazydb):
+//   index.go:15-26, 68-95   replay: per record in (fid, offset) order, SDelete -> Delete(key), else
+//                           Put(key, {fid, offset, EncodeEntry size}); the index holds each key's LAST
+//                           record unless that record is an SDelete.
+//   db.go:383-427           Merge: for each target file in ascending fid (getCCL sorts, discard.go:224),
+//                           for each record: skip SDelete (:403), skip ExpiredAt != 0 && <= now (:406),
+//                           mergeStr (:413).
+//   db.go:243-265           mergeStr: rewrite iff index[key] == (fid, offset) (:255).
+//   db.go:473-523           writeLogEntry: EncodeEntry, then if Offset + size > MaxLogFileSize the active
+//                           file rolls over to fid+1 at offset 0 (one check per record, :485), append.
+// Because a key's index value is its last record, "index[key] == (fid, offset)" is "this record is the
+// last record of its key and not an SDelete"; rewriting one target file never changes that predicate for
+// a record of a later target file (its key's last record is elsewhere), so merging the targets in one
+// batch equals calling Merge once per target fid, ascending.
+//
+// Device pipeline (one context stream, synchronous API):
+//   replay scans    ldb_scan_file_dev per file (ldb_scan.hip), 48-B ldb_entry records, dense
+//   k_locate        per record: key address + 64-bit key hash                (HBM: key bytes + 48 B)
+//   k_insert        open-addressing table keyed by full key bytes; slot = atomicMax(seq)   (random)
+//   k_live          per record: live = (slot max == seq) && !SDelete; emit flag, sizes, per-file stats
+//   k_scan_*        exclusive prefix sums of emitted bytes and counts (3-kernel reduce-then-scan)
+//   k_pack          one lane: greedy rollover packing by binary search over the byte prefix
+//   k_emit_copy     one wave per 64 records: new ValuePos, unaligned 16-B copies of the emitted bytes,
+//                   re-encoded header + CRC-32 for the (rare) non-canonical records
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/lazydb_gpu.h"
+
+__attribute__((visibility("hidden"))) int ldb_ctx_device_(ldb_ctx* c);
+__attribute__((visibility("hidden"))) void** ldb_ctx_merge_slot_(ldb_ctx* c);
+
+namespace {
+
+constexpr uint8_t kSDelete = 1;  // logfile/log_entry.go:13-14
+constexpr int kScanItems = 8;    // items per thread in the prefix-sum kernels
+constexpr int kScanBlock = 256;
+constexpr uint64_t kScanTile = (uint64_t)kScanItems * kScanBlock;
+
+struct FileDesc {       // one input file, in device memory
+  const uint8_t* img;
+  uint64_t seq_base;    // first record index of the file; desc[n_files].seq_base = total records
+  uint32_t is_target;
+  uint32_t fid;
+};
+
+struct Tail {           // k_pack output
+  uint32_t end_fid;
+  uint32_t n_segments;
+  uint64_t end_off;
+};
+
+struct MergeWs {
+  int device = 0;
+  ldb_entry* recs = nullptr;     // replayed records, dense over all files
+  uint64_t rec_cap = 0;
+  uint8_t* seqbuf = nullptr;     // per-record arrays + hash table + scan sums
+  uint64_t seqbuf_bytes = 0;
+  uint8_t* small = nullptr;      // scan results, file descriptors, stats, tail, segments
+  uint64_t small_bytes = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  float t_scan = 0, t_live = 0, t_compact = 0;
+};
+
+#define MHIP(x)                                    \
+  do {                                             \
+    if ((x) != hipSuccess) return LDB_ERR_HIP;     \
+  } while (0)
+
+// ------------------------------------------------------------------------------ device helpers
+__device__ __forceinline__ uint64_t load8u(const uint8_t* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ uint64_t key_hash(const uint8_t* p, uint32_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xFF51AFD7ED558CCDull);
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) h = mix64(h ^ load8u(p + i)) + 0x632BE59BD9B4E019ull;
+  uint64_t t = 0;
+  for (uint32_t j = 0; i + j < n; ++j) t |= (uint64_t)p[i + j] << (8 * j);
+  return mix64(h ^ t ^ ((uint64_t)(n & 7) << 59));
+}
+
+__device__ bool key_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8)
+    if (load8u(a + i) != load8u(b + i)) return false;
+  for (; i < n; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t file_of(const FileDesc* d, uint32_t n_files, uint64_t seq) {
+  uint32_t lo = 0, hi = n_files - 1;   // last file with seq_base <= seq
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (d[mid].seq_base <= seq) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Go binary.PutVarint (zig-zag) — encoding/binary/varint.go; EncodeEntry's field encoder
+__device__ int put_varint(uint8_t* b, int64_t x) {
+  uint64_t ux = (uint64_t)x << 1;
+  if (x < 0) ux = ~ux;
+  int i = 0;
+  while (ux >= 0x80) {
+    b[i++] = (uint8_t)(ux | 0x80);
+    ux >>= 7;
+  }
+  b[i++] = (uint8_t)ux;
+  return i;
+}
+
+__device__ __forceinline__ uint32_t crc_byte(uint32_t c, uint8_t b) {   // reflected CRC-32/IEEE register
+  c ^= b;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+  return c;
+}
+
+// ------------------------------------------------------------------------------ liveness
+__global__ __launch_bounds__(256) void k_locate(const ldb_entry* __restrict__ recs, uint64_t n,
+                                                const FileDesc* __restrict__ fd, uint32_t n_files,
+                                                uint64_t* __restrict__ hash, uint64_t* __restrict__ keyptr) {
+  uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seq >= n) return;
+  const ldb_entry e = recs[seq];
+  const uint8_t* kp = fd[file_of(fd, n_files, seq)].img + e.offset + e.hdr_size;
+  hash[seq] = key_hash(kp, e.k_size);
+  keyptr[seq] = (uint64_t)kp;
+}
+
+// Insert every record into an open-addressing table keyed by the FULL key bytes: a slot word is
+// (hash tag << 32 | representative seq + 1), claimed by CAS; a probe that meets its tag compares its key
+// with the representative's, so distinct keys never share a slot whatever their hashes. The slot's
+// max word (atomicMax of seq + 1) ends as the key's last record (index.go: later Put/Delete wins).
+__global__ __launch_bounds__(256) void k_insert(const ldb_entry* __restrict__ recs, uint64_t n,
+                                                const uint64_t* __restrict__ hash,
+                                                const uint64_t* __restrict__ keyptr, uint64_t* tab_key,
+                                                uint32_t* tab_max, uint64_t mask, uint32_t* __restrict__ slot) {
+  uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seq >= n) return;
+  const uint64_t h = hash[seq];
+  const uint64_t mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
+  const uint8_t* kp = reinterpret_cast<const uint8_t*>(keyptr[seq]);
+  const uint32_t kl = recs[seq].k_size;
+  uint64_t i = h & mask;
+  for (;;) {
+    uint64_t v = __hip_atomic_load(&tab_key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0) {
+      uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tab_key[i]), 0ull,
+                                (unsigned long long)mine);
+      if (prev == 0) break;
+      v = prev;
+    }
+    if ((v >> 32) == (h >> 32)) {
+      uint64_t rep = (v & 0xFFFFFFFFull) - 1;
+      if (recs[rep].k_size == kl && key_equal(kp, reinterpret_cast<const uint8_t*>(keyptr[rep]), kl)) break;
+    }
+    i = (i + 1) & mask;
+  }
+  atomicMax(&tab_max[i], (uint32_t)(seq + 1));
+  slot[seq] = (uint32_t)i;
+}
+
+// live = last record of its key and not an SDelete (index.go:16-25); emit = live && target file &&
+// not expired (db.go:403-409, 255). Per-file live counts/bytes for discard accounting.
+__global__ __launch_bounds__(256) void k_live(const ldb_entry* __restrict__ recs, uint64_t n,
+                                              const FileDesc* __restrict__ fd, uint32_t n_files,
+                                              const uint32_t* __restrict__ tab_max, const uint32_t* __restrict__ slot,
+                                              int64_t now, uint8_t* __restrict__ live_out,
+                                              uint32_t* __restrict__ esz, unsigned long long* __restrict__ fstat) {
+  uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = seq < n;
+  uint32_t f = 0, size = 0;
+  bool live = false;
+  if (valid) {
+    const ldb_entry e = recs[seq];
+    f = file_of(fd, n_files, seq);
+    live = tab_max[slot[seq]] == (uint32_t)(seq + 1) && e.stat != kSDelete;
+    size = (uint32_t)e.enc_hdr_size + e.k_size + e.v_size;
+    const bool expired = e.expired_at != 0 && e.expired_at <= now;
+    esz[seq] = (live && fd[f].is_target && !expired) ? size : 0u;
+    if (live_out) live_out[seq] = live ? 1 : 0;
+  }
+  // per-file stats: one atomic pair per wave when the wave's records share a file (the common case)
+  const uint32_t f0 = __shfl(f, 0);
+  const bool uniform = __all(!valid || f == f0);
+  if (uniform) {
+    unsigned long long c = live ? 1ull : 0ull, b = live ? (unsigned long long)size : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+      c += __shfl_xor(c, o);
+      b += __shfl_xor(b, o);
+    }
+    if ((threadIdx.x & 63) == 0 && c) {
+      atomicAdd(&fstat[2 * f0], c);
+      atomicAdd(&fstat[2 * f0 + 1], b);
+    }
+  } else if (valid && live) {
+    atomicAdd(&fstat[2 * f], 1ull);
+    atomicAdd(&fstat[2 * f + 1], (unsigned long long)size);
+  }
+}
+
+// ------------------------------------------------------------------------------ prefix sums
+// (bytes, count) pairs over esz; exclusive results P (u64 bytes) and C (u32 count), n+1 entries each.
+__device__ __forceinline__ void block_exscan(uint64_t& b, uint32_t& c, uint64_t* sb, uint32_t* sc,
+                                             uint64_t& tb, uint32_t& tc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t ib = b;
+  uint32_t ic = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t xb = __shfl_up(ib, o);
+    uint32_t xc = __shfl_up(ic, o);
+    if (lane >= o) {
+      ib += xb;
+      ic += xc;
+    }
+  }
+  if (lane == 63) {
+    sb[w] = ib;
+    sc[w] = ic;
+  }
+  __syncthreads();
+  uint64_t ob = 0;
+  uint32_t oc = 0;
+  tb = 0;
+  tc = 0;
+  for (int k = 0; k < kScanBlock / 64; ++k) {
+    if (k < w) {
+      ob += sb[k];
+      oc += sc[k];
+    }
+    tb += sb[k];
+    tc += sc[k];
+  }
+  b = ob + ib - b;
+  c = oc + ic - c;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint32_t* __restrict__ esz, uint64_t n,
+                                                            uint64_t* __restrict__ bsum, uint32_t* __restrict__ bcnt) {
+  __shared__ uint64_t sb[kScanBlock / 64];
+  __shared__ uint32_t sc[kScanBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint64_t b = 0;
+  uint32_t c = 0;
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < n) {
+      uint32_t s = esz[base + k];
+      b += s;
+      c += s ? 1u : 0u;
+    }
+  uint64_t tb;
+  uint32_t tc;
+  block_exscan(b, c, sb, sc, tb, tc);
+  if (threadIdx.x == 0) {
+    bsum[blockIdx.x] = tb;
+    bcnt[blockIdx.x] = tc;
+  }
+}
+
+// one workgroup: exclusive scan of the per-tile sums in place; totals go to P[n], C[n]
+__global__ __launch_bounds__(kScanBlock) void k_scan_tiles(uint64_t* bsum, uint32_t* bcnt, uint64_t nb,
+                                                           uint64_t* P, uint32_t* C, uint64_t n) {
+  __shared__ uint64_t sb[kScanBlock / 64];
+  __shared__ uint32_t sc[kScanBlock / 64];
+  uint64_t carry_b = 0;
+  uint32_t carry_c = 0;
+  for (uint64_t o = 0; o < nb; o += kScanBlock) {
+    uint64_t i = o + threadIdx.x;
+    uint64_t b = i < nb ? bsum[i] : 0;
+    uint32_t c = i < nb ? bcnt[i] : 0;
+    uint64_t tb;
+    uint32_t tc;
+    block_exscan(b, c, sb, sc, tb, tc);
+    if (i < nb) {
+      bsum[i] = carry_b + b;
+      bcnt[i] = carry_c + c;
+    }
+    carry_b += tb;
+    carry_c += tc;
+  }
+  if (threadIdx.x == 0) {
+    P[n] = carry_b;
+    C[n] = carry_c;
+  }
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_write(const uint32_t* __restrict__ esz, uint64_t n,
+                                                           const uint64_t* __restrict__ bsum,
+                                                           const uint32_t* __restrict__ bcnt,
+                                                           uint64_t* __restrict__ P, uint32_t* __restrict__ C) {
+  __shared__ uint64_t sb[kScanBlock / 64];
+  __shared__ uint32_t sc[kScanBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint32_t s[kScanItems];
+  uint64_t b = 0;
+  uint32_t c = 0;
+  for (int k = 0; k < kScanItems; ++k) {
+    s[k] = base + k < n ? esz[base + k] : 0u;
+    b += s[k];
+    c += s[k] ? 1u : 0u;
+  }
+  uint64_t tb;
+  uint32_t tc;
+  block_exscan(b, c, sb, sc, tb, tc);
+  b += bsum[blockIdx.x];
+  c += bcnt[blockIdx.x];
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < n) {
+      P[base + k] = b;
+      C[base + k] = c;
+      b += s[k];
+      c += s[k] ? 1u : 0u;
+    }
+}
+
+// ------------------------------------------------------------------------------ rollover packing
+__device__ uint64_t last_le(const uint64_t* P, uint64_t n, uint64_t x) {   // largest i in [0,n] with P[i] <= x
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi + 1) >> 1;
+    if (P[mid] <= x) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// writeLogEntry's greedy rollover (db.go:485-510) over the emitted records in stream order: a record
+// goes to the current file if Offset + size <= MaxLogFileSize, otherwise the file rolls over to fid+1
+// and the record is written there at 0 whatever its size. Runs of records that fit are found by binary
+// search over the byte prefix, so the loop runs once per output segment.
+__global__ void k_pack(const uint64_t* __restrict__ P, uint64_t n, uint32_t active_fid, uint64_t active_off,
+                       uint64_t max_size, ldb_merge_segment* segs, uint32_t seg_cap, Tail* tail) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t total = P[n];
+  uint32_t fid = active_fid, nseg = 0;
+  uint64_t off = active_off, x = 0;
+  while (x < total) {
+    const uint64_t r = last_le(P, n, x);        // the emitted record that starts at stream position x
+    const uint64_t size = P[r + 1] - P[r];
+    ldb_merge_segment sg;
+    sg.reserved_ = 0;
+    sg.stream_off = x;
+    if (off + size > max_size) {                // rollover, then the record is written unconditionally
+      fid += 1;
+      off = 0;
+      sg.fid = fid;
+      sg.file_off = 0;
+      off = size;
+      x += size;
+    } else {
+      sg.fid = fid;
+      sg.file_off = off;
+    }
+    if (off < max_size) {                       // extend with every following record that fits
+      const uint64_t lim = x + (max_size - off);
+      const uint64_t e = last_le(P, n, lim < total ? lim : total);
+      const uint64_t x2 = P[e] > x ? P[e] : x;
+      off += x2 - x;
+      x = x2;
+    }
+    sg.n_bytes = x - sg.stream_off;
+    if (nseg < seg_cap) segs[nseg] = sg;
+    ++nseg;
+  }
+  tail->end_fid = fid;
+  tail->end_off = off;
+  tail->n_segments = nseg;
+}
+
+// ------------------------------------------------------------------------------ emit + copy
+__device__ __forceinline__ uint32_t seg_of(const ldb_merge_segment* s, uint32_t ns, uint64_t sp) {
+  uint32_t lo = 0, hi = ns - 1;   // last segment with stream_off <= sp
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (s[mid].stream_off <= sp) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+constexpr int kCopyWaves = 4;
+
+// One wave per 64 consecutive records. Each emitted record is cut into 16-B pieces (unaligned global
+// loads/stores; a partial last piece is stored bytewise, so neighbouring records never race); the
+// wave's pieces are dealt out over its lanes. Canonical records (hdr_size == enc_hdr_size) are copied
+// verbatim: EncodeEntry re-produces their bytes. A non-canonical record gets its key/value copied and
+// its header re-encoded by its lane, CRC-32 over the new header and the key/value (log_entry.go:48-78).
+__global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
+    const ldb_entry* __restrict__ recs, uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
+    const uint64_t* __restrict__ P, const uint32_t* __restrict__ C, const ldb_merge_segment* __restrict__ segs,
+    uint32_t n_segs, uint8_t* __restrict__ stream, ldb_merge_pos* __restrict__ pos) {
+  __shared__ const uint8_t* s_src[kCopyWaves][64];
+  __shared__ uint8_t* s_dst[kCopyWaves][64];
+  __shared__ uint32_t s_nb[kCopyWaves][64];
+  __shared__ uint32_t s_ex[kCopyWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t seq = ((uint64_t)blockIdx.x * kCopyWaves + w) * 64 + lane;
+  uint32_t pieces = 0;
+  const uint8_t* src = nullptr;
+  uint8_t* dst = nullptr;
+  uint32_t nb = 0;
+  ldb_entry e;
+  bool canon = true;
+  uint64_t sp = 0;
+  const uint8_t* fimg = nullptr;
+  if (seq < n) {
+    sp = P[seq];
+    const uint64_t sz = P[seq + 1] - sp;
+    if (sz) {
+      e = recs[seq];
+      const uint32_t f = file_of(fd, n_files, seq);
+      fimg = fd[f].img;
+      const ldb_merge_segment& sg = segs[seg_of(segs, n_segs, sp)];
+      ldb_merge_pos q;
+      q.offset = sg.file_off + (sp - sg.stream_off);
+      q.fid = sg.fid;
+      q.entry_size = (uint32_t)sz;
+      q.src_offset = e.offset;
+      q.src_file = f;
+      q.reserved_ = 0;
+      pos[C[seq]] = q;
+      canon = e.hdr_size == e.enc_hdr_size;
+      src = fimg + e.offset + (canon ? 0 : e.hdr_size);
+      dst = stream + sp + (canon ? 0 : e.enc_hdr_size);
+      nb = canon ? (uint32_t)sz : e.k_size + e.v_size;
+      pieces = (nb + 15) >> 4;
+    }
+  }
+  uint32_t inc = pieces;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t x = __shfl_up(inc, o);
+    if (lane >= o) inc += x;
+  }
+  const uint32_t total = __shfl(inc, 63);
+  s_src[w][lane] = src;
+  s_dst[w][lane] = dst;
+  s_nb[w][lane] = nb;
+  s_ex[w][lane] = inc - pieces;
+  __syncthreads();
+  for (uint32_t t = lane; t < total; t += 64) {
+    int lo = 0, hi = 63;   // last record with ex <= t and pieces > 0 (ties: the later record owns t)
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (s_ex[w][mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t j = t - s_ex[w][lo];
+    const uint32_t len = min(16u, s_nb[w][lo] - 16 * j);
+    const uint8_t* s = s_src[w][lo] + 16 * j;
+    uint8_t* d = s_dst[w][lo] + 16 * j;
+    if (len == 16) {
+      uint4 v;
+      __builtin_memcpy(&v, s, 16);
+      __builtin_memcpy(d, &v, 16);
+    } else {
+      for (uint32_t b = 0; b < len; ++b) d[b] = s[b];
+    }
+  }
+  if (pieces && !canon) {   // re-encode the header (EncodeEntry :52-66) and its CRC (:75-76)
+    uint8_t h[40];
+    int o = 5;
+    h[4] = e.stat;
+    o += put_varint(h + o, e.expired_at);
+    o += put_varint(h + o, (int64_t)e.tx_id);
+    o += put_varint(h + o, (int64_t)e.tx_stat);
+    o += put_varint(h + o, (int64_t)e.k_size);
+    o += put_varint(h + o, (int64_t)e.v_size);
+    uint32_t c = 0xFFFFFFFFu;
+    for (int i = 4; i < o; ++i) c = crc_byte(c, h[i]);
+    const uint8_t* kv = fimg + e.offset + e.hdr_size;
+    for (uint32_t i = 0; i < nb; ++i) c = crc_byte(c, kv[i]);
+    c = ~c;
+    h[0] = (uint8_t)c;
+    h[1] = (uint8_t)(c >> 8);
+    h[2] = (uint8_t)(c >> 16);
+    h[3] = (uint8_t)(c >> 24);
+    uint8_t* d = stream + sp;
+    for (int i = 0; i < o; ++i) d[i] = h[i];
+  }
+}
+
+// ------------------------------------------------------------------------------ host side
+int grow(uint8_t** p, uint64_t* have, uint64_t need) {
+  if (*have >= need) return LDB_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  if (hipMalloc(p, need) != hipSuccess) return LDB_ERR_NOMEM;
+  *have = need;
+  return LDB_OK;
+}
+
+// grow the record array, keeping the first `keep` records
+int grow_recs(MergeWs* m, uint64_t need, uint64_t keep, hipStream_t s) {
+  if (m->rec_cap >= need) return LDB_OK;
+  uint64_t cap = std::max(need, m->rec_cap + m->rec_cap / 2);
+  ldb_entry* nr = nullptr;
+  if (hipMalloc(&nr, cap * sizeof(ldb_entry)) != hipSuccess) return LDB_ERR_NOMEM;
+  if (keep) MHIP(hipMemcpyAsync(nr, m->recs, keep * sizeof(ldb_entry), hipMemcpyDeviceToDevice, s));
+  MHIP(hipStreamSynchronize(s));
+  if (m->recs) (void)hipFree(m->recs);
+  m->recs = nr;
+  m->rec_cap = cap;
+  return LDB_OK;
+}
+
+MergeWs* get_ws(ldb_ctx* c) {
+  void** slot = ldb_ctx_merge_slot_(c);
+  if (*slot) return static_cast<MergeWs*>(*slot);
+  MergeWs* m = new (std::nothrow) MergeWs();
+  if (!m) return nullptr;
+  m->device = ldb_ctx_device_(c);
+  for (auto& e : m->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete m;
+      return nullptr;
+    }
+  *slot = m;
+  return m;
+}
+
+uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+}  // namespace
+
+__attribute__((visibility("hidden"))) void ldb_merge_release_(void* p) {
+  MergeWs* m = static_cast<MergeWs*>(p);
+  if (!m) return;
+  if (m->recs) (void)hipFree(m->recs);
+  if (m->seqbuf) (void)hipFree(m->seqbuf);
+  if (m->small) (void)hipFree(m->small);
+  for (auto& e : m->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete m;
+}
+
+extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type,
+                                   uint32_t active_fid, uint64_t active_off, uint64_t max_file_size, int64_t now,
+                                   uint8_t* d_stream, uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap,
+                                   ldb_merge_segment* h_segs, uint32_t seg_cap, uint8_t* d_live, uint64_t live_cap,
+                                   ldb_merge_file_stat* h_stats, ldb_merge_result* h_result, void* stream) {
+  if (!ctx || !h_result || n_files < 0 || (n_files && !files) || max_file_size == 0 ||
+      (io_type != LDB_IO_FILEIO && io_type != LDB_IO_MMAP))
+    return LDB_ERR_ARG;
+  std::memset(h_result, 0, sizeof(*h_result));
+  h_result->bad_file = -1;
+  h_result->end_fid = active_fid;
+  h_result->end_off = active_off;
+  for (int i = 0; i < n_files; ++i) {
+    if (i && files[i].fid <= files[i - 1].fid) return h_result->status = LDB_ERR_ARG;   // ascending fids
+    if (files[i].is_target && files[i].fid == active_fid) return h_result->status = LDB_ERR_ARG;
+    if (files[i].len && !files[i].d_image) return h_result->status = LDB_ERR_ARG;
+  }
+  if (hipSetDevice(ldb_ctx_device_(ctx)) != hipSuccess) return LDB_ERR_HIP;
+  MergeWs* m = get_ws(ctx);
+  if (!m) return LDB_ERR_NOMEM;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t nf = (uint32_t)n_files;
+
+  // small device buffer: scan results | file descriptors (nf+1) | per-file stats (2 u64) | tail | segments
+  const uint64_t o_res = 0, o_fd = align256(o_res + sizeof(ldb_scan_result) * (nf + 1));
+  const uint64_t o_fst = align256(o_fd + sizeof(FileDesc) * (nf + 1));
+  const uint64_t o_tail = align256(o_fst + 16ull * (nf + 1));
+  const uint64_t o_seg = align256(o_tail + sizeof(Tail));
+  const uint64_t small_need = o_seg + sizeof(ldb_merge_segment) * ((uint64_t)seg_cap + 1);
+  int rc = grow(&m->small, &m->small_bytes, small_need);
+  if (rc != LDB_OK) return rc;
+  ldb_scan_result* d_res = reinterpret_cast<ldb_scan_result*>(m->small + o_res);
+  FileDesc* d_fd = reinterpret_cast<FileDesc*>(m->small + o_fd);
+  unsigned long long* d_fst = reinterpret_cast<unsigned long long*>(m->small + o_fst);
+  Tail* d_tail = reinterpret_cast<Tail*>(m->small + o_tail);
+  ldb_merge_segment* d_segs = reinterpret_cast<ldb_merge_segment*>(m->small + o_seg);
+
+  // ---- 1. replay scans (index.go:84-95 per file), dense 48-B records
+  MHIP(hipEventRecord(m->ev[0], s));
+  uint64_t total_len = 0;
+  for (int i = 0; i < n_files; ++i) total_len += files[i].len;
+  rc = grow_recs(m, std::max<uint64_t>(total_len / 64 + 64ull * nf, 4096), 0, s);
+  if (rc != LDB_OK) return rc;
+  std::vector<FileDesc> fdh(nf + 1);
+  std::vector<ldb_scan_result> rh(nf);
+  uint64_t base = 0;
+  for (uint32_t i = 0; i < nf; ++i) {
+    for (;;) {
+      rc = ldb_scan_file_dev(ctx, files[i].d_image, files[i].len, files[i].fid, io_type, LDB_TUPLE_ENTRY,
+                             m->recs + base, m->rec_cap - base, d_res + i, s);
+      if (rc != LDB_OK) return rc;
+      MHIP(hipMemcpyAsync(&rh[i], d_res + i, sizeof(ldb_scan_result), hipMemcpyDeviceToHost, s));
+      MHIP(hipStreamSynchronize(s));
+      if (rh[i].status != LDB_ERR_CAPACITY) break;
+      rc = grow_recs(m, base + rh[i].n_entries + 1024, base, s);
+      if (rc != LDB_OK) return rc;
+    }
+    fdh[i] = FileDesc{files[i].d_image, base, files[i].is_target, files[i].fid};
+    if (h_stats) {
+      h_stats[i] = ldb_merge_file_stat{rh[i].status, files[i].fid, rh[i].n_entries, rh[i].end_off, 0, 0};
+    }
+    if (rh[i].status < 0) {   // the replay would stop here (index.go:90 log.Fatalf / db.go:399 return err)
+      h_result->status = rh[i].status;
+      h_result->bad_file = (int32_t)i;
+      h_result->n_records = base + rh[i].n_entries;
+      return h_result->status;
+    }
+    base += rh[i].n_entries;
+  }
+  const uint64_t n = base;
+  fdh[nf] = FileDesc{nullptr, n, 0, 0};
+  h_result->n_records = n;
+  if (n >= 0xFFFFFFFFull) return h_result->status = LDB_ERR_ARG;   // record ids are 32-bit
+  MHIP(hipEventRecord(m->ev[1], s));
+
+  // ---- 2. liveness
+  uint64_t tcap = 1024;
+  while (tcap < 2 * n) tcap <<= 1;
+  const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+  const uint64_t o_hash = 0, o_kp = align256(o_hash + 8 * n), o_slot = align256(o_kp + 8 * n);
+  const uint64_t o_esz = align256(o_slot + 4 * n), o_P = align256(o_esz + 4 * n);
+  const uint64_t o_C = align256(o_P + 8 * (n + 1)), o_tk = align256(o_C + 4 * (n + 1));
+  const uint64_t o_tm = align256(o_tk + 8 * tcap), o_bs = align256(o_tm + 4 * tcap);
+  const uint64_t o_bc = align256(o_bs + 8 * (ntiles + 1)), seq_need = align256(o_bc + 4 * (ntiles + 1));
+  rc = grow(&m->seqbuf, &m->seqbuf_bytes, seq_need);
+  if (rc != LDB_OK) return rc;
+  uint8_t* q = m->seqbuf;
+  uint64_t* d_hash = reinterpret_cast<uint64_t*>(q + o_hash);
+  uint64_t* d_kp = reinterpret_cast<uint64_t*>(q + o_kp);
+  uint32_t* d_slot = reinterpret_cast<uint32_t*>(q + o_slot);
+  uint32_t* d_esz = reinterpret_cast<uint32_t*>(q + o_esz);
+  uint64_t* d_P = reinterpret_cast<uint64_t*>(q + o_P);
+  uint32_t* d_C = reinterpret_cast<uint32_t*>(q + o_C);
+  uint64_t* d_tk = reinterpret_cast<uint64_t*>(q + o_tk);
+  uint32_t* d_tm = reinterpret_cast<uint32_t*>(q + o_tm);
+  uint64_t* d_bs = reinterpret_cast<uint64_t*>(q + o_bs);
+  uint32_t* d_bc = reinterpret_cast<uint32_t*>(q + o_bc);
+
+  const bool live_ok = !d_live || live_cap >= n;
+  MHIP(hipMemcpyAsync(d_fd, fdh.data(), sizeof(FileDesc) * (nf + 1), hipMemcpyHostToDevice, s));
+  MHIP(hipMemsetAsync(d_fst, 0, 16ull * (nf + 1), s));
+  MHIP(hipMemsetAsync(d_tk, 0, o_bs - o_tk, s));   // tab_key and tab_max
+  const uint32_t nbk = (uint32_t)((n + 255) / 256);
+  if (n) {
+    k_locate<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_hash, d_kp);
+    k_insert<<<nbk, 256, 0, s>>>(m->recs, n, d_hash, d_kp, d_tk, d_tm, tcap - 1, d_slot);
+    k_live<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_tm, d_slot, now, live_ok ? d_live : nullptr, d_esz, d_fst);
+    MHIP(hipGetLastError());
+  }
+  MHIP(hipEventRecord(m->ev[2], s));
+
+  // ---- 3. compaction: prefix sums, rollover packing, new positions and the stream
+  if (n) {
+    k_scan_reduce<<<(uint32_t)ntiles, kScanBlock, 0, s>>>(d_esz, n, d_bs, d_bc);
+    k_scan_tiles<<<1, kScanBlock, 0, s>>>(d_bs, d_bc, ntiles, d_P, d_C, n);
+    k_scan_write<<<(uint32_t)ntiles, kScanBlock, 0, s>>>(d_esz, n, d_bs, d_bc, d_P, d_C);
+  } else {
+    MHIP(hipMemsetAsync(d_P, 0, 8, s));
+    MHIP(hipMemsetAsync(d_C, 0, 4, s));
+  }
+  k_pack<<<1, 64, 0, s>>>(d_P, n, active_fid, active_off, max_file_size, d_segs, seg_cap + 1, d_tail);
+  MHIP(hipGetLastError());
+  uint64_t tot_b = 0;
+  uint32_t tot_c = 0;
+  Tail tail;
+  std::vector<unsigned long long> fst(2 * (nf + 1));
+  MHIP(hipMemcpyAsync(&tot_b, d_P + n, 8, hipMemcpyDeviceToHost, s));
+  MHIP(hipMemcpyAsync(&tot_c, d_C + n, 4, hipMemcpyDeviceToHost, s));
+  MHIP(hipMemcpyAsync(&tail, d_tail, sizeof(Tail), hipMemcpyDeviceToHost, s));
+  MHIP(hipMemcpyAsync(fst.data(), d_fst, 16ull * (nf + 1), hipMemcpyDeviceToHost, s));
+  MHIP(hipStreamSynchronize(s));
+  h_result->n_emit = tot_c;
+  h_result->emit_bytes = tot_b;
+  h_result->end_fid = tail.end_fid;
+  h_result->end_off = tail.end_off;
+  h_result->n_segments = tail.n_segments;
+  for (uint32_t i = 0; i < nf; ++i) {
+    h_result->n_live += fst[2 * i];
+    if (h_stats) {
+      h_stats[i].live_count = fst[2 * i];
+      h_stats[i].live_bytes = fst[2 * i + 1];
+    }
+  }
+  if (!live_ok || tot_c > pos_cap || tot_b > stream_cap || tail.n_segments > seg_cap ||
+      (tot_c && (!d_pos || !d_stream)) || (tail.n_segments && !h_segs)) {
+    MHIP(hipEventRecord(m->ev[3], s));
+    return h_result->status = LDB_ERR_CAPACITY;
+  }
+  if (tot_c) {
+    const uint32_t ngrp = (uint32_t)((n + 64 * kCopyWaves - 1) / (64 * kCopyWaves));
+    k_emit_copy<<<ngrp, 64 * kCopyWaves, 0, s>>>(m->recs, n, d_fd, nf, d_P, d_C, d_segs, tail.n_segments,
+                                                 d_stream, d_pos);
+    MHIP(hipGetLastError());
+  }
+  MHIP(hipEventRecord(m->ev[3], s));
+  if (tail.n_segments)
+    MHIP(hipMemcpyAsync(h_segs, d_segs, sizeof(ldb_merge_segment) * tail.n_segments, hipMemcpyDeviceToHost, s));
+  MHIP(hipStreamSynchronize(s));
+  MHIP(hipEventElapsedTime(&m->t_scan, m->ev[0], m->ev[1]));
+  MHIP(hipEventElapsedTime(&m->t_live, m->ev[1], m->ev[2]));
+  MHIP(hipEventElapsedTime(&m->t_compact, m->ev[2], m->ev[3]));
+  h_result->status = LDB_OK;
+  return LDB_OK;
+}
+
+extern "C" int ldb_merge_timing(ldb_ctx* ctx, double* scan_ms, double* live_ms, double* compact_ms) {
+  if (!ctx) return LDB_ERR_ARG;
+  MergeWs* m = static_cast<MergeWs*>(*ldb_ctx_merge_slot_(ctx));
+  if (!m) return LDB_ERR_ARG;
+  if (scan_ms) *scan_ms = m->t_scan;
+  if (live_ms) *live_ms = m->t_live;
+  if (compact_ms) *compact_ms = m->t_compact;
+  return LDB_OK;
+}

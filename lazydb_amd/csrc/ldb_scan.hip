@@ -756,7 +756,13 @@ struct ldb_ctx {
   hipStream_t h_stream = nullptr;
   double t_main = 0, t_total = 0;
   uint64_t t_n = 0;
+  void* merge = nullptr;       // merge/GC workspace (ldb_merge.hip), created on first use
 };
+
+// internal hooks for ldb_merge.hip (not part of the C ABI)
+__attribute__((visibility("hidden"))) void ldb_merge_release_(void* m);
+__attribute__((visibility("hidden"))) int ldb_ctx_device_(ldb_ctx* c) { return c->device; }
+__attribute__((visibility("hidden"))) void** ldb_ctx_merge_slot_(ldb_ctx* c) { return &c->merge; }
 
 static int resolve_timing(ldb_ctx* c) {
   for (size_t i = 0; i < c->ev_used; ++i) {
@@ -966,6 +972,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->h_out) (void)hipFree(c->h_out);
   if (c->h_res) (void)hipFree(c->h_res);
   if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
+  if (c->merge) ldb_merge_release_(c->merge);
   for (const ldb_ctx::EvTriple& t : c->evs) {
     (void)hipEventDestroy(t.e0);
     (void)hipEventDestroy(t.e1);

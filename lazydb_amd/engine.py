@@ -88,6 +88,67 @@ class Engine:
                                       out.ctypes.data, cap, C.byref(res)), "ldb_scan_file")
         return res, out[: min(res.n_entries, cap)]
 
+    # ---------------------------------------------------------------- merge / GC
+    def merge_dev(self, files, active_fid: int, active_off: int, max_file_size: int, now: int,
+                  io_type: int = N.FILEIO, stream_cap: int | None = None, pos_cap: int | None = None,
+                  seg_cap: int = 256, live_cap: int | None = None, want_live: bool = True, stream=None):
+        """Merge the target files of one value type (db.go:383-427 Merge + mergeStr + writeLogEntry).
+
+        files: list of (device uint8 tensor, fid, is_target), ascending fid. Returns a dict with
+        'result' (MergeResult), 'stream' (device tensor, the compacted bytes), 'pos' (ldb_merge_pos
+        records, numpy), 'segments' (numpy), 'live' (device uint8 tensor, one flag per replayed record)
+        and 'stats' (per-file numpy). Outputs that turn out too small are re-sized and the call repeated
+        (LDB_ERR_CAPACITY reports the sizes needed)."""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        arr = (N.MergeFile * max(len(files), 1))()
+        tgt_len = 0
+        tot_len = 0
+        for i, (img, fid, tg) in enumerate(files):
+            assert img.dtype == t.uint8 and img.is_cuda and img.is_contiguous()
+            arr[i].d_image = img.data_ptr() if img.numel() else None
+            arr[i].len = img.numel()
+            arr[i].fid = fid
+            arr[i].is_target = 1 if tg else 0
+            tot_len += img.numel()
+            tgt_len += img.numel() if tg else 0
+        stream_cap = tgt_len if stream_cap is None else stream_cap
+        pos_cap = tgt_len // 64 + 1024 if pos_cap is None else pos_cap
+        live_cap = tot_len // 64 + 1024 if live_cap is None else live_cap
+        if stream is None:
+            stream = t.cuda.current_stream(dev)
+        for _attempt in range(2):
+            d_stream = t.empty(max(stream_cap, 16), dtype=t.uint8, device=dev)
+            d_pos = t.empty(max(pos_cap, 1) * N.MERGE_POS.itemsize, dtype=t.uint8, device=dev)
+            d_live = t.empty(max(live_cap, 1), dtype=t.uint8, device=dev) if want_live else None
+            segs = np.zeros(max(seg_cap, 1), dtype=N.MERGE_SEGMENT)
+            stats = np.zeros(max(len(files), 1), dtype=N.MERGE_FILE_STAT)
+            res = N.MergeResult()
+            rc = N.lib().ldb_merge_files_dev(
+                self.ctx, len(files), C.addressof(arr), io_type, active_fid, active_off, max_file_size, now,
+                d_stream.data_ptr(), stream_cap, d_pos.data_ptr(), pos_cap, segs.ctypes.data, seg_cap,
+                d_live.data_ptr() if want_live else None, live_cap if want_live else 0, stats.ctypes.data,
+                C.byref(res), C.c_void_p(stream.cuda_stream))
+            if rc != N.ERR_CAPACITY or res.bad_file >= 0:
+                break
+            stream_cap = max(stream_cap, res.emit_bytes)
+            pos_cap = max(pos_cap, res.n_emit)
+            seg_cap = max(seg_cap, res.n_segments)
+            live_cap = max(live_cap, res.n_records)
+        if rc not in (N.LDB_OK,) and res.bad_file < 0:
+            N.check(rc, "ldb_merge_files_dev")
+        npos = min(res.n_emit, pos_cap)
+        pos = (np.frombuffer(d_pos[: npos * N.MERGE_POS.itemsize].cpu().numpy().tobytes(), dtype=N.MERGE_POS)
+               if npos else np.zeros(0, N.MERGE_POS))
+        return {"rc": rc, "result": res, "stream": d_stream[: res.emit_bytes],
+                "pos": pos, "segments": segs[: min(res.n_segments, seg_cap)],
+                "live": d_live[: res.n_records] if want_live else None, "stats": stats[: len(files)]}
+
+    def merge_timing(self):
+        a, b, c = C.c_double(), C.c_double(), C.c_double()
+        N.check(N.lib().ldb_merge_timing(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "merge_timing")
+        return a.value, b.value, c.value
+
     def read_ceiling(self, d_img, iters: int = 20) -> float:
         """GB/s of a read-only reduction over the device image (the practical HBM-read ceiling)."""
         g = C.c_double()

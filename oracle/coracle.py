@@ -117,3 +117,74 @@ def gen_log(cap_bytes: int, seed: int, ksize: int = 64, vsize: int = 256, value_
     n = lib().ldbo_gen_log(_ptr(img), cap_bytes, seed, ksize, vsize, value_mode, zipf_s, zipf_max, max_entries,
                            C.byref(end))
     return img, int(n), int(end.value)
+
+
+# ---------------------------------------------------------------- merge / GC (db.go:243-265, 383-427, 473-523)
+class MergeFile(C.Structure):
+    _fields_ = [("d_image", C.c_void_p), ("len", C.c_uint64), ("fid", C.c_uint32), ("is_target", C.c_uint32)]
+
+
+class MergeResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("bad_file", C.c_int32), ("n_records", C.c_uint64), ("n_live", C.c_uint64),
+                ("n_emit", C.c_uint64), ("emit_bytes", C.c_uint64), ("end_fid", C.c_uint32),
+                ("n_segments", C.c_uint32), ("end_off", C.c_uint64)]
+
+
+MERGE_POS = np.dtype([("offset", "<u8"), ("fid", "<u4"), ("entry_size", "<u4"), ("src_offset", "<u8"),
+                      ("src_file", "<u4"), ("reserved_", "<u4")])
+MERGE_SEGMENT = np.dtype([("fid", "<u4"), ("reserved_", "<u4"), ("file_off", "<u8"), ("stream_off", "<u8"),
+                          ("n_bytes", "<u8")])
+MERGE_FILE_STAT = np.dtype([("status", "<i4"), ("fid", "<u4"), ("n_entries", "<u8"), ("end_off", "<u8"),
+                            ("live_count", "<u8"), ("live_bytes", "<u8")])
+
+
+def merge(files, active_fid: int, active_off: int, max_file_size: int, now: int, io_type: int = 0):
+    """C restatement of Merge over host images. files: list of (uint8 ndarray, fid, is_target).
+    Returns (MergeResult, stream bytes ndarray, pos, segments, live flags, per-file stats)."""
+    L = lib()
+    if not hasattr(L.ldbo_merge, "_typed"):
+        L.ldbo_merge.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_uint32, C.c_uint64, C.c_uint64, C.c_int64,
+                                 C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p,
+                                 C.c_uint64, C.c_void_p, C.POINTER(MergeResult)]
+        L.ldbo_merge._typed = True
+    imgs = [np.ascontiguousarray(f[0], dtype=np.uint8) for f in files]
+    arr = (MergeFile * max(len(files), 1))()
+    tgt = 0
+    tot = 0
+    for i, (img, (_, fid, tg)) in enumerate(zip(imgs, files)):
+        arr[i].d_image = _ptr(img) if img.size else None
+        arr[i].len = img.size
+        arr[i].fid = fid
+        arr[i].is_target = 1 if tg else 0
+        tot += img.size
+        tgt += img.size if tg else 0
+    stream = np.zeros(max(tgt, 1), dtype=np.uint8)
+    pos_cap = tgt // 10 + 2
+    pos = np.zeros(pos_cap, dtype=MERGE_POS)
+    seg_cap = 1 << 16
+    segs = np.zeros(seg_cap, dtype=MERGE_SEGMENT)
+    live_cap = tot // 10 + 2
+    live = np.zeros(live_cap, dtype=np.uint8)
+    stats = np.zeros(max(len(files), 1), dtype=MERGE_FILE_STAT)
+    res = MergeResult()
+    L.ldbo_merge(len(files), C.addressof(arr), io_type, active_fid, active_off, max_file_size, now, _ptr(stream),
+                 stream.size, _ptr(pos), pos_cap, _ptr(segs), seg_cap, _ptr(live), live_cap, _ptr(stats), C.byref(res))
+    return (res, stream[: res.emit_bytes], pos[: res.n_emit], segs[: res.n_segments], live[: res.n_records],
+            stats[: len(files)])
+
+
+def gen_merge(n_files: int, cap_bytes: int, n_records: int, seed: int, ksize: int = 64, vsize: int = 256,
+              p_delete_ppm: int = 0, p_expire_ppm: int = 0, now: int = 1_700_000_000):
+    """Config-5-shaped merge set: consecutive files of cap_bytes, every key written twice.
+    Returns (list of per-file uint8 arrays (views of one buffer), records written, end offsets)."""
+    L = lib()
+    if not hasattr(L.ldbo_gen_merge, "_typed"):
+        L.ldbo_gen_merge.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
+                                     C.c_uint32, C.c_uint32, C.c_uint32, C.c_int64, C.c_void_p]
+        L.ldbo_gen_merge.restype = C.c_uint64
+        L.ldbo_gen_merge._typed = True
+    buf = np.zeros(n_files * cap_bytes, dtype=np.uint8)
+    ends = np.zeros(n_files, dtype=np.uint64)
+    n = L.ldbo_gen_merge(_ptr(buf), n_files, cap_bytes, n_records, seed, ksize, vsize, p_delete_ppm, p_expire_ppm,
+                         now, _ptr(ends))
+    return [buf[i * cap_bytes:(i + 1) * cap_bytes] for i in range(n_files)], int(n), [int(e) for e in ends]

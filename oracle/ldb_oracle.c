@@ -356,3 +356,235 @@ uint64_t ldbo_gen_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint32_t 
   if (end_off) *end_off = off;
   return n;
 }
+
+/* ================================================================== merge / GC
+ * Restates, for the string value type:
+ *   index.go:68-95 + :15-26  replay in (fid, offset) order: SDelete -> idxTree.Delete(key), else Put
+ *   db.go:383-427            Merge over the target files in ascending fid (discard.go:224 sorts the ccl):
+ *                            ReadLogEntry loop; skip SDelete (:403); skip ExpiredAt != 0 && <= now (:406)
+ *   db.go:243-265            mergeStr: rewrite iff index[key] == (fid, offset); then updateIndexTree
+ *   db.go:473-523            writeLogEntry: EncodeEntry; rollover when Offset + size > MaxLogFileSize
+ * The index is an open-addressing map keyed by the full key bytes (FNV-1a): value = record id of the
+ * key's current index entry, -1 after Delete, -2 once rewritten to a new position. */
+typedef struct { const uint8_t* key; uint32_t klen; int64_t val; } mapent;
+typedef struct { mapent* t; uint64_t mask; } kmap;
+
+static uint64_t fnv1a(const uint8_t* p, uint32_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+  return h;
+}
+
+static mapent* kmap_find(kmap* m, const uint8_t* key, uint32_t klen, int create) {
+  uint64_t i = fnv1a(key, klen) & m->mask;
+  for (;;) {
+    mapent* e = &m->t[i];
+    if (!e->key) {
+      if (!create) return NULL;
+      e->key = key ? key : (const uint8_t*)"";
+      e->klen = klen;
+      e->val = -1;
+      return e;
+    }
+    if (e->klen == klen && (klen == 0 || memcmp(e->key, key, klen) == 0)) return e;
+    i = (i + 1) & m->mask;
+  }
+}
+
+int ldbo_merge(int n_files, const ldb_merge_file* files, int io_type, uint32_t active_fid, uint64_t active_off,
+               uint64_t max_size, int64_t now, uint8_t* stream, uint64_t stream_cap, ldb_merge_pos* pos,
+               uint64_t pos_cap, ldb_merge_segment* segs, uint32_t seg_cap, uint8_t* live, uint64_t live_cap,
+               ldb_merge_file_stat* stats, ldb_merge_result* res) {
+  memset(res, 0, sizeof(*res));
+  res->bad_file = -1;
+  res->end_fid = active_fid;
+  res->end_off = active_off;
+  /* 1. replay every file (index.go:84-95) into one record table */
+  uint64_t cap = 0;
+  for (int i = 0; i < n_files; ++i) cap += files[i].len / 10 + 2;
+  ldb_entry* recs = (ldb_entry*)malloc(sizeof(ldb_entry) * (cap ? cap : 1));
+  uint32_t* rfile = (uint32_t*)malloc(sizeof(uint32_t) * (cap ? cap : 1));
+  uint64_t n = 0;
+  for (int i = 0; i < n_files; ++i) {
+    ldb_scan_result r;
+    ldbo_scan(files[i].d_image, files[i].len, io_type, files[i].fid, LDB_TUPLE_ENTRY, recs + n, cap - n, &r);
+    if (stats) {
+      memset(&stats[i], 0, sizeof(stats[i]));
+      stats[i].status = r.status;
+      stats[i].fid = files[i].fid;
+      stats[i].n_entries = r.n_entries;
+      stats[i].end_off = r.end_off;
+    }
+    if (r.status < 0) {
+      res->status = r.status;
+      res->bad_file = i;
+      res->n_records = n + r.n_entries;
+      free(recs);
+      free(rfile);
+      return r.status;
+    }
+    for (uint64_t j = 0; j < r.n_entries; ++j) rfile[n + j] = (uint32_t)i;
+    n += r.n_entries;
+  }
+  res->n_records = n;
+  kmap m;
+  uint64_t tc = 1024;
+  while (tc < 2 * n) tc <<= 1;
+  m.t = (mapent*)calloc(tc, sizeof(mapent));
+  m.mask = tc - 1;
+#define KEY(s) (files[rfile[s]].d_image + recs[s].offset + recs[s].hdr_size)
+  /* buildStrIndex (index.go:15-26) */
+  for (uint64_t s = 0; s < n; ++s) {
+    mapent* e = kmap_find(&m, KEY(s), recs[s].k_size, 1);
+    e->val = recs[s].stat == 1 ? -1 : (int64_t)s; /* SDelete: Delete(key); else Put */
+  }
+  for (uint64_t s = 0; s < n; ++s) {
+    int lv = kmap_find(&m, KEY(s), recs[s].k_size, 0)->val == (int64_t)s;
+    if (live && s < live_cap) live[s] = (uint8_t)lv;
+    if (lv) {
+      res->n_live++;
+      if (stats) {
+        stats[rfile[s]].live_count++;
+        stats[rfile[s]].live_bytes += (uint64_t)recs[s].enc_hdr_size + recs[s].k_size + recs[s].v_size;
+      }
+    }
+  }
+  /* 2. Merge (db.go:383-427) with writeLogEntry (db.go:473-523) */
+  uint32_t fid = active_fid;
+  uint64_t off = active_off, sp = 0, ne = 0;
+  uint32_t ns = 0;
+  uint8_t* buf = NULL;
+  size_t bufcap = 0;
+  int over = (live && live_cap < n);
+  for (uint64_t s = 0; s < n; ++s) {
+    const ldb_entry* e = &recs[s];
+    if (!files[rfile[s]].is_target) continue;
+    if (e->stat == 1) continue;                                  /* :403 */
+    if (e->expired_at != 0 && e->expired_at <= now) continue;    /* :406-409 */
+    mapent* me = kmap_find(&m, KEY(s), e->k_size, 0);
+    if (me->val != (int64_t)s) continue;                         /* mergeStr :255 */
+    size_t need = LDBO_MAX_HEADER + (size_t)e->k_size + e->v_size;
+    if (need > bufcap) {
+      bufcap = need * 2;
+      buf = (uint8_t*)realloc(buf, bufcap);
+    }
+    const uint8_t* k = KEY(s);
+    size_t size = ldbo_encode_entry(e->stat, e->expired_at, e->tx_id, e->tx_stat, k, e->k_size, k + e->k_size,
+                                    e->v_size, buf);                 /* :482 EncodeEntry */
+    if (off + size > max_size) {                                 /* :485 rollover */
+      fid += 1;
+      off = 0;
+    }
+    if (ns == 0 || segs == NULL || ns > seg_cap || segs[ns - 1].fid != fid ||
+        segs[ns - 1].file_off + segs[ns - 1].n_bytes != off) {
+      if (segs && ns < seg_cap) {
+        segs[ns].fid = fid;
+        segs[ns].reserved_ = 0;
+        segs[ns].file_off = off;
+        segs[ns].stream_off = sp;
+        segs[ns].n_bytes = 0;
+      }
+      ++ns;
+    }
+    if (segs && ns <= seg_cap) segs[ns - 1].n_bytes += size;
+    if (stream && sp + size <= stream_cap) memcpy(stream + sp, buf, size);
+    else over = 1;
+    if (pos && ne < pos_cap) {
+      pos[ne].offset = off;
+      pos[ne].fid = fid;
+      pos[ne].entry_size = (uint32_t)size;
+      pos[ne].src_offset = e->offset;
+      pos[ne].src_file = rfile[s];
+      pos[ne].reserved_ = 0;
+    } else {
+      over = 1;
+    }
+    me->val = -2;                                                /* updateIndexTree: new position */
+    ++ne;
+    sp += size;
+    off += size;
+  }
+#undef KEY
+  free(buf);
+  free(m.t);
+  free(recs);
+  free(rfile);
+  res->n_emit = ne;
+  res->emit_bytes = sp;
+  res->end_fid = fid;
+  res->end_off = off;
+  res->n_segments = ns;
+  if (over || ns > seg_cap) res->status = LDB_ERR_CAPACITY;
+  return res->status;
+}
+
+/* Merge test set (BASELINE config 5 shape): n_records records of ksize-byte keys / vsize-byte values,
+ * appended to consecutive files of cap_bytes with writeLogEntry's rollover rule (db.go:485); file f
+ * is imgs + f*cap_bytes. Records are paired by a splitmix64(seed) Fisher-Yates permutation: pair i =
+ * (perm[2i], perm[2i+1]) shares key i, so each key is written twice and exactly half the records are
+ * stale. With probability p_delete_ppm/1e6 a pair's later record is an SDelete (empty value); with
+ * p_expire_ppm/1e6 a record carries ExpiredAt = now -/+ 1000 (half expired). Returns the records
+ * written; end_offs[f] receives each file's append offset. */
+uint64_t ldbo_gen_merge(uint8_t* imgs, uint32_t n_files, uint64_t cap_bytes, uint64_t n_records, uint64_t seed,
+                        uint32_t ksize, uint32_t vsize, uint32_t p_delete_ppm, uint32_t p_expire_ppm, int64_t now,
+                        uint64_t* end_offs) {
+  uint64_t st = seed;
+  n_records &= ~1ull;
+  uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * (n_records ? n_records : 1));
+  uint32_t* keyid = (uint32_t*)malloc(sizeof(uint32_t) * (n_records ? n_records : 1));
+  uint8_t* later = (uint8_t*)calloc(n_records ? n_records : 1, 1);
+  for (uint64_t i = 0; i < n_records; ++i) perm[i] = (uint32_t)i;
+  for (uint64_t i = n_records; i > 1; --i) {
+    uint64_t j = ldbo_splitmix64(&st) % i;
+    uint32_t t = perm[i - 1];
+    perm[i - 1] = perm[j];
+    perm[j] = t;
+  }
+  for (uint64_t i = 0; i < n_records / 2; ++i) {
+    uint32_t a = perm[2 * i], b = perm[2 * i + 1];
+    keyid[a] = keyid[b] = (uint32_t)i;
+    later[a > b ? a : b] = 1;
+  }
+  uint8_t* key = (uint8_t*)malloc(ksize + 32);
+  uint8_t* val = (uint8_t*)malloc(vsize + 8);
+  uint64_t off = 0, w = 0;
+  uint32_t f = 0;
+  for (uint32_t i = 0; i < n_files; ++i) end_offs[i] = 0;
+  for (; w < n_records; ++w) {
+    char num[32];
+    int nd = 0;
+    uint64_t t = keyid[w];
+    do { num[nd++] = (char)('0' + t % 10); t /= 10; } while (t);
+    memset(key, '0', ksize);
+    if (ksize >= 4) memcpy(key, "key-", 4);
+    for (int i = 0; ksize >= 4 && i < nd && (uint32_t)i < ksize - 4; ++i) key[ksize - 1 - i] = (uint8_t)num[i];
+    uint8_t stat = 0;
+    uint32_t vl = vsize;
+    int64_t exp = 0;
+    uint64_t r = ldbo_splitmix64(&st);
+    if (later[w] && (r % 1000000) < p_delete_ppm) {
+      stat = 1;
+      vl = 0;
+    }
+    r = ldbo_splitmix64(&st);
+    if ((r % 1000000) < p_expire_ppm) exp = (r >> 40) & 1 ? now - 1000 : now + 1000;
+    for (uint32_t i = 0; i < vl; i += 8) {
+      uint64_t x = ldbo_splitmix64(&st);
+      for (int b = 0; b < 8 && i + b < vl; ++b) { val[i + b] = (uint8_t)kAlphabet[(x & 0xff) % 36]; x >>= 8; }
+    }
+    uint64_t need = 5 + ldbo_varint_len(exp) + 2 + ldbo_varint_len(ksize) + ldbo_varint_len(vl) + ksize + vl;
+    if (off + need > cap_bytes) { /* db.go:485 rollover */
+      end_offs[f] = off;
+      if (++f >= n_files) break;
+      off = 0;
+    }
+    off += ldbo_encode_entry(stat, exp, 0, 0, key, ksize, val, vl, imgs + (uint64_t)f * cap_bytes + off);
+  }
+  if (f < n_files) end_offs[f] = off;
+  free(perm);
+  free(keyid);
+  free(later);
+  free(key);
+  free(val);
+  return w;
+}

@@ -91,6 +91,19 @@ int ldbo_scan_faithful(int fd, uint64_t len, int io_type, uint32_t fid, ldb_inde
 uint64_t ldbo_gen_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint32_t ksize, uint32_t vsize,
                       int value_mode, double zipf_s, uint32_t zipf_max, uint64_t max_entries, uint64_t* end_off);
 
+/* Merge/GC restatement (db.go:243-265, 383-427, 473-523 over the index of index.go:15-26, 68-95).
+ * files[i].d_image is a HOST pointer here. Same outputs and capacity rules as ldb_merge_files_dev. */
+int ldbo_merge(int n_files, const ldb_merge_file* files, int io_type, uint32_t active_fid, uint64_t active_off,
+               uint64_t max_size, int64_t now, uint8_t* stream, uint64_t stream_cap, ldb_merge_pos* pos,
+               uint64_t pos_cap, ldb_merge_segment* segs, uint32_t seg_cap, uint8_t* live, uint64_t live_cap,
+               ldb_merge_file_stat* stats, ldb_merge_result* res);
+
+/* Merge test set (config 5 shape): every key written twice (half the records stale), optional SDelete /
+ * ExpiredAt mix, consecutive files of cap_bytes at imgs + f*cap_bytes. */
+uint64_t ldbo_gen_merge(uint8_t* imgs, uint32_t n_files, uint64_t cap_bytes, uint64_t n_records, uint64_t seed,
+                        uint32_t ksize, uint32_t vsize, uint32_t p_delete_ppm, uint32_t p_expire_ppm, int64_t now,
+                        uint64_t* end_offs);
+
 /* splitmix64 (shared by generator and tests) */
 uint64_t ldbo_splitmix64(uint64_t* state);
 

@@ -179,3 +179,56 @@ def scan(img: bytes, io_type: int = FILEIO, fid: int = 0):
 
 def pack_pos(off: int, h: int, eh: int, stat: int) -> int:
     return (off & 0xFFFFFFFFFF) | ((h & 0x3F) << 40) | ((eh & 0x3F) << 46) | ((stat & 0xFF) << 52)
+
+
+def merge(files, active_fid: int, active_off: int, max_file_size: int, now: int, io_type: int = FILEIO):
+    """Merge of the string type, written as the reference runs it (pure Python; small inputs only).
+
+    files: [(image bytes, fid, is_target)] ascending fid. Replays every file into a dict index
+    (index.go:68-95, buildStrIndex :15-26: SDelete -> Delete, else Put), then for each target file
+    in ascending fid runs db.go:383-427 (skip SDelete :403, skip expired :406-409, mergeStr :255 ->
+    writeLogEntry db.go:473-523 with EncodeEntry and the rollover rule, then updateIndexTree).
+    Returns dict(status, bad_file, stream, pos [(fid, off, size, src_off, src_file)],
+    segments [(fid, file_off, stream_off, n_bytes)], live [0/1 per record], end_fid, end_off)."""
+    recs = []   # (file index, offset, Entry)
+    for fi, (img, fid, _) in enumerate(files):
+        off = 0
+        while True:
+            st, e, es, _h = read_log_entry(img, io_type, off)
+            if st != OK:
+                break
+            recs.append((fi, off, e))
+            off += es
+        if st < 0:
+            return {"status": st, "bad_file": fi}
+    index = {}
+    for i, (fi, off, e) in enumerate(recs):
+        if e.stat == 1:
+            index.pop(e.key, None)   # idxTree.Delete
+        else:
+            index[e.key] = (fi, off)   # idxTree.Put
+    live = [1 if index.get(e.key) == (fi, off) else 0 for (fi, off, e) in recs]
+    fid, foff = active_fid, active_off
+    stream = bytearray()
+    pos, segs = [], []
+    for (fi, off, e) in recs:
+        if not files[fi][2]:
+            continue
+        if e.stat == 1:
+            continue
+        if e.expired_at != 0 and e.expired_at <= now:
+            continue
+        if index.get(e.key) != (fi, off):
+            continue
+        buf = encode_entry(e)
+        if foff + len(buf) > max_file_size:
+            fid, foff = fid + 1, 0
+        if not segs or segs[-1][0] != fid or segs[-1][1] + segs[-1][3] != foff:
+            segs.append([fid, foff, len(stream), 0])
+        segs[-1][3] += len(buf)
+        pos.append((fid, foff, len(buf), off, fi))
+        index[e.key] = ("new", fid, foff)   # updateIndexTree with the new ValuePos
+        stream += buf
+        foff += len(buf)
+    return {"status": 0, "bad_file": -1, "stream": bytes(stream), "pos": pos, "segments": [tuple(s) for s in segs],
+            "live": live, "end_fid": fid, "end_off": foff}

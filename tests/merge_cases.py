@@ -1,0 +1,99 @@
+"""Merge/GC test cases shared by the CPU oracle tests and the GPU parity tests.
+
+Each case is (files, kwargs): files = [(uint8 ndarray image, fid, is_target)] in ascending fid,
+kwargs = active_fid / active_off / max_file_size / now / io_type for Merge (db.go:383-427).
+Images come from the oracle's generators (writeLogEntry format) and the committed golden fixtures.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from oracle import coracle
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NOW = 1_700_000_000
+
+
+def ref_key(n: int) -> bytes:   # db_test.go:336-338 GetKey
+    return b"kvstore-bench-key------" + b"%09d" % n
+
+
+def _log(entries, size: int | None = None) -> np.ndarray:
+    buf = b"".join(coracle.encode_entry(**e) for e in entries)
+    img = np.zeros(len(buf) if size is None else size, dtype=np.uint8)
+    img[: len(buf)] = np.frombuffer(buf, dtype=np.uint8)
+    return img
+
+
+def golden_img(name: str) -> np.ndarray:
+    with open(os.path.join(GOLDEN, name + ".bin"), "rb") as f:
+        return np.frombuffer(f.read(), dtype=np.uint8).copy()
+
+
+def case_ref_writelogentry():
+    """db_test.go:182-229 TestLazyDB_WriteLogEntry: MaxLogFileSize 150, 32-B keys and values ->
+    74-B entries at (1, 0), (1, 74), (2, 0). Here the three records are rewritten by a merge of
+    archived file 0 into the empty active file 1."""
+    val = bytes(range(65, 97))
+    src = _log([dict(key=ref_key(i), value=val) for i in (1, 2, 3)])
+    active = np.zeros(150, dtype=np.uint8)
+    return [(src, 0, True), (active, 1, False)], dict(active_fid=1, active_off=0, max_file_size=150, now=NOW)
+
+
+def case_ref_merge_shape():
+    """db_test.go:64-109 TestLazyDB_Merge shape (strings only): MaxLogFileSize 500, Set(key1) x100
+    then Set(key2) x100 with GetKey(32)-sized values; every archived file is merged."""
+    recs = [dict(key=ref_key(1), value=ref_key(32))] * 100 + [dict(key=ref_key(2), value=ref_key(32))] * 100
+    per = 500 // 74
+    files = []
+    for f in range(0, (len(recs) + per - 1) // per):
+        files.append(_log(recs[f * per:(f + 1) * per], 500))
+    last = len(files) - 1
+    active_off = (len(recs) - last * per) * 74
+    return ([(img, f, f != last) for f, img in enumerate(files)],
+            dict(active_fid=last, active_off=active_off, max_file_size=500, now=NOW))
+
+
+def case_generated(seed: int, n_files: int = 5, cap: int = 1 << 16, n_records: int = 900, max_file_size: int = 1 << 15,
+                   p_delete: int = 50_000, p_expire: int = 50_000, ksize: int = 24, vsize: int = 40, targets=None):
+    imgs, n, ends = coracle.gen_merge(n_files, cap, n_records, seed, ksize=ksize, vsize=vsize,
+                                      p_delete_ppm=p_delete, p_expire_ppm=p_expire, now=NOW)
+    if targets is None:
+        targets = set(range(n_files - 1))
+    last = n_files - 1
+    files = [(imgs[i].copy(), 10 + i, i in targets) for i in range(n_files)]
+    return files, dict(active_fid=10 + last, active_off=ends[last], max_file_size=max_file_size, now=NOW)
+
+
+def case_golden_mix():
+    """Golden fixtures as the files of one type: stat mix (SDelete / SListMeta), nil keys, empty
+    values, non-canonical varints (re-encoded by EncodeEntry), big and binary values."""
+    names = ["mixed_64k", "noncanonical", "noncanonical5", "zero_len_entries", "binary_values", "big_values",
+             "ref_read_entries"]
+    files = [(golden_img(nm), 3 + i, i != len(names) - 1) for i, nm in enumerate(names)]
+    return files, dict(active_fid=3 + len(names) - 1, active_off=0, max_file_size=1 << 17, now=NOW)
+
+
+def case_oversized():
+    """Records larger than MaxLogFileSize: each roll-over check fires even at offset 0 (db.go:485)."""
+    recs = [dict(key=b"k%d" % (i % 7), value=bytes([97 + i % 26]) * (30 + 17 * i)) for i in range(40)]
+    return [(_log(recs[:20]), 1, True), (_log(recs[20:]), 2, True), (np.zeros(64, np.uint8), 3, False)], \
+        dict(active_fid=3, active_off=10, max_file_size=200, now=NOW)
+
+
+def case_crc_corrupt():
+    return [(golden_img("mixed_64k"), 1, True), (golden_img("crc_corrupt"), 2, True),
+            (np.zeros(64, np.uint8), 3, False)], dict(active_fid=3, active_off=0, max_file_size=1 << 20, now=NOW)
+
+
+def small_cases():
+    out = {"ref_writelogentry": case_ref_writelogentry(), "ref_merge_shape": case_ref_merge_shape(),
+           "golden_mix": case_golden_mix(), "oversized": case_oversized(), "crc_corrupt": case_crc_corrupt()}
+    for s in range(1, 5):
+        out[f"gen{s}"] = case_generated(s)
+    out["gen_no_targets"] = case_generated(7, targets=set())
+    out["gen_all_but_one"] = case_generated(8, n_files=6, targets={0, 1, 3, 4}, max_file_size=5000)
+    out["gen_mmap"] = (case_generated(9)[0], dict(case_generated(9)[1], io_type=1))
+    return out

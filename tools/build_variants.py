@@ -52,7 +52,7 @@ def build(name: str) -> str:
         raise SystemExit(f"unknown variant {name}")
     out = os.path.join(OUT, f"var_{name}.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    "-Wno-unused-function", *defs, "-o", out, SRC], check=True)
+                    "-Wno-unused-function", *defs, "-o", out, SRC, SRC.replace("ldb_scan.hip", "ldb_merge.hip")], check=True)
     return out
 
 
