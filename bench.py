@@ -33,8 +33,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
-                    help="BASELINE config: 2 = 1 GiB fixed 64/256; 3 = 8 GiB Zipf values; 4 = 4 GiB per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="BASELINE config: 2 = 1 GiB fixed 64/256; 3 = 8 GiB Zipf values; 4 = 4 GiB per GPU; "
+                         "5 = merge/GC of 16 x 256 MiB files, half the records stale (a separate bench line)")
     ap.add_argument("--io", type=int, default=0, help="0 FileIO bound rule, 1 Mmap")
     ap.add_argument("--kind", type=int, default=0, help="0 index tuples (16 B), 1 full entries (48 B)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -116,8 +117,98 @@ def _cpu_model():
     return "unknown"
 
 
+def main_merge(args):
+    """BASELINE config 5: Merge/GC of one value type -- 16 log files x 256 MiB (64-B keys, 256-B values,
+    every key written twice so exactly half the records are stale), 15 archived targets merged into
+    the active file 16: replay scans + last-writer-wins liveness + compacted stream with rollover
+    (db.go:383-427, 243-265, 473-523). One step = one ldb_merge_files_dev call over device-resident
+    images. With N ranks each rank merges its own independent 16-file set (weak scaling; the
+    cross-rank liveness exchange of SURVEY 8(e) is not built yet)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    from lazydb_amd import Engine
+    from lazydb_amd import multi
+    from oracle import coracle   # format producer for the synthetic input; checker
+    now = 1_700_000_000
+    imgs, n, ends = coracle.gen_merge(16, 256 << 20, 16 * 808_540, 3 + rank, ksize=64, vsize=256)
+    files = [(torch.from_numpy(imgs[i]).to(dev), i + 1, i < 15) for i in range(16)]
+    eng = Engine(local)
+    kw = dict(active_fid=16, active_off=ends[15], max_file_size=256 << 20, now=now)
+    out = eng.merge_dev(files, **kw)
+    r = out["result"]
+    verified = None
+    if not args.no_verify:
+        ref, stream, pos, segs, live, stats = coracle.merge([(imgs[i], i + 1, i < 15) for i in range(16)], 16,
+                                                            ends[15], 256 << 20, now)
+        verified = bool((r.status, r.n_emit, r.emit_bytes, r.end_fid, r.end_off) ==
+                        (ref.status, ref.n_emit, ref.emit_bytes, ref.end_fid, ref.end_off)
+                        and out["pos"].tobytes() == pos.tobytes()
+                        and torch.equal(out["stream"], torch.from_numpy(stream).to(dev)))
+        del stream, pos, live
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        t0 = time.perf_counter()
+        coracle.merge([(imgs[i], i + 1, i < 15) for i in range(16)], 16, ends[15], 256 << 20, now)
+        dt = time.perf_counter() - t0
+        cpu = {"value": round(sum(ends) / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": "the full 16-file set: oracle replay + map-based index + EncodeEntry rewrite, 1 thread",
+               "host_cpu": _cpu_model(), "host_nproc": os.cpu_count()}
+    caps = dict(stream_cap=int(r.emit_bytes) + 16, pos_cap=int(r.n_emit) + 16, seg_cap=64,
+                live_cap=int(r.n_records) + 16, fetch_pos=False)
+    for _ in range(args.warmup):
+        eng.merge_dev(files, **kw, **caps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ph = np.zeros(3)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.merge_dev(files, **kw, **caps)
+        ph += np.array(eng.merge_timing())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = multi.max_over_ranks(time.perf_counter() - t0, dev)
+    ph /= args.steps
+    in_bytes = sum(ends)
+    tot_in = multi.sum_over_ranks([in_bytes], dev)[0]
+    if rank == 0:
+        step = t / args.steps
+        dev_ms = float(ph.sum())
+        alg = in_bytes + 2 * int(r.emit_bytes)   # replay read + compacted stream read and written
+        print(json.dumps({
+            "metric": "merge/GC decode+CRC32+liveness+compaction: input GiB/s (BASELINE config 5)",
+            "value": round(tot_in / step / 2**30, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(step * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (writeLogEntry format, every key written twice)",
+            "config": {"workload": "16 log files x 256 MiB, 64B key / 256B value, 50% stale, 15 targets",
+                       "records": int(r.n_records), "live": int(r.n_live), "emitted": int(r.n_emit),
+                       "emit_bytes": int(r.emit_bytes), "segments": int(r.n_segments),
+                       "parallelism": f"one 16-file set per GPU x{world}"},
+            "phases_ms": {"replay_scans": round(ph[0], 3), "liveness": round(ph[1], 3),
+                          "compaction": round(ph[2], 3)},
+            "roofline": {"bound": "hbm", "kernel": "whole merge pipeline (device time)",
+                         "achieved": round(alg / (dev_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(alg / (dev_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": alg},
+            "verified_vs_oracle": verified, "cpu_baseline": cpu}))
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.config == 5:
+        return main_merge(args)
     import numpy as np
     import torch
     import torch.distributed as dist

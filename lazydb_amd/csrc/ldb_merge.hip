@@ -18,9 +18,10 @@
 //
 // Device pipeline (one context stream, synchronous API):
 //   replay scans    ldb_scan_file_dev per file (ldb_scan.hip), 48-B ldb_entry records, dense
-//   k_locate        per record: key address + 64-bit key hash                (HBM: key bytes + 48 B)
-//   k_insert        open-addressing table keyed by full key bytes; slot = atomicMax(seq)   (random)
-//   k_live          per record: live = (slot max == seq) && !SDelete; emit flag, sizes, per-file stats
+//   k_insert        per record: 64-bit key hash, open-addressing table keyed by the full key bytes,
+//                   slot max = atomicMax(seq)                            (key bytes + random slot lines)
+//   k_live          per record: live = (slot max == seq) && !SDelete; emit flag, sizes; per-block partials
+//   k_file_stats    per file: live counts and bytes
 //   k_scan_*        exclusive prefix sums of emitted bytes and counts (3-kernel reduce-then-scan)
 //   k_pack          one lane: greedy rollover packing by binary search over the byte prefix
 //   k_emit_copy     one wave per 64 records: new ValuePos, unaligned 16-B copies of the emitted bytes,
@@ -135,86 +136,128 @@ __device__ __forceinline__ uint32_t crc_byte(uint32_t c, uint8_t b) {   // refle
 }
 
 // ------------------------------------------------------------------------------ liveness
-__global__ __launch_bounds__(256) void k_locate(const ldb_entry* __restrict__ recs, uint64_t n,
-                                                const FileDesc* __restrict__ fd, uint32_t n_files,
-                                                uint64_t* __restrict__ hash, uint64_t* __restrict__ keyptr) {
-  uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (seq >= n) return;
-  const ldb_entry e = recs[seq];
-  const uint8_t* kp = fd[file_of(fd, n_files, seq)].img + e.offset + e.hdr_size;
-  hash[seq] = key_hash(kp, e.k_size);
-  keyptr[seq] = (uint64_t)kp;
-}
-
 // Insert every record into an open-addressing table keyed by the FULL key bytes: a slot word is
 // (hash tag << 32 | representative seq + 1), claimed by CAS; a probe that meets its tag compares its key
 // with the representative's, so distinct keys never share a slot whatever their hashes. The slot's
 // max word (atomicMax of seq + 1) ends as the key's last record (index.go: later Put/Delete wins).
+__device__ __forceinline__ const uint8_t* key_of(const ldb_entry* recs, const FileDesc* fd, uint32_t n_files,
+                                                uint64_t seq, uint32_t* kl) {
+  const ldb_entry& e = recs[seq];
+  *kl = e.k_size;
+  return fd[file_of(fd, n_files, seq)].img + e.offset + e.hdr_size;
+}
+
+// A slot is 16 B: word 0 = (hash tag << 32 | representative seq + 1), word 1 low half = max seq + 1, so the
+// claim and the max update touch one cache line.
 __global__ __launch_bounds__(256) void k_insert(const ldb_entry* __restrict__ recs, uint64_t n,
-                                                const uint64_t* __restrict__ hash,
-                                                const uint64_t* __restrict__ keyptr, uint64_t* tab_key,
-                                                uint32_t* tab_max, uint64_t mask, uint32_t* __restrict__ slot) {
+                                                const FileDesc* __restrict__ fd, uint32_t n_files, uint64_t* tab,
+                                                uint64_t mask, uint32_t* __restrict__ slot) {
   uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (seq >= n) return;
-  const uint64_t h = hash[seq];
+  uint32_t kl;
+  const uint8_t* kp = key_of(recs, fd, n_files, seq, &kl);
+  const uint64_t h = key_hash(kp, kl);
   const uint64_t mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
-  const uint8_t* kp = reinterpret_cast<const uint8_t*>(keyptr[seq]);
-  const uint32_t kl = recs[seq].k_size;
   uint64_t i = h & mask;
   for (;;) {
-    uint64_t v = __hip_atomic_load(&tab_key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t v = __hip_atomic_load(&tab[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v == 0) {
-      uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tab_key[i]), 0ull,
-                                (unsigned long long)mine);
+      uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[2 * i]), 0ull, (unsigned long long)mine);
       if (prev == 0) break;
       v = prev;
     }
     if ((v >> 32) == (h >> 32)) {
-      uint64_t rep = (v & 0xFFFFFFFFull) - 1;
-      if (recs[rep].k_size == kl && key_equal(kp, reinterpret_cast<const uint8_t*>(keyptr[rep]), kl)) break;
+      uint32_t rl;
+      const uint8_t* rp = key_of(recs, fd, n_files, (v & 0xFFFFFFFFull) - 1, &rl);
+      if (rl == kl && key_equal(kp, rp, kl)) break;
     }
     i = (i + 1) & mask;
   }
-  atomicMax(&tab_max[i], (uint32_t)(seq + 1));
+  atomicMax(reinterpret_cast<uint32_t*>(&tab[2 * i + 1]), (uint32_t)(seq + 1));
   slot[seq] = (uint32_t)i;
 }
 
 // live = last record of its key and not an SDelete (index.go:16-25); emit = live && target file &&
-// not expired (db.go:403-409, 255). Per-file live counts/bytes for discard accounting.
+// not expired (db.go:403-409, 255). Per-file live counts/bytes: a block whose records all lie in one
+// file writes one partial (k_file_stats sums them); a block that straddles files adds per record.
 __global__ __launch_bounds__(256) void k_live(const ldb_entry* __restrict__ recs, uint64_t n,
                                               const FileDesc* __restrict__ fd, uint32_t n_files,
-                                              const uint32_t* __restrict__ tab_max, const uint32_t* __restrict__ slot,
+                                              const uint64_t* __restrict__ tab, const uint32_t* __restrict__ slot,
                                               int64_t now, uint8_t* __restrict__ live_out,
-                                              uint32_t* __restrict__ esz, unsigned long long* __restrict__ fstat) {
-  uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                              uint32_t* __restrict__ esz, unsigned long long* __restrict__ part,
+                                              unsigned long long* __restrict__ fstat) {
+  __shared__ unsigned long long sc[4], sb[4];
+  const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x;
+  const uint64_t seq = b0 + threadIdx.x;
   const bool valid = seq < n;
   uint32_t f = 0, size = 0;
   bool live = false;
   if (valid) {
     const ldb_entry e = recs[seq];
     f = file_of(fd, n_files, seq);
-    live = tab_max[slot[seq]] == (uint32_t)(seq + 1) && e.stat != kSDelete;
+    const uint32_t mx = (uint32_t)tab[2 * (uint64_t)slot[seq] + 1];
+    live = mx == (uint32_t)(seq + 1) && e.stat != kSDelete;
     size = (uint32_t)e.enc_hdr_size + e.k_size + e.v_size;
     const bool expired = e.expired_at != 0 && e.expired_at <= now;
     esz[seq] = (live && fd[f].is_target && !expired) ? size : 0u;
     if (live_out) live_out[seq] = live ? 1 : 0;
   }
-  // per-file stats: one atomic pair per wave when the wave's records share a file (the common case)
-  const uint32_t f0 = __shfl(f, 0);
-  const bool uniform = __all(!valid || f == f0);
-  if (uniform) {
-    unsigned long long c = live ? 1ull : 0ull, b = live ? (unsigned long long)size : 0ull;
-    for (int o = 32; o > 0; o >>= 1) {
-      c += __shfl_xor(c, o);
-      b += __shfl_xor(b, o);
+  const uint64_t last = min(n, b0 + blockDim.x) - 1;
+  const bool uniform = file_of(fd, n_files, b0) == file_of(fd, n_files, last);
+  if (!uniform) {
+    if (valid && live) {
+      atomicAdd(&fstat[2 * f], 1ull);
+      atomicAdd(&fstat[2 * f + 1], (unsigned long long)size);
     }
-    if ((threadIdx.x & 63) == 0 && c) {
-      atomicAdd(&fstat[2 * f0], c);
-      atomicAdd(&fstat[2 * f0 + 1], b);
+    if (threadIdx.x == 0) part[2 * blockIdx.x] = part[2 * blockIdx.x + 1] = 0;
+    return;
+  }
+  unsigned long long c = live ? 1ull : 0ull, b = live ? (unsigned long long)size : 0ull;
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    b += __shfl_xor(b, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sc[threadIdx.x >> 6] = c;
+    sb[threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = sc[0] + sc[1] + sc[2] + sc[3];
+    part[2 * blockIdx.x + 1] = sb[0] + sb[1] + sb[2] + sb[3];
+  }
+}
+
+// one workgroup per file: sum the partials of the k_live blocks that lie wholly inside it
+__global__ __launch_bounds__(256) void k_file_stats(const FileDesc* __restrict__ fd, uint32_t n_files, uint64_t n,
+                                                    const unsigned long long* __restrict__ part,
+                                                    unsigned long long* __restrict__ fstat) {
+  __shared__ unsigned long long sc[4], sb[4];
+  const uint32_t f = blockIdx.x;
+  const uint64_t lo = fd[f].seq_base, hi = fd[f + 1].seq_base;
+  unsigned long long c = 0, b = 0;
+  if (hi > lo) {
+    const uint64_t blo = lo / 256, bhi = (hi - 1) / 256;   // k_live blocks touching the file
+    for (uint64_t k = blo + threadIdx.x; k <= bhi; k += blockDim.x) {
+      const uint64_t s0 = k * 256, s1 = min(n, s0 + 256) - 1;
+      if (s0 >= lo && s1 < hi) {   // wholly inside: a uniform block (straddlers added per record)
+        c += part[2 * k];
+        b += part[2 * k + 1];
+      }
     }
-  } else if (valid && live) {
-    atomicAdd(&fstat[2 * f], 1ull);
-    atomicAdd(&fstat[2 * f + 1], (unsigned long long)size);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    b += __shfl_xor(b, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sc[threadIdx.x >> 6] = c;
+    sb[threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&fstat[2 * f], sc[0] + sc[1] + sc[2] + sc[3]);
+    atomicAdd(&fstat[2 * f + 1], sb[0] + sb[1] + sb[2] + sb[3]);
   }
 }
 
@@ -470,7 +513,26 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
       __builtin_memcpy(&v, s, 16);
       __builtin_memcpy(d, &v, 16);
     } else {
-      for (uint32_t b = 0; b < len; ++b) d[b] = s[b];
+      uint32_t b = 0;
+      if (len & 8) {
+        uint64_t v;
+        __builtin_memcpy(&v, s, 8);
+        __builtin_memcpy(d, &v, 8);
+        b = 8;
+      }
+      if (len & 4) {
+        uint32_t v;
+        __builtin_memcpy(&v, s + b, 4);
+        __builtin_memcpy(d + b, &v, 4);
+        b += 4;
+      }
+      if (len & 2) {
+        uint16_t v;
+        __builtin_memcpy(&v, s + b, 2);
+        __builtin_memcpy(d + b, &v, 2);
+        b += 2;
+      }
+      if (len & 1) d[b] = s[b];
     }
   }
   if (pieces && !canon) {   // re-encode the header (EncodeEntry :52-66) and its CRC (:75-76)
@@ -630,34 +692,34 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   uint64_t tcap = 1024;
   while (tcap < 2 * n) tcap <<= 1;
   const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
-  const uint64_t o_hash = 0, o_kp = align256(o_hash + 8 * n), o_slot = align256(o_kp + 8 * n);
+  const uint64_t nlb = (n + 255) / 256;
+  const uint64_t o_part = 0, o_slot = align256(o_part + 16 * (nlb + 1));
   const uint64_t o_esz = align256(o_slot + 4 * n), o_P = align256(o_esz + 4 * n);
   const uint64_t o_C = align256(o_P + 8 * (n + 1)), o_tk = align256(o_C + 4 * (n + 1));
-  const uint64_t o_tm = align256(o_tk + 8 * tcap), o_bs = align256(o_tm + 4 * tcap);
+  const uint64_t o_bs = align256(o_tk + 16 * tcap);
   const uint64_t o_bc = align256(o_bs + 8 * (ntiles + 1)), seq_need = align256(o_bc + 4 * (ntiles + 1));
   rc = grow(&m->seqbuf, &m->seqbuf_bytes, seq_need);
   if (rc != LDB_OK) return rc;
   uint8_t* q = m->seqbuf;
-  uint64_t* d_hash = reinterpret_cast<uint64_t*>(q + o_hash);
-  uint64_t* d_kp = reinterpret_cast<uint64_t*>(q + o_kp);
+  unsigned long long* d_part = reinterpret_cast<unsigned long long*>(q + o_part);
   uint32_t* d_slot = reinterpret_cast<uint32_t*>(q + o_slot);
   uint32_t* d_esz = reinterpret_cast<uint32_t*>(q + o_esz);
   uint64_t* d_P = reinterpret_cast<uint64_t*>(q + o_P);
   uint32_t* d_C = reinterpret_cast<uint32_t*>(q + o_C);
   uint64_t* d_tk = reinterpret_cast<uint64_t*>(q + o_tk);
-  uint32_t* d_tm = reinterpret_cast<uint32_t*>(q + o_tm);
   uint64_t* d_bs = reinterpret_cast<uint64_t*>(q + o_bs);
   uint32_t* d_bc = reinterpret_cast<uint32_t*>(q + o_bc);
 
   const bool live_ok = !d_live || live_cap >= n;
   MHIP(hipMemcpyAsync(d_fd, fdh.data(), sizeof(FileDesc) * (nf + 1), hipMemcpyHostToDevice, s));
   MHIP(hipMemsetAsync(d_fst, 0, 16ull * (nf + 1), s));
-  MHIP(hipMemsetAsync(d_tk, 0, o_bs - o_tk, s));   // tab_key and tab_max
+  MHIP(hipMemsetAsync(d_tk, 0, 16 * tcap, s));   // hash table slots
   const uint32_t nbk = (uint32_t)((n + 255) / 256);
   if (n) {
-    k_locate<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_hash, d_kp);
-    k_insert<<<nbk, 256, 0, s>>>(m->recs, n, d_hash, d_kp, d_tk, d_tm, tcap - 1, d_slot);
-    k_live<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_tm, d_slot, now, live_ok ? d_live : nullptr, d_esz, d_fst);
+    k_insert<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_tk, tcap - 1, d_slot);
+    k_live<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_tk, d_slot, now, live_ok ? d_live : nullptr, d_esz, d_part,
+                               d_fst);
+    k_file_stats<<<nf, 256, 0, s>>>(d_fd, nf, n, d_part, d_fst);
     MHIP(hipGetLastError());
   }
   MHIP(hipEventRecord(m->ev[2], s));

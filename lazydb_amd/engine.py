@@ -91,7 +91,8 @@ class Engine:
     # ---------------------------------------------------------------- merge / GC
     def merge_dev(self, files, active_fid: int, active_off: int, max_file_size: int, now: int,
                   io_type: int = N.FILEIO, stream_cap: int | None = None, pos_cap: int | None = None,
-                  seg_cap: int = 256, live_cap: int | None = None, want_live: bool = True, stream=None):
+                  seg_cap: int = 256, live_cap: int | None = None, want_live: bool = True, stream=None,
+                  fetch_pos: bool = True):
         """Merge the target files of one value type (db.go:383-427 Merge + mergeStr + writeLogEntry).
 
         files: list of (device uint8 tensor, fid, is_target), ascending fid. Returns a dict with
@@ -138,8 +139,11 @@ class Engine:
         if rc not in (N.LDB_OK,) and res.bad_file < 0:
             N.check(rc, "ldb_merge_files_dev")
         npos = min(res.n_emit, pos_cap)
-        pos = (np.frombuffer(d_pos[: npos * N.MERGE_POS.itemsize].cpu().numpy().tobytes(), dtype=N.MERGE_POS)
-               if npos else np.zeros(0, N.MERGE_POS))
+        if not fetch_pos:   # leave the positions on the device (bench)
+            pos = d_pos[: npos * N.MERGE_POS.itemsize]
+        else:
+            pos = (np.frombuffer(d_pos[: npos * N.MERGE_POS.itemsize].cpu().numpy().tobytes(), dtype=N.MERGE_POS)
+                   if npos else np.zeros(0, N.MERGE_POS))
         return {"rc": rc, "result": res, "stream": d_stream[: res.emit_bytes],
                 "pos": pos, "segments": segs[: min(res.n_segments, seg_cap)],
                 "live": d_live[: res.n_records] if want_live else None, "stats": stats[: len(files)]}

@@ -12,7 +12,9 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for k in ("k_scan_main", "k_link", "k_repair", "k_combine", "k_final", "k_compact", "k_serial"):
+    for k in ("k_scan_main", "k_link", "k_repair", "k_combine", "k_final", "k_compact", "k_serial", "k_fallback",
+              "k_locate", "k_insert", "k_live", "k_scan_reduce", "k_scan_tiles", "k_scan_write", "k_pack",
+              "k_emit_copy"):
         if k in name:
             return k
     return name[:60]
