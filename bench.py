@@ -33,8 +33,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
-                    help="BASELINE config: 2 = 1 GiB fixed 64/256; 3 = 8 GiB Zipf values; 4 = 4 GiB per GPU; "
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
+                    help="BASELINE config: 1 = 500K entries 64/256 in a 512 MiB preallocated file (reopen); 2 = 1 GiB fixed 64/256; 3 = 8 GiB Zipf values; 4 = 4 GiB per GPU; "
                          "5 = merge/GC of 16 x 256 MiB files, half the records stale (a separate bench line)")
     ap.add_argument("--io", type=int, default=0, help="0 FileIO bound rule, 1 Mmap")
     ap.add_argument("--kind", type=int, default=0, help="0 index tuples (16 B), 1 full entries (48 B)")
@@ -48,7 +48,13 @@ def parse():
 
 def make_image(cfg: int, rank: int):
     from oracle import coracle  # format producer (writeLogEntry restatement) for synthetic inputs
-    if cfg == 2:
+    if cfg == 1:
+        # bench/db_bench_test.go shape: 500 000 STRING entries, close, reopen;
+        # the file is preallocated to MaxLogFileSize = 512 MiB (fileio.go:66-68), so the replay ends at
+        # the zero sentinel
+        img, n, end = coracle.gen_log(512 << 20, 1 + rank, ksize=64, vsize=256, max_entries=500_000)
+        wl = "reopen replay of 500K entries, 64B key / 256B value, 512 MiB preallocated file"
+    elif cfg == 2:
         img, n, end = coracle.gen_log(1 << 30, 1 + rank, ksize=64, vsize=256)
         wl = "1GiB log file, 64B key / 256B value (332B entries), FileIO bound"
     elif cfg == 3:

@@ -346,6 +346,34 @@ LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv, int seg = 0) {
   scan_step_seg<5>(wp, tab, cpriv, seg);
 }
 
+// Zero-region shortcut (k_scan_main and the emulator call it before region_chained): a speculative
+// region (!st.on) whose bytes and halo are all zero -- the preallocated tail of a log file,
+// iocontroller/fileio.go:66-68 -- has no plausible start (every candidate decodes with kSize == 0),
+// so region_chained would end in covered(false) with raw register 0. zero_region() decides that
+// with one 16-B LDS read per 16 bytes and a ballot, without the candidate rounds and the CRC pass.
+// Only for full regions whose halo lies inside the file (past it the buffer holds other bytes).
+template <class WP>
+LDB_HD bool zero_region(WP& wp, const View& v) {
+  if (v.rlen != (uint32_t)kW || v.R0 + (uint64_t)(kW + kHalo) > v.len) return false;
+  return !wp.ballot([&](int l) {
+    const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + l * kS);
+    uint32_t o = 0;
+    for (int k2 = 0; k2 < kS / 16; ++k2) o |= row[k2].w[0] | row[k2].w[1] | row[k2].w[2] | row[k2].w[3];
+    if (l < kHalo / 16) {
+      const Row16 h = reinterpret_cast<const Row16*>(v.buf + kPre + kW)[l];
+      o |= h.w[0] | h.w[1] | h.w[2] | h.w[3];
+    }
+    return o != 0;
+  });
+}
+
+LDB_HD RegionSum zero_summary() {   // covered(false) of an all-zero region
+  RegionSum r;
+  r.start = kNone64; r.exitp = 0; r.soff = 0; r.status = kCont; r.count = 0;
+  r.rpre = 0; r.rout = 0; r.scrc = 0; r.sflag = 0;
+  return r;
+}
+
 // The lean path for one region, in one of two modes:
 //   chained (st.on): the chain enters at st.x with the CRC state st.I / st.owner; the owner of the
 //     region's first start is CRC-checked here (kOwnerOk);

@@ -339,6 +339,18 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
       continue;
     }
 #endif
+    if (!st.on && zero_region(wp, v)) {
+      // all-zero speculative region (a preallocated file tail, fileio.go:66-68): covered, raw register 0
+      // (ldb_chain.h zero_region)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      GpuWave::sync();
+      if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
+      store_summary(p, r, zero_summary(), lane);
+      ++n_fast;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      GpuWave::sync();
+      continue;
+    }
     bool released = false;
     const bool fast = region_chained(
         wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },

@@ -120,6 +120,11 @@ struct Emu {
     CpuWave wp;
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
     ChainPriv cpriv[kLanes];
+    if (!st.on && zero_region(wp, v)) {   // as k_scan_main
+      store_region(p, r, zero_summary());
+      EMU_FOLD();
+      return true;
+    }
     bool released = false;
     const bool fast = region_chained(
         wp, v, buf.data(), sh, st, [&](int l) -> ChainPriv& { return cpriv[l]; },

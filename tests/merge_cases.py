@@ -83,6 +83,29 @@ def case_oversized():
         dict(active_fid=3, active_off=10, max_file_size=200, now=NOW)
 
 
+def case_hot_keys(seed: int):
+    """Few distinct keys (incl. the nil key) rewritten many times across files, with SDeletes that are
+    sometimes followed by a re-Put, expiring records, empty values and odd sizes."""
+    import random
+    rnd = random.Random(seed)
+    keys = [b""] + [b"hot-%d" % i for i in range(9)] + [bytes([255 - i]) * (1 + i * 13) for i in range(6)]
+    files = []
+    for f in range(6):
+        recs = []
+        for _ in range(rnd.randint(20, 400)):
+            k = rnd.choice(keys)
+            if rnd.random() < 0.15:
+                recs.append(dict(stat=1, key=k))
+            else:
+                exp = rnd.choice([0, 0, 0, NOW - 5, NOW + 5, NOW])
+                recs.append(dict(stat=rnd.choice([0, 0, 0, 2]), expired_at=exp, tx_id=rnd.choice([0, 7, 1 << 40]),
+                                 tx_stat=rnd.choice([0, 1, 2]), key=k,
+                                 value=bytes(rnd.getrandbits(8) for _ in range(rnd.choice([0, 1, 15, 16, 17, 333])))))
+        files.append(_log(recs, sum(len(coracle.encode_entry(**r)) for r in recs) + rnd.choice([0, 3, 40])))
+    return [(img, 100 + f, f != 5) for f, img in enumerate(files)], \
+        dict(active_fid=105, active_off=int(files[5].size), max_file_size=4096, now=NOW)
+
+
 def case_crc_corrupt():
     return [(golden_img("mixed_64k"), 1, True), (golden_img("crc_corrupt"), 2, True),
             (np.zeros(64, np.uint8), 3, False)], dict(active_fid=3, active_off=0, max_file_size=1 << 20, now=NOW)
@@ -96,4 +119,6 @@ def small_cases():
     out["gen_no_targets"] = case_generated(7, targets=set())
     out["gen_all_but_one"] = case_generated(8, n_files=6, targets={0, 1, 3, 4}, max_file_size=5000)
     out["gen_mmap"] = (case_generated(9)[0], dict(case_generated(9)[1], io_type=1))
+    for s in (1, 2, 3):
+        out[f"hot_keys{s}"] = case_hot_keys(s)
     return out

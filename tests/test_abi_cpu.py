@@ -201,3 +201,34 @@ def test_emulated_file_end(seed):
             assert_same(res, tup, ref, rt)
             if not (pad == 0 and io == 1):
                 assert int(st[2]) == nreg, (pad, io, int(st[2]), nreg)
+
+
+@pytest.mark.parametrize("run_len", [1, 3, 64])
+def test_emulated_zero_regions(run_len):
+    """All-zero regions (the preallocated tail of a log file, fileio.go:66-68; zero-valued entries)
+    take the zero-region shortcut of the speculative lean path (ldb_chain.h): a zero tail after the
+    last entry, zero tails followed by garbage, and chains running through zero-valued entries that
+    span whole regions, with runs starting inside the zeros; intact and with flipped bytes."""
+    from oracle import pyoracle as P
+    rng = random.Random(5 + run_len)
+    base, n, end = coracle.gen_log(40_000, 3, ksize=64, vsize=256)
+    tail = np.concatenate([base[:end], np.zeros(60_000, np.uint8)])
+    garbage = tail.copy()
+    garbage[-3000:] = np.frombuffer(bytes(rng.randrange(256) for _ in range(3000)), np.uint8)
+    ents = bytearray()
+    for i in range(12):
+        vl = rng.choice([0, 100, 7000, 12000, 16000])
+        ents += P.encode_entry(P.Entry(key=b"zk%03d" % i, value=bytes(vl), k_size=5, v_size=vl))
+    zeroval = np.frombuffer(bytes(ents) + bytes(20_000), np.uint8).copy()
+    for img in (tail, garbage, zeroval):
+        nreg = (img.size + 5119) // 5120
+        for flip in (None, rng.randrange(img.size // 2)):
+            im = img.copy()
+            if flip is not None:
+                im[flip] ^= 0x04
+            for io in (0, 1):
+                res, tup, st = emu_scan(im, io, run_len)
+                ref, rt = coracle.scan(im, io)
+                assert_same(res, tup, ref, rt)
+                if flip is None and img is tail:
+                    assert int(st[2]) == nreg

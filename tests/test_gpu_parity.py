@@ -123,3 +123,23 @@ def test_config3_shape_fast_path(eng):
     # ~13 regions per wavefront run at this size; each run starts speculative (region_process)
     # and stays so across covered regions until its first entry start
     assert res.n_fast >= 0.6 * res.n_regions, (res.n_fast, res.n_regions)
+
+
+def test_zero_tail_and_zero_values(eng):
+    """Preallocated zero tails (config 1 shape, fileio.go:66-68) and zero-valued entries spanning
+    regions: the zero-region shortcut of the lean path must give the oracle's tuples exactly."""
+    from oracle import pyoracle as P
+    img, n, end = coracle.gen_log(64 << 20, 5, ksize=64, vsize=256, max_entries=60_000)
+    rng = random.Random(3)
+    ents = bytearray()
+    for i in range(3000):
+        vl = rng.choice([0, 100, 7000, 12000, 16000])
+        ents += P.encode_entry(P.Entry(key=b"zk%05d" % i, value=bytes(vl), k_size=6, v_size=vl))
+    zeroval = np.frombuffer(bytes(ents) + bytes(1 << 20), np.uint8).copy()
+    for im in (img, zeroval):
+        for io in (0, 1):
+            res, tup = eng.scan_dev(to_dev(im), io_type=io)
+            ref, rt = coracle.scan(im, io)
+            assert_same(res, tup, ref, rt)
+            if im is img:   # zeroval has entries under 84 B, which the lean path leaves to region_process
+                assert res.n_fast == res.n_regions

@@ -42,7 +42,9 @@ def build(name: str) -> str:
                                             capture_output=True).stdout)
         out = os.path.join(OUT, f"var_{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                        "-Wno-unused-function", "-o", out, os.path.join(tmp, "lazydb_amd/csrc/ldb_scan.hip")], check=True)
+                        "-Wno-unused-function", "-o", out, os.path.join(tmp, "lazydb_amd/csrc/ldb_scan.hip"),
+                        *([m] if os.path.exists(m := os.path.join(tmp, "lazydb_amd/csrc/ldb_merge.hip")) else [])],
+                       check=True)
         return out
     elif name == "stamps":
         defs = ["-DLDB_STAMPS=1"]
