@@ -17,7 +17,7 @@
 // batch equals calling Merge once per target fid, ascending.
 //
 // Device pipeline (one context stream, synchronous API):
-//   replay scans    ldb_scan_file_dev per file (ldb_scan.hip), 48-B ldb_entry records, dense
+//   replay scans    ldb_scan_file_dev per file (ldb_scan.hip), 16-B index tuples, one slot per file
 //   k_insert        per record: 64-bit key hash, open-addressing table keyed by the full key bytes,
 //                   slot max = atomicMax(seq)                            (key bytes + random slot lines)
 //   k_live          per record: live = (slot max == seq) && !SDelete; emit flag, sizes; per-block partials
@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../../include/lazydb_gpu.h"
+#include "ldb_common.h"
 
 __attribute__((visibility("hidden"))) int ldb_ctx_device_(ldb_ctx* c);
 __attribute__((visibility("hidden"))) void** ldb_ctx_merge_slot_(ldb_ctx* c);
@@ -47,6 +48,7 @@ constexpr uint64_t kScanTile = (uint64_t)kScanItems * kScanBlock;
 
 struct FileDesc {       // one input file, in device memory
   const uint8_t* img;
+  const ldb_index_tuple* recs;   // the file's replayed records (record seq is recs[seq - seq_base])
   uint64_t seq_base;    // first record index of the file; desc[n_files].seq_base = total records
   uint32_t is_target;
   uint32_t fid;
@@ -60,7 +62,7 @@ struct Tail {           // k_pack output
 
 struct MergeWs {
   int device = 0;
-  ldb_entry* recs = nullptr;     // replayed records, dense over all files
+  ldb_index_tuple* recs = nullptr;   // replayed records: one slot per file (or dense, after a capacity miss)
   uint64_t rec_cap = 0;
   uint8_t* seqbuf = nullptr;     // per-record arrays + hash table + scan sums
   uint64_t seqbuf_bytes = 0;
@@ -140,22 +142,54 @@ __device__ __forceinline__ uint32_t crc_byte(uint32_t c, uint8_t b) {   // refle
 // (hash tag << 32 | representative seq + 1), claimed by CAS; a probe that meets its tag compares its key
 // with the representative's, so distinct keys never share a slot whatever their hashes. The slot's
 // max word (atomicMax of seq + 1) ends as the key's last record (index.go: later Put/Delete wins).
-__device__ __forceinline__ const uint8_t* key_of(const ldb_entry* recs, const FileDesc* fd, uint32_t n_files,
-                                                uint64_t seq, uint32_t* kl) {
-  const ldb_entry& e = recs[seq];
+struct Rec {   // an index tuple unpacked (lazydb_gpu.h LDB_POS_*)
+  uint64_t offset;
+  uint32_t hdr_size, enc_hdr_size, stat, k_size, v_size;
+};
+
+__device__ __forceinline__ Rec rec_of(const FileDesc* fd, uint32_t f, uint64_t seq) {
+  const ldb_index_tuple t = fd[f].recs[seq - fd[f].seq_base];
+  Rec r;
+  r.offset = LDB_POS_OFFSET(t.pos);
+  r.hdr_size = LDB_POS_HDR(t.pos);
+  r.enc_hdr_size = LDB_POS_ENCHDR(t.pos);
+  r.stat = LDB_POS_STAT(t.pos);
+  r.k_size = t.k_size;
+  r.v_size = t.v_size;
+  return r;
+}
+
+// The record's header decoded exactly as logfile.decodeHeader does (ldb_common.h), from its 38-byte
+// window in the image (readable: the replay accepted the record, log_file.go:117-122).
+__device__ __forceinline__ ldb::Header header_of(const uint8_t* img, uint64_t offset) {
+  ldb::Header h;
+  const uint8_t* w = img + offset;
+  ldb::decode_header([&](int i) -> uint32_t { return w[i]; }, &h);
+  return h;
+}
+
+// ExpiredAt of a record: the first varint after crc and stat (log_entry.go:90-91); a single 0 byte
+// (every record without a TTL) is decided without the full decode.
+__device__ __forceinline__ int64_t expired_at_of(const uint8_t* img, uint64_t offset) {
+  if (img[offset + 5] == 0) return 0;
+  return header_of(img, offset).expired_at;
+}
+
+__device__ __forceinline__ const uint8_t* key_of(const FileDesc* fd, uint32_t n_files, uint64_t seq, uint32_t* kl) {
+  const uint32_t f = file_of(fd, n_files, seq);
+  const Rec e = rec_of(fd, f, seq);
   *kl = e.k_size;
-  return fd[file_of(fd, n_files, seq)].img + e.offset + e.hdr_size;
+  return fd[f].img + e.offset + e.hdr_size;
 }
 
 // A slot is 16 B: word 0 = (hash tag << 32 | representative seq + 1), word 1 low half = max seq + 1, so the
 // claim and the max update touch one cache line.
-__global__ __launch_bounds__(256) void k_insert(const ldb_entry* __restrict__ recs, uint64_t n,
-                                                const FileDesc* __restrict__ fd, uint32_t n_files, uint64_t* tab,
+__global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files, uint64_t* tab,
                                                 uint64_t mask, uint32_t* __restrict__ slot) {
   uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (seq >= n) return;
   uint32_t kl;
-  const uint8_t* kp = key_of(recs, fd, n_files, seq, &kl);
+  const uint8_t* kp = key_of(fd, n_files, seq, &kl);
   const uint64_t h = key_hash(kp, kl);
   const uint64_t mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
   uint64_t i = h & mask;
@@ -168,7 +202,7 @@ __global__ __launch_bounds__(256) void k_insert(const ldb_entry* __restrict__ re
     }
     if ((v >> 32) == (h >> 32)) {
       uint32_t rl;
-      const uint8_t* rp = key_of(recs, fd, n_files, (v & 0xFFFFFFFFull) - 1, &rl);
+      const uint8_t* rp = key_of(fd, n_files, (v & 0xFFFFFFFFull) - 1, &rl);
       if (rl == kl && key_equal(kp, rp, kl)) break;
     }
     i = (i + 1) & mask;
@@ -180,8 +214,7 @@ __global__ __launch_bounds__(256) void k_insert(const ldb_entry* __restrict__ re
 // live = last record of its key and not an SDelete (index.go:16-25); emit = live && target file &&
 // not expired (db.go:403-409, 255). Per-file live counts/bytes: a block whose records all lie in one
 // file writes one partial (k_file_stats sums them); a block that straddles files adds per record.
-__global__ __launch_bounds__(256) void k_live(const ldb_entry* __restrict__ recs, uint64_t n,
-                                              const FileDesc* __restrict__ fd, uint32_t n_files,
+__global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
                                               const uint64_t* __restrict__ tab, const uint32_t* __restrict__ slot,
                                               int64_t now, uint8_t* __restrict__ live_out,
                                               uint32_t* __restrict__ esz, unsigned long long* __restrict__ part,
@@ -193,13 +226,17 @@ __global__ __launch_bounds__(256) void k_live(const ldb_entry* __restrict__ recs
   uint32_t f = 0, size = 0;
   bool live = false;
   if (valid) {
-    const ldb_entry e = recs[seq];
     f = file_of(fd, n_files, seq);
+    const Rec e = rec_of(fd, f, seq);
     const uint32_t mx = (uint32_t)tab[2 * (uint64_t)slot[seq] + 1];
     live = mx == (uint32_t)(seq + 1) && e.stat != kSDelete;
-    size = (uint32_t)e.enc_hdr_size + e.k_size + e.v_size;
-    const bool expired = e.expired_at != 0 && e.expired_at <= now;
-    esz[seq] = (live && fd[f].is_target && !expired) ? size : 0u;
+    size = e.enc_hdr_size + e.k_size + e.v_size;
+    bool emit = live && fd[f].is_target;
+    if (emit) {
+      const int64_t ea = expired_at_of(fd[f].img, e.offset);
+      emit = !(ea != 0 && ea <= now);
+    }
+    esz[seq] = emit ? size : 0u;
     if (live_out) live_out[seq] = live ? 1 : 0;
   }
   const uint64_t last = min(n, b0 + blockDim.x) - 1;
@@ -447,7 +484,7 @@ constexpr int kCopyWaves = 4;
 // verbatim: EncodeEntry re-produces their bytes. A non-canonical record gets its key/value copied and
 // its header re-encoded by its lane, CRC-32 over the new header and the key/value (log_entry.go:48-78).
 __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
-    const ldb_entry* __restrict__ recs, uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
+    uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
     const uint64_t* __restrict__ P, const uint32_t* __restrict__ C, const ldb_merge_segment* __restrict__ segs,
     uint32_t n_segs, uint8_t* __restrict__ stream, ldb_merge_pos* __restrict__ pos) {
   __shared__ const uint8_t* s_src[kCopyWaves][64];
@@ -460,7 +497,7 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
   const uint8_t* src = nullptr;
   uint8_t* dst = nullptr;
   uint32_t nb = 0;
-  ldb_entry e;
+  Rec e;
   bool canon = true;
   uint64_t sp = 0;
   const uint8_t* fimg = nullptr;
@@ -468,8 +505,8 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
     sp = P[seq];
     const uint64_t sz = P[seq + 1] - sp;
     if (sz) {
-      e = recs[seq];
       const uint32_t f = file_of(fd, n_files, seq);
+      e = rec_of(fd, f, seq);
       fimg = fd[f].img;
       const ldb_merge_segment& sg = segs[seg_of(segs, n_segs, sp)];
       ldb_merge_pos q;
@@ -536,12 +573,13 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
     }
   }
   if (pieces && !canon) {   // re-encode the header (EncodeEntry :52-66) and its CRC (:75-76)
+    const ldb::Header dh = header_of(fimg, e.offset);
     uint8_t h[40];
     int o = 5;
-    h[4] = e.stat;
-    o += put_varint(h + o, e.expired_at);
-    o += put_varint(h + o, (int64_t)e.tx_id);
-    o += put_varint(h + o, (int64_t)e.tx_stat);
+    h[4] = (uint8_t)e.stat;
+    o += put_varint(h + o, dh.expired_at);
+    o += put_varint(h + o, (int64_t)dh.tx_id);
+    o += put_varint(h + o, (int64_t)(uint16_t)dh.tx_stat);
     o += put_varint(h + o, (int64_t)e.k_size);
     o += put_varint(h + o, (int64_t)e.v_size);
     uint32_t c = 0xFFFFFFFFu;
@@ -573,9 +611,9 @@ int grow(uint8_t** p, uint64_t* have, uint64_t need) {
 int grow_recs(MergeWs* m, uint64_t need, uint64_t keep, hipStream_t s) {
   if (m->rec_cap >= need) return LDB_OK;
   uint64_t cap = std::max(need, m->rec_cap + m->rec_cap / 2);
-  ldb_entry* nr = nullptr;
-  if (hipMalloc(&nr, cap * sizeof(ldb_entry)) != hipSuccess) return LDB_ERR_NOMEM;
-  if (keep) MHIP(hipMemcpyAsync(nr, m->recs, keep * sizeof(ldb_entry), hipMemcpyDeviceToDevice, s));
+  ldb_index_tuple* nr = nullptr;
+  if (hipMalloc(&nr, cap * sizeof(ldb_index_tuple)) != hipSuccess) return LDB_ERR_NOMEM;
+  if (keep) MHIP(hipMemcpyAsync(nr, m->recs, keep * sizeof(ldb_index_tuple), hipMemcpyDeviceToDevice, s));
   MHIP(hipStreamSynchronize(s));
   if (m->recs) (void)hipFree(m->recs);
   m->recs = nr;
@@ -650,27 +688,44 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   Tail* d_tail = reinterpret_cast<Tail*>(m->small + o_tail);
   ldb_merge_segment* d_segs = reinterpret_cast<ldb_merge_segment*>(m->small + o_seg);
 
-  // ---- 1. replay scans (index.go:84-95 per file), dense 48-B records
+  // ---- 1. replay scans (index.go:84-95 per file), 16-B index tuples. All files are enqueued back to back,
+  // each into its own slot of len/64 + 1024 records, and read back with one synchronisation; only
+  // if a file has more records than its slot are the files rescanned one by one into dense storage.
   MHIP(hipEventRecord(m->ev[0], s));
-  uint64_t total_len = 0;
-  for (int i = 0; i < n_files; ++i) total_len += files[i].len;
-  rc = grow_recs(m, std::max<uint64_t>(total_len / 64 + 64ull * nf, 4096), 0, s);
-  if (rc != LDB_OK) return rc;
   std::vector<FileDesc> fdh(nf + 1);
   std::vector<ldb_scan_result> rh(nf);
+  std::vector<uint64_t> sbase(nf + 1, 0);
+  for (uint32_t i = 0; i < nf; ++i) sbase[i + 1] = sbase[i] + files[i].len / 64 + 1024;
+  rc = grow_recs(m, std::max<uint64_t>(sbase[nf], 4096), 0, s);
+  if (rc != LDB_OK) return rc;
+  for (uint32_t i = 0; i < nf; ++i) {
+    rc = ldb_scan_file_dev(ctx, files[i].d_image, files[i].len, files[i].fid, io_type, LDB_TUPLE_INDEX,
+                           m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i, s);
+    if (rc != LDB_OK) return rc;
+  }
+  if (nf) MHIP(hipMemcpyAsync(rh.data(), d_res, sizeof(ldb_scan_result) * nf, hipMemcpyDeviceToHost, s));
+  MHIP(hipStreamSynchronize(s));
+  bool slotted = true;
+  for (uint32_t i = 0; i < nf && slotted; ++i) {
+    if (rh[i].status == LDB_ERR_CAPACITY) slotted = false;
+    if (rh[i].status < 0) break;   // a fatal scan status: later files do not matter
+  }
   uint64_t base = 0;
   for (uint32_t i = 0; i < nf; ++i) {
-    for (;;) {
-      rc = ldb_scan_file_dev(ctx, files[i].d_image, files[i].len, files[i].fid, io_type, LDB_TUPLE_ENTRY,
-                             m->recs + base, m->rec_cap - base, d_res + i, s);
-      if (rc != LDB_OK) return rc;
-      MHIP(hipMemcpyAsync(&rh[i], d_res + i, sizeof(ldb_scan_result), hipMemcpyDeviceToHost, s));
-      MHIP(hipStreamSynchronize(s));
-      if (rh[i].status != LDB_ERR_CAPACITY) break;
-      rc = grow_recs(m, base + rh[i].n_entries + 1024, base, s);
-      if (rc != LDB_OK) return rc;
+    if (!slotted) {   // dense rescan, growing the record array as needed
+      for (;;) {
+        rc = ldb_scan_file_dev(ctx, files[i].d_image, files[i].len, files[i].fid, io_type, LDB_TUPLE_INDEX,
+                               m->recs + base, m->rec_cap - base, d_res + i, s);
+        if (rc != LDB_OK) return rc;
+        MHIP(hipMemcpyAsync(&rh[i], d_res + i, sizeof(ldb_scan_result), hipMemcpyDeviceToHost, s));
+        MHIP(hipStreamSynchronize(s));
+        if (rh[i].status != LDB_ERR_CAPACITY) break;
+        rc = grow_recs(m, base + rh[i].n_entries + 1024, base, s);
+        if (rc != LDB_OK) return rc;
+      }
     }
-    fdh[i] = FileDesc{files[i].d_image, base, files[i].is_target, files[i].fid};
+    fdh[i] = FileDesc{files[i].d_image, slotted ? m->recs + sbase[i] : m->recs + base, base, files[i].is_target,
+                      files[i].fid};
     if (h_stats) {
       h_stats[i] = ldb_merge_file_stat{rh[i].status, files[i].fid, rh[i].n_entries, rh[i].end_off, 0, 0};
     }
@@ -683,7 +738,7 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
     base += rh[i].n_entries;
   }
   const uint64_t n = base;
-  fdh[nf] = FileDesc{nullptr, n, 0, 0};
+  fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0};
   h_result->n_records = n;
   if (n >= 0xFFFFFFFFull) return h_result->status = LDB_ERR_ARG;   // record ids are 32-bit
   MHIP(hipEventRecord(m->ev[1], s));
@@ -716,8 +771,8 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   MHIP(hipMemsetAsync(d_tk, 0, 16 * tcap, s));   // hash table slots
   const uint32_t nbk = (uint32_t)((n + 255) / 256);
   if (n) {
-    k_insert<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_tk, tcap - 1, d_slot);
-    k_live<<<nbk, 256, 0, s>>>(m->recs, n, d_fd, nf, d_tk, d_slot, now, live_ok ? d_live : nullptr, d_esz, d_part,
+    k_insert<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot);
+    k_live<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, d_slot, now, live_ok ? d_live : nullptr, d_esz, d_part,
                                d_fst);
     k_file_stats<<<nf, 256, 0, s>>>(d_fd, nf, n, d_part, d_fst);
     MHIP(hipGetLastError());
@@ -763,7 +818,7 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   }
   if (tot_c) {
     const uint32_t ngrp = (uint32_t)((n + 64 * kCopyWaves - 1) / (64 * kCopyWaves));
-    k_emit_copy<<<ngrp, 64 * kCopyWaves, 0, s>>>(m->recs, n, d_fd, nf, d_P, d_C, d_segs, tail.n_segments,
+    k_emit_copy<<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, tail.n_segments,
                                                  d_stream, d_pos);
     MHIP(hipGetLastError());
   }

@@ -106,6 +106,17 @@ def case_hot_keys(seed: int):
         dict(active_fid=105, active_off=int(files[5].size), max_file_size=4096, now=NOW)
 
 
+def case_tiny_entries():
+    """15-B entries (5-B keys that repeat every 10 records, empty values): more records per file than
+    the engine's first-pass slot of len/64 + 1024, so the scans are redone densely."""
+    files = []
+    for i in range(3):
+        img, n, end = coracle.gen_log(200_000 + 999 * i, 20 + i, ksize=5, vsize=0)
+        files.append((img, 1 + i, i < 2))
+    return files, dict(active_fid=3, active_off=int(coracle.scan(files[2][0])[0].end_off), max_file_size=1 << 16,
+                       now=NOW)
+
+
 def case_crc_corrupt():
     return [(golden_img("mixed_64k"), 1, True), (golden_img("crc_corrupt"), 2, True),
             (np.zeros(64, np.uint8), 3, False)], dict(active_fid=3, active_off=0, max_file_size=1 << 20, now=NOW)
@@ -121,4 +132,5 @@ def small_cases():
     out["gen_mmap"] = (case_generated(9)[0], dict(case_generated(9)[1], io_type=1))
     for s in (1, 2, 3):
         out[f"hot_keys{s}"] = case_hot_keys(s)
+    out["tiny_entries"] = case_tiny_entries()
     return out
