@@ -18,8 +18,8 @@
 //
 // Device pipeline (one context stream, synchronous API):
 //   replay scans    ldb_scan_file_dev per file (ldb_scan.hip), 16-B index tuples, one slot per file
-//   k_insert        per record: 64-bit key hash, open-addressing table keyed by the full key bytes,
-//                   slot max = atomicMax(seq)                            (key bytes + random slot lines)
+//   k_insert        per record: 64-bit key hash, open-addressing table of 8-B slots keyed by the full
+//                   key bytes, (tag | max record) by CAS + atomicMax     (key bytes + random slot lines)
 //   k_live          per record: live = (slot max == seq) && !SDelete; emit flag, sizes; per-block partials
 //   k_file_stats    per file: live counts and bytes
 //   k_scan_*        exclusive prefix sums of emitted bytes and counts (3-kernel reduce-then-scan)
@@ -182,32 +182,36 @@ __device__ __forceinline__ const uint8_t* key_of(const FileDesc* fd, uint32_t n_
   return fd[f].img + e.offset + e.hdr_size;
 }
 
-// A slot is 16 B: word 0 = (hash tag << 32 | representative seq + 1), word 1 low half = max seq + 1, so the
-// claim and the max update touch one cache line.
-__global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files, uint64_t* tab,
-                                                uint64_t mask, uint32_t* __restrict__ slot) {
+// A slot is one 64-bit word (hash tag << 32 | max record id + 1), claimed by CAS and then raised by a
+// 64-bit atomicMax: every record that reaches a slot has the slot's key (it claimed it, or compared its
+// key bytes equal with the slot's current record), so the tag half never changes and the low half ends
+// as the key's last record. 8-B slots keep the table within the Infinity Cache at config-5 sizes.
+__global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
+                                                unsigned long long* tab, uint64_t mask, uint32_t* __restrict__ slot) {
   uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (seq >= n) return;
   uint32_t kl;
   const uint8_t* kp = key_of(fd, n_files, seq, &kl);
   const uint64_t h = key_hash(kp, kl);
-  const uint64_t mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
+  const unsigned long long mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
   uint64_t i = h & mask;
   for (;;) {
-    uint64_t v = __hip_atomic_load(&tab[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long v = __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v == 0) {
-      uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[2 * i]), 0ull, (unsigned long long)mine);
+      const unsigned long long prev = atomicCAS(&tab[i], 0ull, mine);
       if (prev == 0) break;
       v = prev;
     }
     if ((v >> 32) == (h >> 32)) {
       uint32_t rl;
       const uint8_t* rp = key_of(fd, n_files, (v & 0xFFFFFFFFull) - 1, &rl);
-      if (rl == kl && key_equal(kp, rp, kl)) break;
+      if (rl == kl && key_equal(kp, rp, kl)) {
+        atomicMax(&tab[i], mine);
+        break;
+      }
     }
     i = (i + 1) & mask;
   }
-  atomicMax(reinterpret_cast<uint32_t*>(&tab[2 * i + 1]), (uint32_t)(seq + 1));
   slot[seq] = (uint32_t)i;
 }
 
@@ -215,7 +219,8 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
 // not expired (db.go:403-409, 255). Per-file live counts/bytes: a block whose records all lie in one
 // file writes one partial (k_file_stats sums them); a block that straddles files adds per record.
 __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
-                                              const uint64_t* __restrict__ tab, const uint32_t* __restrict__ slot,
+                                              const unsigned long long* __restrict__ tab,
+                                              const uint32_t* __restrict__ slot,
                                               int64_t now, uint8_t* __restrict__ live_out,
                                               uint32_t* __restrict__ esz, unsigned long long* __restrict__ part,
                                               unsigned long long* __restrict__ fstat) {
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __rest
   if (valid) {
     f = file_of(fd, n_files, seq);
     const Rec e = rec_of(fd, f, seq);
-    const uint32_t mx = (uint32_t)tab[2 * (uint64_t)slot[seq] + 1];
+    const uint32_t mx = (uint32_t)tab[slot[seq]];
     live = mx == (uint32_t)(seq + 1) && e.stat != kSDelete;
     size = e.enc_hdr_size + e.k_size + e.v_size;
     bool emit = live && fd[f].is_target;
@@ -744,14 +749,14 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   MHIP(hipEventRecord(m->ev[1], s));
 
   // ---- 2. liveness
-  uint64_t tcap = 1024;
-  while (tcap < 2 * n) tcap <<= 1;
+  uint64_t tcap = 1024;   // >= 1.25 slots per record (load <= 0.8 when every key is distinct)
+  while (tcap < n + n / 4) tcap <<= 1;
   const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
   const uint64_t nlb = (n + 255) / 256;
   const uint64_t o_part = 0, o_slot = align256(o_part + 16 * (nlb + 1));
   const uint64_t o_esz = align256(o_slot + 4 * n), o_P = align256(o_esz + 4 * n);
   const uint64_t o_C = align256(o_P + 8 * (n + 1)), o_tk = align256(o_C + 4 * (n + 1));
-  const uint64_t o_bs = align256(o_tk + 16 * tcap);
+  const uint64_t o_bs = align256(o_tk + 8 * tcap);
   const uint64_t o_bc = align256(o_bs + 8 * (ntiles + 1)), seq_need = align256(o_bc + 4 * (ntiles + 1));
   rc = grow(&m->seqbuf, &m->seqbuf_bytes, seq_need);
   if (rc != LDB_OK) return rc;
@@ -761,14 +766,14 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   uint32_t* d_esz = reinterpret_cast<uint32_t*>(q + o_esz);
   uint64_t* d_P = reinterpret_cast<uint64_t*>(q + o_P);
   uint32_t* d_C = reinterpret_cast<uint32_t*>(q + o_C);
-  uint64_t* d_tk = reinterpret_cast<uint64_t*>(q + o_tk);
+  unsigned long long* d_tk = reinterpret_cast<unsigned long long*>(q + o_tk);
   uint64_t* d_bs = reinterpret_cast<uint64_t*>(q + o_bs);
   uint32_t* d_bc = reinterpret_cast<uint32_t*>(q + o_bc);
 
   const bool live_ok = !d_live || live_cap >= n;
   MHIP(hipMemcpyAsync(d_fd, fdh.data(), sizeof(FileDesc) * (nf + 1), hipMemcpyHostToDevice, s));
   MHIP(hipMemsetAsync(d_fst, 0, 16ull * (nf + 1), s));
-  MHIP(hipMemsetAsync(d_tk, 0, 16 * tcap, s));   // hash table slots
+  MHIP(hipMemsetAsync(d_tk, 0, 8 * tcap, s));   // hash table slots
   const uint32_t nbk = (uint32_t)((n + 255) / 256);
   if (n) {
     k_insert<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot);
