@@ -230,6 +230,32 @@ int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, 
                         uint32_t seg_cap, uint8_t* d_live, uint64_t live_cap, ldb_merge_file_stat* h_stats,
                         ldb_merge_result* h_result, void* stream);
 
+/* ---- batch writeLogEntry: EncodeEntry + CRC-32 + rollover for bulk writes ------------------------
+ * Replaces the per-entry loop of a transaction commit (tx.go:156-206: for each pending entry,
+ * db.writeLogEntry, db.go:473-523) for entries whose bytes are already on the device: every entry is
+ * encoded as logfile.EncodeEntry does (log_entry.go:48-78, CRC-32/IEEE over header[4:] ++ key ++ value)
+ * and placed with writeLogEntry's rollover rule starting at the active file's append offset. */
+typedef struct ldb_encode_item {
+  uint64_t key_off;    /* key bytes at d_blob + key_off */
+  uint64_t value_off;  /* value bytes at d_blob + value_off */
+  uint32_t k_size;
+  uint32_t v_size;
+  int64_t expired_at;
+  uint64_t tx_id;
+  uint16_t tx_stat;
+  uint8_t stat;
+  uint8_t pad_[5];
+} ldb_encode_item;
+
+/* Encode n items (device array d_items, bytes in d_blob) into d_stream in item order. Outputs as
+ * ldb_merge_files_dev: d_pos[i] = the ValuePos of item i (src_offset = i, src_file = 0), h_segs = the
+ * runs per log file, h_result: n_emit = n, emit_bytes, end_fid / end_off / n_segments.
+ * Synchronous; LDB_ERR_CAPACITY (sizes in h_result) when an output is too small. */
+int ldb_encode_entries_dev(ldb_ctx* ctx, uint64_t n, const ldb_encode_item* d_items, const uint8_t* d_blob,
+                           uint32_t active_fid, uint64_t active_off, uint64_t max_file_size, uint8_t* d_stream,
+                           uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap, ldb_merge_segment* h_segs,
+                           uint32_t seg_cap, ldb_merge_result* h_result, void* stream);
+
 /* Timing hook for bench.py: device time (ms) of the last ldb_merge_files_dev call, split into the
  * replay scans, the liveness resolution (hash + last-writer-wins) and the compaction (prefix sums,
  * rollover packing, stream copy), measured with HIP events on the merge stream. */

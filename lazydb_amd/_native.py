@@ -53,7 +53,10 @@ MERGE_SEGMENT = np.dtype([("fid", "<u4"), ("reserved_", "<u4"), ("file_off", "<u
                           ("n_bytes", "<u8")])
 MERGE_FILE_STAT = np.dtype([("status", "<i4"), ("fid", "<u4"), ("n_entries", "<u8"), ("end_off", "<u8"),
                             ("live_count", "<u8"), ("live_bytes", "<u8")])
-assert C.sizeof(MergeFile) == 24 and C.sizeof(MergeResult) == 56
+ENCODE_ITEM = np.dtype([("key_off", "<u8"), ("value_off", "<u8"), ("k_size", "<u4"), ("v_size", "<u4"),
+                        ("expired_at", "<i8"), ("tx_id", "<u8"), ("tx_stat", "<u2"), ("stat", "u1"),
+                        ("pad_", "u1", (5,))])
+assert C.sizeof(MergeFile) == 24 and C.sizeof(MergeResult) == 56 and ENCODE_ITEM.itemsize == 48
 assert MERGE_POS.itemsize == 32 and MERGE_SEGMENT.itemsize == 32 and MERGE_FILE_STAT.itemsize == 40
 
 RESULT_BYTES = C.sizeof(ScanResult)
@@ -98,6 +101,10 @@ def lib():
             L.ldb_merge_files_dev.restype = i32
             L.ldb_merge_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
             L.ldb_merge_timing.restype = i32
+        if hasattr(L, "ldb_encode_entries_dev"):
+            L.ldb_encode_entries_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u64, vp, u64, vp, u32,
+                                                 C.POINTER(MergeResult), vp]
+            L.ldb_encode_entries_dev.restype = i32
         if L.ldb_abi_version() != 1:
             raise LdbError("liblazydb_gpu ABI version mismatch")
         _lib = L
@@ -107,7 +114,7 @@ def lib():
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
            "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_read_ceiling", "ldb_merge_files_dev",
-           "ldb_merge_timing")
+           "ldb_merge_timing", "ldb_encode_entries_dev")
 
 
 def status_str(s: int) -> str:

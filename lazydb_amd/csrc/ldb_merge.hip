@@ -26,6 +26,8 @@
 //   k_pack          one lane: greedy rollover packing by binary search over the byte prefix
 //   k_emit_copy     one wave per 64 records: new ValuePos, unaligned 16-B copies of the emitted bytes,
 //                   re-encoded header + CRC-32 for the (rare) non-canonical records
+// and the batch writeLogEntry of a transaction commit (ldb_encode_entries_dev: k_enc_size, the same
+// prefix sums and k_pack, k_enc_copy, k_enc_hdr).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -601,6 +603,138 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
   }
 }
 
+// ------------------------------------------------------------------------------ batch writeLogEntry
+// (tx.go:156-206 commit loop: writeLogEntry per pending entry). Sizes, prefix sums and k_pack are
+// shared with the merge; k_enc_copy places the key/value bytes, k_enc_hdr encodes each header and
+// its CRC-32 (log_entry.go:48-78).
+__device__ __forceinline__ uint32_t enc_hdr_len(const ldb_encode_item& it) {
+  return 5u + (uint32_t)ldb::varint_len(it.expired_at) + (uint32_t)ldb::varint_len((int64_t)it.tx_id) +
+         (uint32_t)ldb::varint_len((int64_t)it.tx_stat) + (uint32_t)ldb::varint_len((int64_t)it.k_size) +
+         (uint32_t)ldb::varint_len((int64_t)it.v_size);
+}
+
+__global__ __launch_bounds__(256) void k_enc_size(const ldb_encode_item* __restrict__ items, uint64_t n,
+                                                  uint32_t* __restrict__ esz, uint32_t* __restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ldb_encode_item it = items[i];
+  const uint64_t sz = (uint64_t)enc_hdr_len(it) + it.k_size + it.v_size;
+  if (sz > 0xFFFFFFFFull) atomicOr(bad, 1u);   // one entry beyond 4 GiB: not representable here
+  esz[i] = (uint32_t)sz;
+}
+
+// one wave per 64 items: ValuePos and the key and value bytes (two pieces lists per item)
+__global__ __launch_bounds__(64 * kCopyWaves) void k_enc_copy(
+    const ldb_encode_item* __restrict__ items, uint64_t n, const uint8_t* __restrict__ blob,
+    const uint64_t* __restrict__ P, const ldb_merge_segment* __restrict__ segs, uint32_t n_segs,
+    uint8_t* __restrict__ stream, ldb_merge_pos* __restrict__ pos) {
+  __shared__ const uint8_t* s_src[kCopyWaves][128];
+  __shared__ uint8_t* s_dst[kCopyWaves][128];
+  __shared__ uint32_t s_nb[kCopyWaves][128];
+  __shared__ uint32_t s_ex[kCopyWaves][128];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t i = ((uint64_t)blockIdx.x * kCopyWaves + w) * 64 + lane;
+  uint32_t pk = 0, pv = 0;
+  const uint8_t *ks = nullptr, *vs = nullptr;
+  uint8_t *kd = nullptr, *vd = nullptr;
+  uint32_t kn = 0, vn = 0;
+  if (i < n) {
+    const ldb_encode_item it = items[i];
+    const uint64_t sp = P[i];
+    const ldb_merge_segment& sg = segs[seg_of(segs, n_segs, sp)];
+    ldb_merge_pos q;
+    q.offset = sg.file_off + (sp - sg.stream_off);
+    q.fid = sg.fid;
+    q.entry_size = (uint32_t)(P[i + 1] - sp);
+    q.src_offset = i;
+    q.src_file = 0;
+    q.reserved_ = 0;
+    pos[i] = q;
+    const uint32_t h = enc_hdr_len(it);
+    ks = blob + it.key_off;
+    vs = blob + it.value_off;
+    kd = stream + sp + h;
+    vd = kd + it.k_size;
+    kn = it.k_size;
+    vn = it.v_size;
+    pk = (kn + 15) >> 4;
+    pv = (vn + 15) >> 4;
+  }
+  // pieces list: entry 2l = key of lane l, 2l+1 = value of lane l
+  const uint32_t mine = pk + pv;
+  uint32_t inc = mine;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t x = __shfl_up(inc, o);
+    if (lane >= o) inc += x;
+  }
+  const uint32_t total = __shfl(inc, 63);
+  const uint32_t ex = inc - mine;
+  s_src[w][2 * lane] = ks;
+  s_dst[w][2 * lane] = kd;
+  s_nb[w][2 * lane] = kn;
+  s_ex[w][2 * lane] = ex;
+  s_src[w][2 * lane + 1] = vs;
+  s_dst[w][2 * lane + 1] = vd;
+  s_nb[w][2 * lane + 1] = vn;
+  s_ex[w][2 * lane + 1] = ex + pk;
+  __syncthreads();
+  for (uint32_t t = lane; t < total; t += 64) {
+    int lo = 0, hi = 127;   // last list entry with ex <= t (empty entries share the next one's ex)
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (s_ex[w][mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t j = t - s_ex[w][lo];
+    const uint32_t len = min(16u, s_nb[w][lo] - 16 * j);
+    const uint8_t* sp = s_src[w][lo] + 16 * j;
+    uint8_t* d = s_dst[w][lo] + 16 * j;
+    if (len == 16) {
+      uint4 v;
+      __builtin_memcpy(&v, sp, 16);
+      __builtin_memcpy(d, &v, 16);
+    } else {
+      for (uint32_t b = 0; b < len; ++b) d[b] = sp[b];
+    }
+  }
+}
+
+// one thread per item: header bytes and CRC-32/IEEE over header[4:] ++ key ++ value, byte-table CRC
+__global__ __launch_bounds__(256) void k_enc_hdr(const ldb_encode_item* __restrict__ items, uint64_t n,
+                                                 const uint8_t* __restrict__ blob, const uint64_t* __restrict__ P,
+                                                 uint8_t* __restrict__ stream) {
+  __shared__ uint32_t t8[256];
+  for (int b = threadIdx.x; b < 256; b += blockDim.x) {
+    uint32_t c = (uint32_t)b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    t8[b] = c;
+  }
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ldb_encode_item it = items[i];
+  uint8_t h[40];
+  int o = 5;
+  h[4] = it.stat;                                 // log_entry.go:54
+  o += put_varint(h + o, it.expired_at);          // :57
+  o += put_varint(h + o, (int64_t)it.tx_id);      // :59
+  o += put_varint(h + o, (int64_t)it.tx_stat);    // :61
+  o += put_varint(h + o, (int64_t)it.k_size);     // :63
+  o += put_varint(h + o, (int64_t)it.v_size);     // :65
+  uint32_t c = 0xFFFFFFFFu;
+  for (int k = 4; k < o; ++k) c = t8[(c ^ h[k]) & 0xFF] ^ (c >> 8);
+  const uint8_t* kp = blob + it.key_off;
+  for (uint32_t k = 0; k < it.k_size; ++k) c = t8[(c ^ kp[k]) & 0xFF] ^ (c >> 8);
+  const uint8_t* vp = blob + it.value_off;
+  for (uint32_t k = 0; k < it.v_size; ++k) c = t8[(c ^ vp[k]) & 0xFF] ^ (c >> 8);
+  c = ~c;                                         // :75 ChecksumIEEE(buf[4:])
+  h[0] = (uint8_t)c;                              // :76 LittleEndian.PutUint32
+  h[1] = (uint8_t)(c >> 8);
+  h[2] = (uint8_t)(c >> 16);
+  h[3] = (uint8_t)(c >> 24);
+  uint8_t* d = stream + P[i];
+  for (int k = 0; k < o; ++k) d[k] = h[k];
+}
+
 // ------------------------------------------------------------------------------ host side
 int grow(uint8_t** p, uint64_t* have, uint64_t need) {
   if (*have >= need) return LDB_OK;
@@ -834,6 +968,78 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   MHIP(hipEventElapsedTime(&m->t_scan, m->ev[0], m->ev[1]));
   MHIP(hipEventElapsedTime(&m->t_live, m->ev[1], m->ev[2]));
   MHIP(hipEventElapsedTime(&m->t_compact, m->ev[2], m->ev[3]));
+  h_result->status = LDB_OK;
+  return LDB_OK;
+}
+
+extern "C" int ldb_encode_entries_dev(ldb_ctx* ctx, uint64_t n, const ldb_encode_item* d_items,
+                                      const uint8_t* d_blob, uint32_t active_fid, uint64_t active_off,
+                                      uint64_t max_file_size, uint8_t* d_stream, uint64_t stream_cap,
+                                      ldb_merge_pos* d_pos, uint64_t pos_cap, ldb_merge_segment* h_segs,
+                                      uint32_t seg_cap, ldb_merge_result* h_result, void* stream) {
+  if (!ctx || !h_result || (n && (!d_items || !d_blob)) || max_file_size == 0 || n >= 0xFFFFFFFFull)
+    return LDB_ERR_ARG;
+  std::memset(h_result, 0, sizeof(*h_result));
+  h_result->bad_file = -1;
+  h_result->end_fid = active_fid;
+  h_result->end_off = active_off;
+  h_result->n_records = n;
+  if (hipSetDevice(ldb_ctx_device_(ctx)) != hipSuccess) return LDB_ERR_HIP;
+  MergeWs* m = get_ws(ctx);
+  if (!m) return LDB_ERR_NOMEM;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t o_tail = 0, o_bad = align256(sizeof(Tail)), o_seg = align256(o_bad + 4);
+  int rc = grow(&m->small, &m->small_bytes, o_seg + sizeof(ldb_merge_segment) * ((uint64_t)seg_cap + 1));
+  if (rc != LDB_OK) return rc;
+  Tail* d_tail = reinterpret_cast<Tail*>(m->small + o_tail);
+  uint32_t* d_bad = reinterpret_cast<uint32_t*>(m->small + o_bad);
+  ldb_merge_segment* d_segs = reinterpret_cast<ldb_merge_segment*>(m->small + o_seg);
+  const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+  const uint64_t o_esz = 0, o_P = align256(4 * n), o_C = align256(o_P + 8 * (n + 1));
+  const uint64_t o_bs = align256(o_C + 4 * (n + 1)), o_bc = align256(o_bs + 8 * (ntiles + 1));
+  rc = grow(&m->seqbuf, &m->seqbuf_bytes, align256(o_bc + 4 * (ntiles + 1)));
+  if (rc != LDB_OK) return rc;
+  uint32_t* d_esz = reinterpret_cast<uint32_t*>(m->seqbuf + o_esz);
+  uint64_t* d_P = reinterpret_cast<uint64_t*>(m->seqbuf + o_P);
+  uint32_t* d_C = reinterpret_cast<uint32_t*>(m->seqbuf + o_C);
+  uint64_t* d_bs = reinterpret_cast<uint64_t*>(m->seqbuf + o_bs);
+  uint32_t* d_bc = reinterpret_cast<uint32_t*>(m->seqbuf + o_bc);
+  MHIP(hipMemsetAsync(d_bad, 0, 4, s));
+  if (n) {
+    k_enc_size<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(d_items, n, d_esz, d_bad);
+    k_scan_reduce<<<(uint32_t)ntiles, kScanBlock, 0, s>>>(d_esz, n, d_bs, d_bc);
+    k_scan_tiles<<<1, kScanBlock, 0, s>>>(d_bs, d_bc, ntiles, d_P, d_C, n);
+    k_scan_write<<<(uint32_t)ntiles, kScanBlock, 0, s>>>(d_esz, n, d_bs, d_bc, d_P, d_C);
+  } else {
+    MHIP(hipMemsetAsync(d_P, 0, 8, s));
+  }
+  k_pack<<<1, 64, 0, s>>>(d_P, n, active_fid, active_off, max_file_size, d_segs, seg_cap + 1, d_tail);
+  MHIP(hipGetLastError());
+  uint64_t tot = 0;
+  uint32_t bad = 0;
+  Tail tail;
+  MHIP(hipMemcpyAsync(&tot, d_P + n, 8, hipMemcpyDeviceToHost, s));
+  MHIP(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
+  MHIP(hipMemcpyAsync(&tail, d_tail, sizeof(Tail), hipMemcpyDeviceToHost, s));
+  MHIP(hipStreamSynchronize(s));
+  if (bad) return h_result->status = LDB_ERR_ARG;
+  h_result->n_emit = n;
+  h_result->emit_bytes = tot;
+  h_result->end_fid = tail.end_fid;
+  h_result->end_off = tail.end_off;
+  h_result->n_segments = tail.n_segments;
+  if (tot > stream_cap || n > pos_cap || tail.n_segments > seg_cap || (n && (!d_stream || !d_pos)) ||
+      (tail.n_segments && !h_segs))
+    return h_result->status = LDB_ERR_CAPACITY;
+  if (n) {
+    const uint32_t ngrp = (uint32_t)((n + 64 * kCopyWaves - 1) / (64 * kCopyWaves));
+    k_enc_copy<<<ngrp, 64 * kCopyWaves, 0, s>>>(d_items, n, d_blob, d_P, d_segs, tail.n_segments, d_stream, d_pos);
+    k_enc_hdr<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(d_items, n, d_blob, d_P, d_stream);
+    MHIP(hipGetLastError());
+  }
+  if (tail.n_segments)
+    MHIP(hipMemcpyAsync(h_segs, d_segs, sizeof(ldb_merge_segment) * tail.n_segments, hipMemcpyDeviceToHost, s));
+  MHIP(hipStreamSynchronize(s));
   h_result->status = LDB_OK;
   return LDB_OK;
 }

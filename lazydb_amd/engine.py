@@ -148,6 +148,37 @@ class Engine:
                 "pos": pos, "segments": segs[: min(res.n_segments, seg_cap)],
                 "live": d_live[: res.n_records] if want_live else None, "stats": stats[: len(files)]}
 
+    def encode_entries(self, items, blob, active_fid: int, active_off: int, max_file_size: int, seg_cap: int = 256,
+                       stream=None):
+        """Batch writeLogEntry (tx.go:156-206 commit loop; EncodeEntry log_entry.go:48-78 + the rollover
+        of db.go:485). items: numpy ENCODE_ITEM array; blob: device uint8 tensor holding the keys and
+        values. Returns dict(result, stream (device tensor), pos (numpy ldb_merge_pos), segments)."""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        items = np.ascontiguousarray(items, dtype=N.ENCODE_ITEM)
+        n = items.size
+        d_items = t.from_numpy(items.view(np.uint8).reshape(-1).copy()).to(dev) if n else None
+        cap = int(n * 38 + (int(items["k_size"].sum()) + int(items["v_size"].sum()) if n else 0)) + 16
+        if stream is None:
+            stream = t.cuda.current_stream(dev)
+        for _attempt in range(2):
+            d_stream = t.empty(max(cap, 16), dtype=t.uint8, device=dev)
+            d_pos = t.empty(max(n, 1) * N.MERGE_POS.itemsize, dtype=t.uint8, device=dev)
+            segs = np.zeros(max(seg_cap, 1), dtype=N.MERGE_SEGMENT)
+            res = N.MergeResult()
+            rc = N.lib().ldb_encode_entries_dev(
+                self.ctx, n, d_items.data_ptr() if n else None, blob.data_ptr() if blob.numel() else None,
+                active_fid, active_off, max_file_size, d_stream.data_ptr(), cap, d_pos.data_ptr(), n,
+                segs.ctypes.data, seg_cap, C.byref(res), C.c_void_p(stream.cuda_stream))
+            if rc != N.ERR_CAPACITY:
+                break
+            seg_cap = max(seg_cap, res.n_segments)
+        N.check(rc, "ldb_encode_entries_dev")
+        pos = (np.frombuffer(d_pos[: n * N.MERGE_POS.itemsize].cpu().numpy().tobytes(), dtype=N.MERGE_POS)
+               if n else np.zeros(0, N.MERGE_POS))
+        return {"result": res, "stream": d_stream[: res.emit_bytes], "pos": pos,
+                "segments": segs[: res.n_segments]}
+
     def merge_timing(self):
         a, b, c = C.c_double(), C.c_double(), C.c_double()
         N.check(N.lib().ldb_merge_timing(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "merge_timing")

@@ -232,3 +232,23 @@ def merge(files, active_fid: int, active_off: int, max_file_size: int, now: int,
         foff += len(buf)
     return {"status": 0, "bad_file": -1, "stream": bytes(stream), "pos": pos, "segments": [tuple(s) for s in segs],
             "live": live, "end_fid": fid, "end_off": foff}
+
+
+def write_entries(entries, active_fid: int, active_off: int, max_file_size: int):
+    """A transaction commit's writeLogEntry loop (tx.go:156-206 -> db.go:473-523) over Entry objects:
+    EncodeEntry, rollover to fid+1 when Offset + size > MaxLogFileSize, append. Returns
+    (stream bytes, [(fid, offset, size)], segments [(fid, file_off, stream_off, n_bytes)], end_fid, end_off)."""
+    fid, off = active_fid, active_off
+    stream = bytearray()
+    pos, segs = [], []
+    for e in entries:
+        buf = encode_entry(e)
+        if off + len(buf) > max_file_size:
+            fid, off = fid + 1, 0
+        if not segs or segs[-1][0] != fid or segs[-1][1] + segs[-1][3] != off:
+            segs.append([fid, off, len(stream), 0])
+        segs[-1][3] += len(buf)
+        pos.append((fid, off, len(buf)))
+        stream += buf
+        off += len(buf)
+    return bytes(stream), pos, [tuple(x) for x in segs], fid, off
