@@ -132,6 +132,12 @@ int ldb_scan_file_dev(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, uint32
 int ldb_scan_file(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type,
                   int tuple_kind, void* h_out, uint64_t cap, ldb_scan_result* h_result);
 
+/* Page-lock a host range (e.g. an mmap'd log file, mmap/mmap_linux.go:14-20) for the lifetime of the
+ * mapping, so ldb_scan_file's host-to-device copy runs as direct DMA at PCIe rate instead of through
+ * the runtime's pageable staging. Optional: ldb_scan_file works on any host memory. */
+int ldb_host_register(ldb_ctx* ctx, const void* h_ptr, uint64_t len);
+int ldb_host_unregister(ldb_ctx* ctx, const void* h_ptr);
+
 /* Batch of device-resident files scanned back to back on one stream (one device).
  * Multi-GPU callers give each device its own context and file subset. */
 int ldb_scan_files_dev(ldb_ctx* ctx, int n_files, const uint8_t* const* d_images, const uint64_t* lens,

@@ -101,6 +101,11 @@ def lib():
             L.ldb_merge_files_dev.restype = i32
             L.ldb_merge_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
             L.ldb_merge_timing.restype = i32
+        if hasattr(L, "ldb_host_register"):
+            L.ldb_host_register.argtypes = [vp, vp, u64]
+            L.ldb_host_register.restype = i32
+            L.ldb_host_unregister.argtypes = [vp, vp]
+            L.ldb_host_unregister.restype = i32
         if hasattr(L, "ldb_encode_entries_dev"):
             L.ldb_encode_entries_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u64, vp, u64, vp, u32,
                                                  C.POINTER(MergeResult), vp]
@@ -114,7 +119,7 @@ def lib():
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
            "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_read_ceiling", "ldb_merge_files_dev",
-           "ldb_merge_timing", "ldb_encode_entries_dev")
+           "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_host_register", "ldb_host_unregister")
 
 
 def status_str(s: int) -> str:

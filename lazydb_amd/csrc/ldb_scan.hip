@@ -1032,6 +1032,18 @@ int ldb_scan_files_dev(ldb_ctx* c, int n_files, const uint8_t* const* d_images, 
   return LDB_OK;
 }
 
+int ldb_host_register(ldb_ctx* c, const void* h_ptr, uint64_t len) {
+  if (!c || !h_ptr || !len) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  return hipHostRegister(const_cast<void*>(h_ptr), len, hipHostRegisterDefault) == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+}
+
+int ldb_host_unregister(ldb_ctx* c, const void* h_ptr) {
+  if (!c || !h_ptr) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  return hipHostUnregister(const_cast<void*>(h_ptr)) == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+}
+
 int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
                   void* h_out, uint64_t cap, ldb_scan_result* h_result) {
   if (!c || !h_result || (len && !h_image) || (cap && !h_out)) return LDB_ERR_ARG;

@@ -184,6 +184,13 @@ class Engine:
         N.check(N.lib().ldb_merge_timing(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "merge_timing")
         return a.value, b.value, c.value
 
+    def host_register(self, img: np.ndarray):
+        """Page-lock a host image (ldb_host_register) so ldb_scan_file copies it by direct DMA."""
+        N.check(N.lib().ldb_host_register(self.ctx, img.ctypes.data, img.nbytes), "ldb_host_register")
+
+    def host_unregister(self, img: np.ndarray):
+        N.check(N.lib().ldb_host_unregister(self.ctx, img.ctypes.data), "ldb_host_unregister")
+
     def read_ceiling(self, d_img, iters: int = 20) -> float:
         """GB/s of a read-only reduction over the device image (the practical HBM-read ceiling)."""
         g = C.c_double()
