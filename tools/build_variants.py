@@ -46,6 +46,12 @@ def build(name: str) -> str:
                         *([m] if os.path.exists(m := os.path.join(tmp, "lazydb_amd/csrc/ldb_merge.hip")) else [])],
                        check=True)
         return out
+    elif name.startswith("llvm_"):   # backend scheduling options (A/B of codegen only)
+        opts = {"maxilp": ["-amdgpu-sched-strategy=max-ilp"], "iterilp": ["-amdgpu-sched-strategy=iterative-ilp"],
+                "memclause": ["-amdgpu-sched-strategy=max-memory-clause"], "wavepri": ["-amdgpu-set-wave-priority"],
+                "trackers": ["-amdgpu-use-amdgpu-trackers=1"], "relaxocc": ["-amdgpu-schedule-relaxed-occupancy"],
+                "bias100": ["-amdgpu-schedule-metric-bias=100"], "bias0": ["-amdgpu-schedule-metric-bias=0"]}[name[5:]]
+        defs = [x for o in opts for x in ("-mllvm", o)]
     elif name == "stamps":
         defs = ["-DLDB_STAMPS=1"]
     elif name == "stamps1":   # one wave per SIMD: phase stamps measure each wave's own critical path
