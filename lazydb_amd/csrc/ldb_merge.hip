@@ -95,6 +95,12 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __device__ uint64_t key_hash(const uint8_t* p, uint32_t n) {
   uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xFF51AFD7ED558CCDull);
   uint32_t i = 0;
+  for (; i + 16 <= n; i += 16) {   // 16-B (unaligned) loads: half the memory instructions
+    uint64_t w[2];
+    __builtin_memcpy(w, p + i, 16);
+    h = mix64(h ^ w[0]) + 0x632BE59BD9B4E019ull;
+    h = mix64(h ^ w[1]) + 0x632BE59BD9B4E019ull;
+  }
   for (; i + 8 <= n; i += 8) h = mix64(h ^ load8u(p + i)) + 0x632BE59BD9B4E019ull;
   uint64_t t = 0;
   for (uint32_t j = 0; i + j < n; ++j) t |= (uint64_t)p[i + j] << (8 * j);
@@ -103,6 +109,12 @@ __device__ uint64_t key_hash(const uint8_t* p, uint32_t n) {
 
 __device__ bool key_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
   uint32_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    uint4 x, y;
+    __builtin_memcpy(&x, a + i, 16);
+    __builtin_memcpy(&y, b + i, 16);
+    if (((x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w)) != 0) return false;
+  }
   for (; i + 8 <= n; i += 8)
     if (load8u(a + i) != load8u(b + i)) return false;
   for (; i < n; ++i)
@@ -117,6 +129,16 @@ __device__ __forceinline__ uint32_t file_of(const FileDesc* d, uint32_t n_files,
     if (d[mid].seq_base <= seq) lo = mid; else hi = mid - 1;
   }
   return lo;
+}
+
+// File descriptors staged in LDS (small file counts, the common case): the per-record binary search
+// then costs LDS reads instead of dependent global loads. Every thread of the block must call it.
+constexpr uint32_t kFdLds = 256;
+__device__ __forceinline__ const FileDesc* stage_fd(const FileDesc* fd, uint32_t n_files, FileDesc* s) {
+  if (n_files + 1 > kFdLds) return fd;
+  for (uint32_t i = threadIdx.x; i <= n_files; i += blockDim.x) s[i] = fd[i];
+  __syncthreads();
+  return s;
 }
 
 // Go binary.PutVarint (zig-zag) — encoding/binary/varint.go; EncodeEntry's field encoder
@@ -188,8 +210,10 @@ __device__ __forceinline__ const uint8_t* key_of(const FileDesc* fd, uint32_t n_
 // 64-bit atomicMax: every record that reaches a slot has the slot's key (it claimed it, or compared its
 // key bytes equal with the slot's current record), so the tag half never changes and the low half ends
 // as the key's last record. 8-B slots keep the table within the Infinity Cache at config-5 sizes.
-__global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
+__global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
                                                 unsigned long long* tab, uint64_t mask, uint32_t* __restrict__ slot) {
+  __shared__ FileDesc s_fd[kFdLds];
+  const FileDesc* fd = stage_fd(gfd, n_files, s_fd);
   uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (seq >= n) return;
   uint32_t kl;
@@ -220,13 +244,15 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
 // live = last record of its key and not an SDelete (index.go:16-25); emit = live && target file &&
 // not expired (db.go:403-409, 255). Per-file live counts/bytes: a block whose records all lie in one
 // file writes one partial (k_file_stats sums them); a block that straddles files adds per record.
-__global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
+__global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
                                               const unsigned long long* __restrict__ tab,
                                               const uint32_t* __restrict__ slot,
                                               int64_t now, uint8_t* __restrict__ live_out,
                                               uint32_t* __restrict__ esz, unsigned long long* __restrict__ part,
                                               unsigned long long* __restrict__ fstat) {
   __shared__ unsigned long long sc[4], sb[4];
+  __shared__ FileDesc s_fd[kFdLds];
+  const FileDesc* fd = stage_fd(gfd, n_files, s_fd);
   const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x;
   const uint64_t seq = b0 + threadIdx.x;
   const bool valid = seq < n;
@@ -491,13 +517,15 @@ constexpr int kCopyWaves = 4;
 // verbatim: EncodeEntry re-produces their bytes. A non-canonical record gets its key/value copied and
 // its header re-encoded by its lane, CRC-32 over the new header and the key/value (log_entry.go:48-78).
 __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
-    uint64_t n, const FileDesc* __restrict__ fd, uint32_t n_files,
+    uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
     const uint64_t* __restrict__ P, const uint32_t* __restrict__ C, const ldb_merge_segment* __restrict__ segs,
     uint32_t n_segs, uint8_t* __restrict__ stream, ldb_merge_pos* __restrict__ pos) {
   __shared__ const uint8_t* s_src[kCopyWaves][64];
   __shared__ uint8_t* s_dst[kCopyWaves][64];
   __shared__ uint32_t s_nb[kCopyWaves][64];
   __shared__ uint32_t s_ex[kCopyWaves][64];
+  __shared__ FileDesc s_fd[kFdLds];
+  const FileDesc* fd = stage_fd(gfd, n_files, s_fd);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t seq = ((uint64_t)blockIdx.x * kCopyWaves + w) * 64 + lane;
   uint32_t pieces = 0;
