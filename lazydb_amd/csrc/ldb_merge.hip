@@ -72,6 +72,11 @@ struct MergeWs {
   uint64_t small_bytes = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float t_scan = 0, t_live = 0, t_compact = 0;
+  // a second scan context on its own stream: files alternate between the two, so one file's small
+  // pipeline kernels (k_link .. k_compact) overlap the next file's k_scan_main
+  ldb_ctx* aux = nullptr;
+  hipStream_t aux_s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 #define MHIP(x)                                    \
@@ -815,6 +820,10 @@ __attribute__((visibility("hidden"))) void ldb_merge_release_(void* p) {
   if (m->small) (void)hipFree(m->small);
   for (auto& e : m->ev)
     if (e) (void)hipEventDestroy(e);
+  if (m->aux) (void)ldb_ctx_destroy(m->aux);
+  if (m->aux_s) (void)hipStreamDestroy(m->aux_s);
+  if (m->fork) (void)hipEventDestroy(m->fork);
+  if (m->join) (void)hipEventDestroy(m->join);
   delete m;
 }
 
@@ -865,10 +874,26 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   for (uint32_t i = 0; i < nf; ++i) sbase[i + 1] = sbase[i] + files[i].len / 64 + 1024;
   rc = grow_recs(m, std::max<uint64_t>(sbase[nf], 4096), 0, s);
   if (rc != LDB_OK) return rc;
+  if (nf > 1 && !m->aux) {
+    if (ldb_ctx_create(m->device, &m->aux) != LDB_OK) return LDB_ERR_HIP;
+    MHIP(hipStreamCreateWithFlags(&m->aux_s, hipStreamNonBlocking));
+    MHIP(hipEventCreateWithFlags(&m->fork, hipEventDisableTiming));
+    MHIP(hipEventCreateWithFlags(&m->join, hipEventDisableTiming));
+  }
+  if (nf > 1) {
+    MHIP(hipEventRecord(m->fork, s));
+    MHIP(hipStreamWaitEvent(m->aux_s, m->fork, 0));
+  }
   for (uint32_t i = 0; i < nf; ++i) {
-    rc = ldb_scan_file_dev(ctx, files[i].d_image, files[i].len, files[i].fid, io_type, LDB_TUPLE_INDEX,
-                           m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i, s);
+    const bool odd = (i & 1) && nf > 1;
+    rc = ldb_scan_file_dev(odd ? m->aux : ctx, files[i].d_image, files[i].len, files[i].fid, io_type,
+                           LDB_TUPLE_INDEX, m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i,
+                           odd ? m->aux_s : s);
     if (rc != LDB_OK) return rc;
+  }
+  if (nf > 1) {
+    MHIP(hipEventRecord(m->join, m->aux_s));
+    MHIP(hipStreamWaitEvent(s, m->join, 0));
   }
   if (nf) MHIP(hipMemcpyAsync(rh.data(), d_res, sizeof(ldb_scan_result) * nf, hipMemcpyDeviceToHost, s));
   MHIP(hipStreamSynchronize(s));
