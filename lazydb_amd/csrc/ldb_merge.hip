@@ -561,7 +561,9 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
       src = fimg + e.offset + (canon ? 0 : e.hdr_size);
       dst = stream + sp + (canon ? 0 : e.enc_hdr_size);
       nb = canon ? (uint32_t)sz : e.k_size + e.v_size;
-      pieces = (nb + 15) >> 4;
+      // destination-aligned pieces: a head up to the next 16-B boundary, then aligned 16-B stores
+      const uint32_t head = min(nb, (16u - (uint32_t)((uintptr_t)dst & 15u)) & 15u);
+      pieces = (head ? 1u : 0u) + ((nb - head + 15) >> 4);
     }
   }
   uint32_t inc = pieces;
@@ -582,13 +584,17 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
       if (s_ex[w][mid] <= t) lo = mid; else hi = mid - 1;
     }
     const uint32_t j = t - s_ex[w][lo];
-    const uint32_t len = min(16u, s_nb[w][lo] - 16 * j);
-    const uint8_t* s = s_src[w][lo] + 16 * j;
-    uint8_t* d = s_dst[w][lo] + 16 * j;
-    if (len == 16) {
+    uint8_t* const d0 = s_dst[w][lo];
+    const uint32_t nbr = s_nb[w][lo];
+    const uint32_t head = min(nbr, (16u - (uint32_t)((uintptr_t)d0 & 15u)) & 15u);
+    const uint32_t at = head ? (j ? head + 16 * (j - 1) : 0u) : 16 * j;   // piece start within the record
+    const uint32_t len = (head && j == 0) ? head : min(16u, nbr - at);
+    const uint8_t* s = s_src[w][lo] + at;
+    uint8_t* d = d0 + at;
+    if (len == 16) {   // d is 16-B aligned here
       uint4 v;
       __builtin_memcpy(&v, s, 16);
-      __builtin_memcpy(d, &v, 16);
+      *reinterpret_cast<uint4*>(d) = v;
     } else {
       uint32_t b = 0;
       if (len & 8) {
