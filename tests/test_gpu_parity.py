@@ -143,3 +143,27 @@ def test_zero_tail_and_zero_values(eng):
             assert_same(res, tup, ref, rt)
             if im is img:   # zeroval has entries under 84 B, which the lean path leaves to region_process
                 assert res.n_fast == res.n_regions
+
+
+def test_config4_4gib_64bit_offsets(eng):
+    """BASELINE config 4 per-GPU file: 4 GiB of 64/256 entries (seed 10), offsets past 2^32.
+    Full tuple parity, then one corrupted value byte beyond 2^32: the scan must stop with
+    ErrInvalidCrc at that entry's 64-bit offset, with every earlier tuple delivered
+    (log_file.go:141-143, index.go:90)."""
+    img, n, end = coracle.gen_log(4 << 30, 10, ksize=64, vsize=256)
+    assert n == 12936648
+    d = to_dev(img)
+    res, tup = eng.scan_dev(d, cap=n + 16)
+    ref, rt = coracle.scan(img)
+    assert_same(res, tup, ref, rt)
+    assert res.status == 2 and res.n_repairs == 0
+    offs = rt["pos"] & ((1 << 40) - 1)                         # pos bits [0, 40): offset
+    k = int(np.searchsorted(offs, (1 << 32) + 12345))          # first entry starting past the mark
+    bad = int(offs[k]) + 100
+    del tup, rt, offs
+    img[bad] ^= 0x5A
+    d[bad] = int(img[bad])
+    res, tup = eng.scan_dev(d, cap=n + 16)
+    ref, rt = coracle.scan(img)
+    assert_same(res, tup, ref, rt)
+    assert ref.status == -1 and ref.end_off > (1 << 32) and res.n_entries == k
