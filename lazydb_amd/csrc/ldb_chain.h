@@ -89,15 +89,22 @@ LDB_HD uint32_t shift_tab_uniform(const uint32_t* gtab, uint32_t r) {
 // register shift by a fixed byte count: 4 lookups in a byte-indexed table set at `off`
 LDB_HD uint32_t shift_tab(const uint32_t* tab, int off, uint32_t r) {
   if (LDB_ABLATE & 2) return (r << 1) ^ (r >> 3) ^ (uint32_t)off;
+#if LDB_NIB_SHIFT
+  uint32_t x = tab[off + (r & 0xFu)];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) x ^= tab[off + 16 * q + ((r >> (4 * q)) & 0xFu)];
+  return x;
+#else
   return tab[off + (r & 0xFFu)] ^ tab[off + 256 + ((r >> 8) & 0xFFu)] ^ tab[off + 512 + ((r >> 16) & 0xFFu)] ^
          tab[off + 768 + (r >> 24)];
+#endif
 }
 
 // register shift by 8 * n bytes, n in [0, 15] (binary decomposition over the kVSOff tables)
 LDB_HD uint32_t shift_8n(const uint32_t* tab, uint32_t r, uint32_t n) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const uint32_t t = shift_tab(tab, kVSOff + i * 1024, r);
+    const uint32_t t = shift_tab(tab, kVSOff + i * kShW, r);
     r = ((n >> i) & 1u) ? t : r;
   }
   return r;
@@ -279,7 +286,7 @@ LDB_HD void crc_slice_cap(const uint32_t* tab, const SliceRows& rows, uint32_t k
     }
   }
   *ya = ra;
-  *y = shift_tab(tab, kVSOff + 2 * 1024, ra) ^ rb;
+  *y = shift_tab(tab, kVSOff + 2 * kShW, ra) ^ rb;
   *cap = kb == (uint32_t)(kS / 8) ? rb : c;   // chain B's register after the slice
   *wc = cw;
 }
@@ -320,7 +327,7 @@ LDB_HD void rewrite8(uint8_t* wbuf, const ChainPriv& c, bool inject) {
 // Lane scan of the G-chain: O_l = sum_{i <= l} shift(y_i, (l - i) slices) (Hillis-Steele, 6 steps).
 template <int I, class WP, class CPriv>
 LDB_HD void scan_step(WP& wp, const uint32_t* tab, CPriv cpriv) {
-  constexpr int off = I == 0 ? kZSOff : kSCOff + (I - 1) * 1024;
+  constexpr int off = I == 0 ? kZCOff : kSCOff + (I - 1) * kShW;
   wp.template shfl_up<(1 << I)>([&](int l) { return cpriv(l).O; },
                                 [&](int l, uint32_t t, bool valid) { if (valid) cpriv(l).O ^= shift_tab(tab, off, t); });
 }
@@ -329,7 +336,7 @@ LDB_HD void scan_step(WP& wp, const uint32_t* tab, CPriv cpriv) {
 // one segment).
 template <int I, class WP, class CPriv>
 LDB_HD void scan_step_seg(WP& wp, const uint32_t* tab, CPriv cpriv, int seg) {
-  constexpr int off = I == 0 ? kZSOff : kSCOff + (I - 1) * 1024;
+  constexpr int off = I == 0 ? kZCOff : kSCOff + (I - 1) * kShW;
   constexpr int d = 1 << I;
   wp.template shfl_up<d>([&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
     if (valid && (l < seg || l - d >= seg)) cpriv(l).O ^= shift_tab(tab, off, t);
@@ -625,14 +632,14 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       return shift_8n(v.tab, at_p, (uint32_t)(kS / 8 - 1) - c.kb);   // from P to the slice end
     });
   }
-  const uint32_t I0 = spec ? 0u : shift_tab(v.tab, kZSOff, st.I);
+  const uint32_t I0 = spec ? 0u : shift_tab(v.tab, kZCOff, st.I);
   wp.each([&](int l) {
     ChainPriv& c = cpriv(l);
     c.O = c.y ^ (l == 0 ? I0 : 0u) ^ (spec && l == L0 ? chainA : 0u);
   });
   lane_scan(wp, v.tab, cpriv, spec ? L0 : 0);
   uint32_t rpre = 0;
-  if (spec) rpre = (L0 > 0 ? shift_tab(v.tab, kZSOff, wp.from(L0 - 1, [&](int l) { return cpriv(l).O; })) : 0u) ^ chainA;
+  if (spec) rpre = (L0 > 0 ? shift_tab(v.tab, kZCOff, wp.from(L0 - 1, [&](int l) { return cpriv(l).O; })) : 0u) ^ chainA;
   const uint32_t Iin = st.I;
   wp.template shfl_up<1>([&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
     ChainPriv& c = cpriv(l);
@@ -642,7 +649,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     // G at P = slice start + 8 (kb + 1) = shift(G at the chain start, P - chain start) ^ the chain's
     // register at P; the second chain starts at byte 48, where G = shift48(G) ^ (first chain)
     const bool second = c.kb >= (uint32_t)kSplit;
-    const uint32_t base = second ? shift_tab(v.tab, kVSOff + 2 * 1024, shift_tab(v.tab, kVSOff + 1024, g)) ^ c.ya : g;
+    const uint32_t base = second ? shift_tab(v.tab, kVSOff + 2 * kShW, shift_tab(v.tab, kVSOff + kShW, g)) ^ c.ya : g;
     const uint32_t n = second ? c.kb + 1 - kSplit : c.kb + 1;
     c.y = shift_8n(v.tab, base, n) ^ crc_step8(v.tab, c.cap, (uint32_t)w, (uint32_t)(w >> 32));
   });

@@ -62,10 +62,17 @@ constexpr int kTBOff = LDB_CRC_AB ? 5120 : 0;   // 2048 + 2048 + 1024: B (LDB_CR
 constexpr int kT8Off = LDB_CRC_AB ? 10240 : 5120;   // 256: byte-at-a-time table (rare paths)
 constexpr int kZSOff = kT8Off + 256;      // 4 x 256: register shift by kS zero bytes (fold chains)
 constexpr int kKOff = kZSOff + 1024;      // kS + 1 (padded to 96): K[n] = register after n zero bytes from ~0
-// chained fast path (ldb_chain.h): register shifts as 4 byte-indexed tables of 256 each
-constexpr int kVSOff = kKOff + 96;        // 4 x 1024: shift by 8, 16, 32, 64 bytes (check-point shifts)
-constexpr int kSCOff = kVSOff + 4 * 1024; // 5 x 1024: shift by 2, 4, 8, 16, 32 slices (lane scan; 1 slice = kZSOff)
-constexpr int kTabWords = kSCOff + 5 * 1024;
+// chained fast path (ldb_chain.h): register shifts. Default: 4 byte-indexed tables of 256 each
+// (4 lookups per shift). LDB_NIB_SHIFT=1: 8 nibble-indexed tables of 16 each (8 lookups, but the
+// 16 words of a table sit in 16 distinct banks, so a wave's lookups never conflict; 31 KB less LDS).
+#ifndef LDB_NIB_SHIFT
+#define LDB_NIB_SHIFT 0
+#endif
+constexpr int kShW = LDB_NIB_SHIFT ? 128 : 1024;   // words per chain shift table
+constexpr int kVSOff = kKOff + 96;        // 4 x kShW: shift by 8, 16, 32, 64 bytes (check-point shifts)
+constexpr int kSCOff = kVSOff + 4 * kShW; // 5 x kShW: shift by 2, 4, 8, 16, 32 slices (lane scan)
+constexpr int kZCOff = LDB_NIB_SHIFT ? kSCOff + 5 * kShW : kZSOff;   // shift by 1 slice, chain layout
+constexpr int kTabWords = kSCOff + 5 * kShW + (LDB_NIB_SHIFT ? kShW : 0);
 constexpr int kTabBytes = kTabWords * 4;
 
 // Force codes for a lane (re)run.
@@ -96,11 +103,17 @@ inline void build_tables(uint32_t* tab) {
     for (uint32_t b = 0; b < 256; ++b) tab[kZSOff + q * 256 + b] = step_bits(b << (8 * q), 8 * kS);
   for (int n = 0; n < kVSOff - kKOff; ++n) tab[kKOff + n] = n <= kS ? step_bits(0xFFFFFFFFu, 8 * n) : 0u;
   auto shift_table = [&](int off, int nbytes) {
-    for (int q = 0; q < 4; ++q)
-      for (uint32_t b = 0; b < 256; ++b) tab[off + q * 256 + b] = step_bits(b << (8 * q), 8 * nbytes);
+    if (LDB_NIB_SHIFT) {
+      for (int q = 0; q < 8; ++q)
+        for (uint32_t b = 0; b < 16; ++b) tab[off + q * 16 + b] = step_bits(b << (4 * q), 8 * nbytes);
+    } else {
+      for (int q = 0; q < 4; ++q)
+        for (uint32_t b = 0; b < 256; ++b) tab[off + q * 256 + b] = step_bits(b << (8 * q), 8 * nbytes);
+    }
   };
-  for (int i = 0; i < 4; ++i) shift_table(kVSOff + i * 1024, 8 << i);
-  for (int i = 0; i < 5; ++i) shift_table(kSCOff + i * 1024, kS << (i + 1));
+  for (int i = 0; i < 4; ++i) shift_table(kVSOff + i * kShW, 8 << i);
+  for (int i = 0; i < 5; ++i) shift_table(kSCOff + i * kShW, kS << (i + 1));
+  if (LDB_NIB_SHIFT) shift_table(kZCOff, kS);
 }
 
 // ---------------------------------------------------------------- memory views

@@ -146,12 +146,13 @@ def test_zero_tail_and_zero_values(eng):
 
 
 def test_config4_4gib_64bit_offsets(eng):
-    """BASELINE config 4 per-GPU file: 4 GiB of 64/256 entries (seed 10), offsets past 2^32.
-    Full tuple parity, then one corrupted value byte beyond 2^32: the scan must stop with
+    """BASELINE config 4's per-GPU file shape (64/256 entries, seed 10) at 4.5 GiB, so entry offsets
+    pass 2^32 (a 4 GiB file ends 160 B short of it). Full tuple parity, then one corrupted value
+    byte beyond 2^32: the scan must stop with
     ErrInvalidCrc at that entry's 64-bit offset, with every earlier tuple delivered
     (log_file.go:141-143, index.go:90)."""
-    img, n, end = coracle.gen_log(4 << 30, 10, ksize=64, vsize=256)
-    assert n == 12936648
+    img, n, end = coracle.gen_log(9 << 29, 10, ksize=64, vsize=256)
+    assert n == (9 << 29) // 332 and end > (1 << 32)
     d = to_dev(img)
     res, tup = eng.scan_dev(d, cap=n + 16)
     ref, rt = coracle.scan(img)

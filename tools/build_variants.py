@@ -16,9 +16,12 @@ OUT = os.path.join(ROOT, "lazydb_amd", "_lib")
 
 def build(name: str) -> str:
     defs = []
-    m = re.fullmatch(r"(ab)?w(\d+)n(\d+)", name)
+    m = re.fullmatch(r"(ab)?(nib)?w(\d+)n(\d+)", name)
     if m:
-        defs = [f"-DLDB_WPB={m.group(2)}", f"-DLDB_NB={m.group(3)}"] + (["-DLDB_CRC_AB=1"] if m.group(1) else [])
+        defs = [f"-DLDB_WPB={m.group(3)}", f"-DLDB_NB={m.group(4)}"] + (["-DLDB_CRC_AB=1"] if m.group(1) else []) + \
+               (["-DLDB_NIB_SHIFT=1"] if m.group(2) else [])
+    elif name == "nib":   # nibble-indexed chain shift tables (conflict-free, 31 KB less LDS)
+        defs = ["-DLDB_NIB_SHIFT=1"]
     elif name == "bperm":
         defs = ["-DLDB_SCAN_BPERM=1"]
     elif name == "late":
