@@ -262,6 +262,17 @@ int ldb_encode_entries_dev(ldb_ctx* ctx, uint64_t n, const ldb_encode_item* d_it
                            uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap, ldb_merge_segment* h_segs,
                            uint32_t seg_cap, ldb_merge_result* h_result, void* stream);
 
+/* Cross-GPU merge (SURVEY.md 8(e), config 5 over N GPUs): each rank merges a contiguous fid block,
+ * and the ranks' compacted streams form one writeLogEntry rollover chain (db.go:485-510) in rank
+ * order. This re-places n records (entry sizes d_sizes, stream order; NULL: d_pos[i].entry_size) from
+ * the start state (active_fid, active_off): h_result gets emit_bytes, end_fid, end_off, n_segments;
+ * h_segs (host, seg_cap; may be NULL) the segments; d_pos (device; may be NULL) has offset and fid of
+ * every record rewritten, other fields kept. Synchronous. LDB_ERR_CAPACITY: more than seg_cap
+ * segments (d_pos is still complete). */
+int ldb_merge_repack_dev(ldb_ctx* ctx, uint64_t n, const uint32_t* d_sizes, ldb_merge_pos* d_pos,
+                         uint32_t active_fid, uint64_t active_off, uint64_t max_file_size,
+                         ldb_merge_segment* h_segs, uint32_t seg_cap, ldb_merge_result* h_result, void* stream);
+
 /* Timing hook for bench.py: device time (ms) of the last ldb_merge_files_dev call, split into the
  * replay scans, the liveness resolution (hash + last-writer-wins) and the compaction (prefix sums,
  * rollover packing, stream copy), measured with HIP events on the merge stream. */

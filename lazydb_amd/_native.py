@@ -106,6 +106,9 @@ def lib():
             L.ldb_host_register.restype = i32
             L.ldb_host_unregister.argtypes = [vp, vp]
             L.ldb_host_unregister.restype = i32
+        if hasattr(L, "ldb_merge_repack_dev"):
+            L.ldb_merge_repack_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u32, vp, vp]
+            L.ldb_merge_repack_dev.restype = i32
         if hasattr(L, "ldb_encode_entries_dev"):
             L.ldb_encode_entries_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u64, vp, u64, vp, u32,
                                                  C.POINTER(MergeResult), vp]
@@ -119,7 +122,7 @@ def lib():
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
            "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_read_ceiling", "ldb_merge_files_dev",
-           "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_host_register", "ldb_host_unregister")
+           "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_merge_repack_dev", "ldb_host_register", "ldb_host_unregister")
 
 
 def status_str(s: int) -> str:

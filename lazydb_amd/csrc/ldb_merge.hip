@@ -1103,6 +1103,101 @@ extern "C" int ldb_encode_entries_dev(ldb_ctx* ctx, uint64_t n, const ldb_encode
   return LDB_OK;
 }
 
+// ------------------------------------------------------------------------------ repack (cross-GPU merge)
+// A compacted stream cut into per-rank pieces is placed by one global writeLogEntry rollover chain
+// (db.go:485-510): rank r's records start where rank r-1's ended. ldb_merge_repack_dev re-runs k_pack
+// over a record-size list from a given (fid, offset) and rewrites the records' ValuePos.
+__global__ __launch_bounds__(256) void k_pos_size(uint64_t n, const ldb_merge_pos* __restrict__ pos,
+                                                  uint32_t* __restrict__ esz) {
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i < n) esz[i] = pos[i].entry_size;
+}
+
+__global__ __launch_bounds__(256) void k_repos(uint64_t n, const uint64_t* __restrict__ P,
+                                               const ldb_merge_segment* __restrict__ segs, uint32_t n_segs,
+                                               ldb_merge_pos* __restrict__ pos) {
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t sp = P[i];
+  const ldb_merge_segment& sg = segs[seg_of(segs, n_segs, sp)];
+  pos[i].offset = sg.file_off + (sp - sg.stream_off);
+  pos[i].fid = sg.fid;
+}
+
+extern "C" int ldb_merge_repack_dev(ldb_ctx* ctx, uint64_t n, const uint32_t* d_sizes, ldb_merge_pos* d_pos,
+                                    uint32_t active_fid, uint64_t active_off, uint64_t max_file_size,
+                                    ldb_merge_segment* h_segs, uint32_t seg_cap, ldb_merge_result* h_result,
+                                    void* stream) {
+  if (!ctx || !h_result || (n && !d_sizes && !d_pos) || max_file_size == 0 || n >= 0xFFFFFFFFull)
+    return LDB_ERR_ARG;
+  std::memset(h_result, 0, sizeof(*h_result));
+  h_result->bad_file = -1;
+  h_result->end_fid = active_fid;
+  h_result->end_off = active_off;
+  h_result->n_emit = n;
+  if (hipSetDevice(ldb_ctx_device_(ctx)) != hipSuccess) return LDB_ERR_HIP;
+  MergeWs* m = get_ws(ctx);
+  if (!m) return LDB_ERR_NOMEM;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+  const uint64_t o_esz = 0, o_P = align256(4 * n), o_C = align256(o_P + 8 * (n + 1));
+  const uint64_t o_bs = align256(o_C + 4 * (n + 1)), o_bc = align256(o_bs + 8 * (ntiles + 1));
+  int rc = grow(&m->seqbuf, &m->seqbuf_bytes, align256(o_bc + 4 * (ntiles + 1)));
+  if (rc != LDB_OK) return rc;
+  uint32_t* d_esz = reinterpret_cast<uint32_t*>(m->seqbuf + o_esz);
+  uint64_t* d_P = reinterpret_cast<uint64_t*>(m->seqbuf + o_P);
+  uint32_t* d_C = reinterpret_cast<uint32_t*>(m->seqbuf + o_C);
+  uint64_t* d_bs = reinterpret_cast<uint64_t*>(m->seqbuf + o_bs);
+  uint32_t* d_bc = reinterpret_cast<uint32_t*>(m->seqbuf + o_bc);
+  if (n) {
+    const uint32_t* esz = d_sizes;
+    if (!esz) {
+      k_pos_size<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(n, d_pos, d_esz);
+      esz = d_esz;
+    }
+    k_scan_reduce<<<(uint32_t)ntiles, kScanBlock, 0, s>>>(esz, n, d_bs, d_bc);
+    k_scan_tiles<<<1, kScanBlock, 0, s>>>(d_bs, d_bc, ntiles, d_P, d_C, n);
+    k_scan_write<<<(uint32_t)ntiles, kScanBlock, 0, s>>>(esz, n, d_bs, d_bc, d_P, d_C);
+  } else {
+    MHIP(hipMemsetAsync(d_P, 0, 8, s));
+  }
+  // every segment stays on the device for k_repos: a second k_pack with room for all of them if needed
+  uint32_t dev_cap = std::max<uint32_t>(seg_cap, 64);
+  Tail tail;
+  uint64_t tot = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    const uint64_t o_tail = 0, o_seg = align256(sizeof(Tail));
+    rc = grow(&m->small, &m->small_bytes, o_seg + sizeof(ldb_merge_segment) * ((uint64_t)dev_cap + 1));
+    if (rc != LDB_OK) return rc;
+    Tail* d_tail = reinterpret_cast<Tail*>(m->small + o_tail);
+    ldb_merge_segment* d_segs = reinterpret_cast<ldb_merge_segment*>(m->small + o_seg);
+    k_pack<<<1, 64, 0, s>>>(d_P, n, active_fid, active_off, max_file_size, d_segs, dev_cap + 1, d_tail);
+    MHIP(hipGetLastError());
+    MHIP(hipMemcpyAsync(&tot, d_P + n, 8, hipMemcpyDeviceToHost, s));
+    MHIP(hipMemcpyAsync(&tail, d_tail, sizeof(Tail), hipMemcpyDeviceToHost, s));
+    MHIP(hipStreamSynchronize(s));
+    if (tail.n_segments <= dev_cap + 1) {
+      if (n && d_pos) {
+        k_repos<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(n, d_P, d_segs, tail.n_segments, d_pos);
+        MHIP(hipGetLastError());
+      }
+      if (h_segs && tail.n_segments)
+        MHIP(hipMemcpyAsync(h_segs, d_segs, sizeof(ldb_merge_segment) * std::min(tail.n_segments, seg_cap),
+                            hipMemcpyDeviceToHost, s));
+      MHIP(hipStreamSynchronize(s));
+      break;
+    }
+    dev_cap = tail.n_segments;
+  }
+  h_result->emit_bytes = tot;
+  h_result->end_fid = tail.end_fid;
+  h_result->end_off = tail.end_off;
+  h_result->n_segments = tail.n_segments;
+  if (h_segs && tail.n_segments > seg_cap) return h_result->status = LDB_ERR_CAPACITY;
+  h_result->status = LDB_OK;
+  return LDB_OK;
+}
+
 extern "C" int ldb_merge_timing(ldb_ctx* ctx, double* scan_ms, double* live_ms, double* compact_ms) {
   if (!ctx) return LDB_ERR_ARG;
   MergeWs* m = static_cast<MergeWs*>(*ldb_ctx_merge_slot_(ctx));
