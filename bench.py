@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--gather", type=int, default=1)
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
+    ap.add_argument("--xmerge", action="store_true",
+                    help="config 5 as ONE 16-file set split over the ranks in fid blocks (cross-GPU merge)")
+    ap.add_argument("--xsim", type=int, default=0,
+                    help="config 5 --xmerge: play K ranks in this one process and time each rank's phases")
     ap.add_argument("--e2e", type=int, default=3, help="iterations of the PCIe-inclusive host-API leg (0: skip)")
     return ap.parse_args()
 
@@ -128,8 +132,8 @@ def main_merge(args):
     every key written twice so exactly half the records are stale), 15 archived targets merged into
     the active file 16: replay scans + last-writer-wins liveness + compacted stream with rollover
     (db.go:383-427, 243-265, 473-523). One step = one ldb_merge_files_dev call over device-resident
-    images. With N ranks each rank merges its own independent 16-file set (weak scaling; the
-    cross-rank liveness exchange of SURVEY 8(e) is not built yet)."""
+    images. With N ranks each rank merges its own independent 16-file set (weak scaling); --xmerge
+    splits ONE set over the ranks instead (main_xmerge)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -211,8 +215,128 @@ def main_merge(args):
         dist.destroy_process_group()
 
 
+def main_xmerge(args):
+    """BASELINE config 5 over N GPUs as ONE merge: the 16-file set is split in contiguous fid blocks,
+    one per rank (lazydb_amd/xmerge.py: summary all-gather, per-rank ldb_merge_files_dev, global
+    rollover by ldb_merge_repack_dev). One step = one merge_distributed call; value = the set's
+    input bytes / step time (strong scaling: the total work is fixed). --xsim K plays K ranks in this
+    process, times each rank's phases on its own and reports the critical path (no exchange cost)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    from lazydb_amd import Engine
+    from lazydb_amd import multi
+    from lazydb_amd import xmerge as X
+    from oracle import coracle   # format producer for the synthetic input; checker
+    now = 1_700_000_000
+    imgs, n, ends = coracle.gen_merge(16, 256 << 20, 16 * 808_540, 3, ksize=64, vsize=256)
+    kw = dict(active_fid=16, active_off=ends[15], max_file_size=256 << 20, now=now)
+    eng = Engine(local)
+    sim = args.xsim
+    nr = sim if sim else world
+    blocks = [list(b) for b in np.array_split(np.arange(16), nr)]
+    mine = blocks[rank] if not sim else list(range(16))
+    dfiles = {i: (torch.from_numpy(imgs[i]).to(dev), i + 1, i < 15) for i in mine}
+    in_bytes = sum(ends)
+    ref = None if args.no_verify else coracle.merge([(imgs[i], i + 1, i < 15) for i in range(16)], 16, ends[15],
+                                                    256 << 20, now)
+
+    def sync():
+        torch.cuda.synchronize()
+
+    if sim:
+        ph = np.zeros((nr, 3))
+        verified = None
+        for step in range(args.warmup + args.steps):
+            own = [[dfiles[i] for i in b] for b in blocks]
+            summ, parts, places = [], [], []
+            for r in range(nr):
+                sync(); t0 = time.perf_counter()
+                summ.append(X.rank_summary(eng, own[r])[0] if r > 0 else None)   # rank 0's is never read
+                sync(); ph[r, 0] += (time.perf_counter() - t0) if step >= args.warmup else 0
+            for r in range(nr):
+                sync(); t0 = time.perf_counter()
+                parts.append(X.rank_merge(eng, own[r], summ[r + 1:], X.summary_fid_base(16) + r + 1, **kw))
+                sync(); ph[r, 1] += (time.perf_counter() - t0) if step >= args.warmup else 0
+            sizes = [X.entry_sizes(eng, p) for p in parts]
+            for r in range(nr):
+                sync(); t0 = time.perf_counter()
+                places.append(X.rank_place(eng, parts[r], torch.cat(sizes[:r]) if r else None, kw["active_fid"],
+                                           kw["active_off"], kw["max_file_size"], fetch_pos=False))
+                sync(); ph[r, 2] += (time.perf_counter() - t0) if step >= args.warmup else 0
+        ph /= args.steps
+        if ref is not None:
+            verified = bool(b"".join(p["stream"].cpu().numpy().tobytes() for p in parts) == ref[1].tobytes()
+                            and places[-1]["end"] == (ref[0].end_fid, ref[0].end_off))
+        crit = float(ph.max(axis=0).sum())
+        xbytes = sum(int(s.numel()) for s in summ if s is not None)
+        print(json.dumps({
+            "metric": "merge/GC decode+CRC32+liveness+compaction: input GiB/s (BASELINE config 5), simulated ranks",
+            "simulated_ranks": nr, "steps": args.steps, "warmup": args.warmup,
+            "per_rank_ms": {"summary": [round(x * 1e3, 3) for x in ph[:, 0]],
+                            "merge": [round(x * 1e3, 3) for x in ph[:, 1]],
+                            "place": [round(x * 1e3, 3) for x in ph[:, 2]]},
+            "critical_path_ms": round(crit * 1e3, 3),
+            "est_GiB_per_s_without_exchange": round(in_bytes / crit / 2**30, 3),
+            "summary_bytes_all_gathered": xbytes, "verified_vs_oracle": verified}))
+        eng.close()
+        return
+    files = [dfiles[i] for i in mine]
+
+    def step_once():
+        return (X.merge_distributed(eng, files, 16, **kw, fetch_pos=False) if world > 1
+                else X.merge_distributed_single(eng, files, **kw, fetch_pos=False))
+
+    out = step_once()
+    verified = None
+    if ref is not None:
+        got = multi.gather_tuples(out["stream"]) if world > 1 else [out["stream"]]
+        if rank == 0:
+            verified = bool(b"".join(g.cpu().numpy().tobytes() for g in got) == ref[1].tobytes())
+        if world > 1:
+            ends_ok = torch.tensor([int(out["end"] == (ref[0].end_fid, ref[0].end_off)) if rank == world - 1 else 1],
+                                   device=dev)
+            dist.all_reduce(ends_ok, op=dist.ReduceOp.MIN)
+            verified = bool(verified and int(ends_ok.item())) if rank == 0 else verified
+    for _ in range(args.warmup):
+        step_once()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_once()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t = multi.max_over_ranks(time.perf_counter() - t0, dev)
+    if rank == 0:
+        step = t / args.steps
+        print(json.dumps({
+            "metric": "merge/GC decode+CRC32+liveness+compaction: input GiB/s (BASELINE config 5), one set over N GPUs",
+            "value": round(in_bytes / step / 2**30, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(step * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (writeLogEntry format, every key written twice)",
+            "config": {"workload": "16 log files x 256 MiB, 64B key / 256B value, 50% stale, 15 targets",
+                       "parallelism": f"fid blocks over {world} GPU(s), summary all-gather + rollover chain"},
+            "verified_vs_oracle": verified}))
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.config == 5 and (args.xmerge or args.xsim):
+        return main_xmerge(args)
     if args.config == 5:
         return main_merge(args)
     import numpy as np

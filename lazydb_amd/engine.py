@@ -179,6 +179,31 @@ class Engine:
         return {"result": res, "stream": d_stream[: res.emit_bytes], "pos": pos,
                 "segments": segs[: res.n_segments]}
 
+    def encode_entries_dev(self, d_items, n: int, blob, cap: int, active_fid: int, active_off: int,
+                           max_file_size: int, seg_cap: int = 256, stream=None):
+        """encode_entries with the ENCODE_ITEM array already on the device (d_items: uint8 tensor of
+        n * 48 bytes) and the stream capacity given (n * 38 + the key and value bytes suffice)."""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        if stream is None:
+            stream = t.cuda.current_stream(dev)
+        for _attempt in range(2):
+            d_stream = t.empty(max(cap, 16), dtype=t.uint8, device=dev)
+            d_pos = t.empty(max(n, 1) * N.MERGE_POS.itemsize, dtype=t.uint8, device=dev)
+            segs = np.zeros(max(seg_cap, 1), dtype=N.MERGE_SEGMENT)
+            res = N.MergeResult()
+            rc = N.lib().ldb_encode_entries_dev(
+                self.ctx, n, d_items.data_ptr() if n else None, blob.data_ptr() if blob.numel() else None,
+                active_fid, active_off, max_file_size, d_stream.data_ptr(), cap, d_pos.data_ptr(), n,
+                segs.ctypes.data, seg_cap, C.byref(res), C.c_void_p(stream.cuda_stream))
+            if rc != N.ERR_CAPACITY:
+                break
+            seg_cap = max(seg_cap, res.n_segments)
+            cap = max(cap, res.emit_bytes)
+        N.check(rc, "ldb_encode_entries_dev")
+        return {"result": res, "stream": d_stream[: res.emit_bytes], "pos": d_pos[: n * N.MERGE_POS.itemsize],
+                "segments": segs[: res.n_segments]}
+
     def merge_timing(self):
         a, b, c = C.c_double(), C.c_double(), C.c_double()
         N.check(N.lib().ldb_merge_timing(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "merge_timing")

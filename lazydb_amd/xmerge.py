@@ -47,7 +47,8 @@ def summary_fid_base(max_fid: int) -> int:
 
 def rank_summary(eng, files, io_type: int = N.FILEIO):
     """Phase 1 on one rank. files: [(device uint8 tensor, fid, is_target)], ascending fid.
-    Returns the summary log (device uint8 tensor, zero-padded) and its record count."""
+    Returns the summary log (device uint8 tensor, zero-padded) and its record count. Device-resident:
+    the replay tuples, the selection and the ENCODE_ITEM array never leave the GPU."""
     t = eng.torch
     dev = f"cuda:{eng.device}"
     plain = [(img, fid, False) for img, fid, _ in files]
@@ -56,33 +57,40 @@ def rank_summary(eng, files, io_type: int = N.FILEIO):
     r = out["result"]
     if r.bad_file >= 0:
         raise N.LdbError(f"replay of file {files[r.bad_file][1]} failed: {N.status_str(r.status)}")
-    live = out["live"].cpu().numpy().astype(bool)
+    live = out["live"]
     blob = t.cat([img for img, _, _ in files]) if len(files) > 1 else files[0][0]
-    items = []
-    base = 0
-    k = 0
-    for img, fid, _ in files:
-        res, tup = eng.scan_dev(img, fid=fid, io_type=io_type)
-        n = len(tup)
-        pos = tup["pos"]
-        stat = ((pos >> np.uint64(52)) & np.uint64(0xFF)).astype(np.uint8)
-        keep = live[k:k + n] | (stat == 1)
-        off = (pos & np.uint64((1 << 40) - 1)) + ((pos >> np.uint64(40)) & np.uint64(0x3F))
-        it = np.zeros(int(keep.sum()), dtype=N.ENCODE_ITEM)
-        it["key_off"] = off[keep] + np.uint64(base)
-        it["value_off"] = it["key_off"]
-        it["k_size"] = tup["k_size"][keep]
-        it["stat"] = stat[keep]
-        items.append(it)
+    tups, ress = [], []
+    for img, fid, _ in files:   # index tuples of every file, enqueued back to back
+        cap = img.numel() // 10 + 16
+        o, res = eng.alloc_out(cap), eng.alloc_result()
+        eng.scan_dev_async(img, fid, io_type, N.TUPLE_INDEX, o, cap, res)
+        tups.append(o)
+        ress.append(res)
+    counts = [N.ScanResult.from_buffer_copy(x.cpu().numpy().tobytes()).n_entries for x in ress]
+    assert sum(counts) == r.n_records, (counts, r.n_records)
+    sel, base, k = [], 0, 0
+    for (img, _, _), o, n in zip(files, tups, counts):
+        q = o[: 16 * n].view(t.int64).view(n, 2)                    # ldb_index_tuple: pos, k | v << 32
+        pos, kv = q[:, 0], q[:, 1]
+        stat = (pos >> 52) & 0xFF
+        keep = (live[k:k + n] != 0) | (stat == 1)
+        key_off = (pos & ((1 << 40) - 1)) + ((pos >> 40) & 0x3F) + base
+        sel.append(t.stack([key_off, kv & 0xFFFFFFFF, stat], 1)[keep])
         base += img.numel()
         k += n
-    assert k == r.n_records, (k, r.n_records)
-    items = np.concatenate(items) if items else np.zeros(0, N.ENCODE_ITEM)
-    enc = eng.encode_entries(items, blob, 0, 0, NO_ROLLOVER, seg_cap=4)
+    sel = t.cat(sel) if sel else t.zeros(0, 3, dtype=t.int64, device=dev)
+    m = int(sel.shape[0])
+    items = t.zeros(m, 6, dtype=t.int64, device=dev)              # ENCODE_ITEM, 48 B
+    items[:, 0] = sel[:, 0]                                       # key_off
+    items[:, 1] = sel[:, 0]                                       # value_off (empty value)
+    items[:, 2] = sel[:, 1]                                       # k_size, v_size = 0
+    items[:, 5] = sel[:, 2] << 16                                 # tx_stat = 0, stat
+    cap = m * 38 + int(sel[:, 1].sum().item()) + 16
+    enc = eng.encode_entries_dev(items.view(t.uint8).view(-1), m, blob, cap, 0, 0, NO_ROLLOVER, seg_cap=4)
     s = enc["stream"]
     summ = t.zeros(s.numel() + SUMMARY_PAD, dtype=t.uint8, device=dev)
     summ[: s.numel()] = s
-    return summ, len(items)
+    return summ, m
 
 
 def rank_merge(eng, files, later_summaries, sum_fid0: int, active_fid: int, active_off: int,
@@ -127,7 +135,8 @@ def repack(eng, n: int, d_sizes, d_pos, start_fid: int, start_off: int, max_file
     return res, segs[: res.n_segments]
 
 
-def rank_place(eng, part, earlier_sizes, active_fid: int, active_off: int, max_file_size: int):
+def rank_place(eng, part, earlier_sizes, active_fid: int, active_off: int, max_file_size: int,
+               fetch_pos: bool = True):
     """Phase 3 on one rank: start state from the earlier ranks' entry sizes (rank order,
     concatenated, device int32), then this rank's records re-placed from it. Returns the start
     state, the segments (rank-local stream offsets), the end state and the positions (numpy)."""
@@ -137,7 +146,11 @@ def rank_place(eng, part, earlier_sizes, active_fid: int, active_off: int, max_f
     f0, o0 = (st.end_fid, st.end_off) if st is not None else (active_fid, active_off)
     n = part["n_emit"]
     res, segs = repack(eng, n, None, part["pos"], f0, o0, max_file_size)
-    pos = (np.frombuffer(part["pos"].cpu().numpy().tobytes(), dtype=N.MERGE_POS) if n else np.zeros(0, N.MERGE_POS))
+    if not fetch_pos:   # leave the positions on the device (bench)
+        pos = part["pos"]
+    else:
+        pos = (np.frombuffer(part["pos"].cpu().numpy().tobytes(), dtype=N.MERGE_POS) if n
+               else np.zeros(0, N.MERGE_POS))
     return {"start": (f0, o0), "end": (res.end_fid, res.end_off), "segments": segs, "pos": pos}
 
 
@@ -162,7 +175,7 @@ def _all_gather_varlen(x, dist):
 
 
 def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int, max_file_size: int, now: int,
-                      io_type: int = N.FILEIO):
+                      io_type: int = N.FILEIO, fetch_pos: bool = True):
     """Config 5 over the ranks of torch.distributed: this rank's contiguous fid block `files`
     ([(device tensor, fid, is_target)], ascending; blocks ascending in rank order); max_fid = the
     largest fid over all ranks. Returns this rank's piece: stream, positions, segments, liveness,
@@ -170,12 +183,25 @@ def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
-    summ, _ = rank_summary(eng, files, io_type)
-    allsum = _all_gather_varlen(summ, dist)
+    if world == 1:
+        allsum = []
+    else:   # rank r reads the summaries of ranks r+1..: nobody reads rank 0's
+        summ = rank_summary(eng, files, io_type)[0] if rank > 0 else \
+            torch.zeros(0, dtype=torch.uint8, device=files[0][0].device)
+        allsum = _all_gather_varlen(summ, dist)
     part = rank_merge(eng, files, allsum[rank + 1:], summary_fid_base(max_fid) + rank + 1, active_fid, active_off,
                       max_file_size, now, io_type)
-    sizes = _all_gather_varlen(entry_sizes(eng, part), dist)
+    sizes = _all_gather_varlen(entry_sizes(eng, part), dist) if world > 1 else []
     earlier = torch.cat(sizes[:rank]) if rank else None
-    pl = rank_place(eng, part, earlier, active_fid, active_off, max_file_size)
+    pl = rank_place(eng, part, earlier, active_fid, active_off, max_file_size, fetch_pos)
+    pl.update(stream=part["stream"], live=part["live"], stats=part["stats"], n_emit=part["n_emit"])
+    return pl
+
+
+def merge_distributed_single(eng, files, active_fid: int, active_off: int, max_file_size: int, now: int,
+                             io_type: int = N.FILEIO, fetch_pos: bool = True):
+    """merge_distributed at world size 1 without torch.distributed: the plain merge, same outputs."""
+    part = rank_merge(eng, files, [], 0, active_fid, active_off, max_file_size, now, io_type)
+    pl = rank_place(eng, part, None, active_fid, active_off, max_file_size, fetch_pos)
     pl.update(stream=part["stream"], live=part["live"], stats=part["stats"], n_emit=part["n_emit"])
     return pl
