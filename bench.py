@@ -127,6 +127,24 @@ def _cpu_model():
     return "unknown"
 
 
+def init_dist(world: int, local: int) -> int:
+    """One process per GPU over RCCL (backend "nccl"). LDB_BENCH_BACKEND=gloo rehearses the N>1
+    path with ranks sharing the GPUs of a smaller box (device = local rank mod device count);
+    the collectives then run on host copies (lazydb_amd.multi)."""
+    import torch
+    import torch.distributed as dist
+    backend = os.environ.get("LDB_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(local)
+    return local
+
+
 def main_merge(args):
     """BASELINE config 5: Merge/GC of one value type -- 16 log files x 256 MiB (64-B keys, 256-B values,
     every key written twice so exactly half the records are stale), 15 archived targets merged into
@@ -140,9 +158,7 @@ def main_merge(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
+    local = init_dist(world, local)
     dev = torch.device(f"cuda:{local}")
     from lazydb_amd import Engine
     from lazydb_amd import multi
@@ -227,9 +243,7 @@ def main_xmerge(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
+    local = init_dist(world, local)
     dev = torch.device(f"cuda:{local}")
     from lazydb_amd import Engine
     from lazydb_amd import multi
@@ -302,7 +316,7 @@ def main_xmerge(args):
             verified = bool(b"".join(g.cpu().numpy().tobytes() for g in got) == ref[1].tobytes())
         if world > 1:
             ends_ok = torch.tensor([int(out["end"] == (ref[0].end_fid, ref[0].end_off)) if rank == world - 1 else 1],
-                                   device=dev)
+                                   device=multi.coll_device(dev))
             dist.all_reduce(ends_ok, op=dist.ReduceOp.MIN)
             verified = bool(verified and int(ends_ok.item())) if rank == 0 else verified
     for _ in range(args.warmup):
@@ -346,9 +360,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
+    local = init_dist(world, local)
     dev = torch.device(f"cuda:{local}")
 
     from lazydb_amd import Engine

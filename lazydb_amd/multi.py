@@ -16,7 +16,16 @@ def files_for_rank(fids, rank: int, world: int):
     return sorted(fids)[rank::world]
 
 
+def coll_device(device):
+    """Where collective buffers live: the GPU under RCCL; host memory under gloo (CPU tests, and
+    the bench's one-GPU rehearsal of the N>1 path)."""
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return device
+
+
 def max_over_ranks(x: float, device) -> float:
+    device = coll_device(device)
     t = torch.tensor([x], dtype=torch.float64, device=device)
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -24,6 +33,7 @@ def max_over_ranks(x: float, device) -> float:
 
 
 def sum_over_ranks(xs, device):
+    device = coll_device(device)
     t = torch.tensor(list(xs), dtype=torch.float64, device=device)
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -39,6 +49,7 @@ def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0):
     assert tuple_bytes.dtype == torch.uint8 and tuple_bytes.dim() == 1
     world = dist.get_world_size()
     rank = dist.get_rank()
+    tuple_bytes = tuple_bytes.to(coll_device(tuple_bytes.device))
     dev = tuple_bytes.device
     n = torch.tensor([tuple_bytes.numel()], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(world)]
