@@ -777,7 +777,10 @@ __global__ __launch_bounds__(256) void k_enc_hdr(const ldb_encode_item* __restri
 // ------------------------------------------------------------------------------ host side
 int grow(uint8_t** p, uint64_t* have, uint64_t need) {
   if (*have >= need) return LDB_OK;
-  if (*p) (void)hipFree(*p);
+  if (*p) {   // launches on either merge stream may still read the old buffer
+    (void)hipDeviceSynchronize();
+    (void)hipFree(*p);
+  }
   *p = nullptr;
   *have = 0;
   if (hipMalloc(p, need) != hipSuccess) return LDB_ERR_NOMEM;
@@ -793,7 +796,10 @@ int grow_recs(MergeWs* m, uint64_t need, uint64_t keep, hipStream_t s) {
   if (hipMalloc(&nr, cap * sizeof(ldb_index_tuple)) != hipSuccess) return LDB_ERR_NOMEM;
   if (keep) MHIP(hipMemcpyAsync(nr, m->recs, keep * sizeof(ldb_index_tuple), hipMemcpyDeviceToDevice, s));
   MHIP(hipStreamSynchronize(s));
-  if (m->recs) (void)hipFree(m->recs);
+  if (m->recs) {   // and the aux stream's scans, which write into the record slots
+    (void)hipDeviceSynchronize();
+    (void)hipFree(m->recs);
+  }
   m->recs = nr;
   m->rec_cap = cap;
   return LDB_OK;

@@ -823,7 +823,13 @@ WsLayout layout(uint64_t len) {
 
 int ensure_ws(ldb_ctx* c, uint64_t bytes) {
   if (c->ws_bytes >= bytes) return LDB_OK;
-  if (c->ws) (void)hipFree(c->ws);
+  // The old workspace may still be read by launches in flight on any stream that used this
+  // context (the merge engine alternates two contexts on two streams): drain the device before
+  // the free, so a growth can never pull memory from under a running kernel. Growth is rare.
+  if (c->ws) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(c->ws);
+  }
   c->ws = nullptr;
   c->ws_bytes = 0;
   if (hipMalloc(&c->ws, bytes) != hipSuccess) return LDB_ERR_NOMEM;
@@ -976,6 +982,7 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
 int ldb_ctx_destroy(ldb_ctx* c) {
   if (!c) return LDB_ERR_ARG;
   (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();   // no launch of this context may outlive its buffers
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->d_xw) (void)hipFree(c->d_xw);
   if (c->d_gsh) (void)hipFree(c->d_gsh);
@@ -1053,6 +1060,8 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
   // context-owned staging (grow-only): image, tuples, result; one stream per context
   if (!c->h_stream && hipStreamCreateWithFlags(&c->h_stream, hipStreamNonBlocking) != hipSuccess) return LDB_ERR_HIP;
   const uint64_t img_need = (len + 15) & ~15ull, out_need = cap * tsz;
+  if ((img_need > c->h_img_cap || !c->h_img || out_need > c->h_out_cap || !c->h_out) && (c->h_img || c->h_out))
+    (void)hipDeviceSynchronize();   // staging buffers are freed below: nothing may still use them
   if (img_need > c->h_img_cap || !c->h_img) {
     if (c->h_img) (void)hipFree(c->h_img);
     c->h_img = nullptr;
