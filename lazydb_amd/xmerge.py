@@ -24,7 +24,7 @@ holds a block below rank r+1's), both couplings are one exchange each:
 
 Every byte of scanning, hashing, liveness, encoding, packing and copying runs in the gfx950
 kernels of liblazydb_gpu.so; this module only moves buffers between ranks. Phases are separate
-functions so one process can play every rank (tests/test_gpu_xmerge.py), and `merge_distributed`
+functions so one process can play every rank (tests/test_gpu_cross_merge.py), and `merge_distributed`
 wires them with torch.distributed.
 """
 from __future__ import annotations
