@@ -16,6 +16,22 @@ import numpy as np
 from . import _native as N
 
 
+PINNED_D2H_MIN = 1 << 20
+
+
+def d2h_bytes(t) -> bytes:
+    """Device uint8 tensor -> host bytes. Large downloads land in a pinned staging block from torch's
+    pinned-memory cache (page-locked once, never unlocked while the process runs) rather than in a
+    fresh pageable tensor that the runtime would have to lock and that is unmapped right after."""
+    import torch
+    n = int(t.numel())
+    if n < PINNED_D2H_MIN:
+        return t.cpu().numpy().tobytes()
+    h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    h.copy_(t)
+    return h.numpy().tobytes()
+
+
 class Engine:
     def __init__(self, device: int = 0):
         import torch
@@ -72,7 +88,7 @@ class Engine:
         r = N.ScanResult.from_buffer_copy(res.cpu().numpy().tobytes())
         n = min(r.n_entries, cap)
         dt = N.INDEX_TUPLE if kind == N.TUPLE_INDEX else N.ENTRY_TUPLE
-        tuples = np.frombuffer(out[: n * dt.itemsize].cpu().numpy().tobytes(), dtype=dt) if n else np.zeros(0, dt)
+        tuples = np.frombuffer(d2h_bytes(out[: n * dt.itemsize]), dtype=dt) if n else np.zeros(0, dt)
         return r, tuples
 
     # ---------------------------------------------------------------- host memory
@@ -142,7 +158,7 @@ class Engine:
         if not fetch_pos:   # leave the positions on the device (bench)
             pos = d_pos[: npos * N.MERGE_POS.itemsize]
         else:
-            pos = (np.frombuffer(d_pos[: npos * N.MERGE_POS.itemsize].cpu().numpy().tobytes(), dtype=N.MERGE_POS)
+            pos = (np.frombuffer(d2h_bytes(d_pos[: npos * N.MERGE_POS.itemsize]), dtype=N.MERGE_POS)
                    if npos else np.zeros(0, N.MERGE_POS))
         return {"rc": rc, "result": res, "stream": d_stream[: res.emit_bytes],
                 "pos": pos, "segments": segs[: min(res.n_segments, seg_cap)],
@@ -174,7 +190,7 @@ class Engine:
                 break
             seg_cap = max(seg_cap, res.n_segments)
         N.check(rc, "ldb_encode_entries_dev")
-        pos = (np.frombuffer(d_pos[: n * N.MERGE_POS.itemsize].cpu().numpy().tobytes(), dtype=N.MERGE_POS)
+        pos = (np.frombuffer(d2h_bytes(d_pos[: n * N.MERGE_POS.itemsize]), dtype=N.MERGE_POS)
                if n else np.zeros(0, N.MERGE_POS))
         return {"result": res, "stream": d_stream[: res.emit_bytes], "pos": pos,
                 "segments": segs[: res.n_segments]}

@@ -34,6 +34,7 @@ import ctypes as C
 import numpy as np
 
 from . import _native as N
+from .engine import d2h_bytes
 
 SUMMARY_PAD = 64          # zero bytes after a summary log: the replay stops at the zero sentinel
                           # (log_file.go:124-126) under both IOController bound rules
@@ -149,7 +150,7 @@ def rank_place(eng, part, earlier_sizes, active_fid: int, active_off: int, max_f
     if not fetch_pos:   # leave the positions on the device (bench)
         pos = part["pos"]
     else:
-        pos = (np.frombuffer(part["pos"].cpu().numpy().tobytes(), dtype=N.MERGE_POS) if n
+        pos = (np.frombuffer(d2h_bytes(part["pos"]), dtype=N.MERGE_POS) if n
                else np.zeros(0, N.MERGE_POS))
     return {"start": (f0, o0), "end": (res.end_fid, res.end_off), "segments": segs, "pos": pos}
 
