@@ -24,3 +24,16 @@ def golden():
             with open(os.path.join(ROOT, "tests", "golden", m["name"] + ".bin"), "rb") as f:
                 imgs[m["name"]] = f.read()
     return meta, imgs
+
+
+@pytest.fixture(scope="session")
+def gpu_engine():
+    """One engine (ldb_ctx) for every GPU test module of the session: the modules used to create and
+    destroy one each, and a fresh context after a destroyed one met a GPU memory fault in its first
+    test."""
+    import torch
+    from lazydb_amd import Engine
+    e = Engine(0)
+    yield e
+    torch.cuda.synchronize()
+    e.close()

@@ -15,14 +15,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def eng():
-    import torch
-    from lazydb_amd import Engine
-    torch.cuda.synchronize()   # a fault left by an earlier module surfaces here, not inside a case
-    e = Engine(0)
-    torch.cuda.synchronize()
-    yield e
-    e.close()
+def eng(gpu_engine):
+    return gpu_engine
 
 
 def to_dev(img):

@@ -15,11 +15,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def eng():
-    from lazydb_amd import Engine
-    e = Engine(0)
-    yield e
-    e.close()
+def eng(gpu_engine):
+    return gpu_engine
 
 
 def to_dev(img):
