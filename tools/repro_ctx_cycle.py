@@ -25,6 +25,15 @@ def use(eng, mode):
         files, kw = MC.small_cases()["gen1"]
         d = [(torch.from_numpy(np.ascontiguousarray(f[0])).to("cuda:0"), f[1], f[2]) for f in files]
         eng.merge_dev(d, kw["active_fid"], kw["active_off"], kw["max_file_size"], kw["now"])
+    elif mode == "bigscan":   # multi-GiB workspace, as the parity module's 4.5 GiB case
+        img, n, end = coracle.gen_log(9 << 29, 10, ksize=64, vsize=256)
+        res, tup = eng.scan_dev(torch.from_numpy(img).to("cuda:0"))
+        assert res.n_entries == n
+    elif mode == "crcmerge":   # a merge that stops at a file with a bad CRC
+        files, kw = MC.small_cases()["crc_corrupt"]
+        d = [(torch.from_numpy(np.ascontiguousarray(f[0])).to("cuda:0"), f[1], f[2]) for f in files]
+        out = eng.merge_dev(d, kw["active_fid"], kw["active_off"], kw["max_file_size"], kw["now"])
+        assert out["result"].bad_file == 1
     elif mode == "encode":
         files, kw = MC.small_cases()["gen1"]
         d = [(torch.from_numpy(np.ascontiguousarray(f[0])).to("cuda:0"), f[1], False) for f in files]
