@@ -1,14 +1,19 @@
 """Benchmark: device-resident LazyDB log decode + CRC32 on MI355X.
 
 One "step" = one full replay scan (ReadLogEntry chain of index.go:84-95: decode,
-CRC-32 verify, index tuples) of one log-file image already resident in HBM.
-Default workload = BASELINE.json configs[1]: one 1 GiB log file of 64-B key /
-256-B value entries (FileIO bound) -> 3 234 162 entries, 1 073 741 784 valid bytes.
+CRC-32 verify, index tuples) of one log-file image already resident in HBM, per GPU.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-one independent log file per rank (weak scaling, BASELINE config 4 shape),
-no collective on the scan path; after the timed scans the index tuples are
-gathered to rank 0 with one RCCL gather and that is reported separately.
+Default workload, at every N = BASELINE config 4's per-GPU file: one 4 GiB log file of
+64-B key / 256-B value entries per GPU (seed 10 + rank, FileIO bound) -> 12 936 648
+entries, 4 294 967 136 valid bytes each. The same per-GPU file at N = 1, 2, 4, 8 makes
+the 1 -> N curve comparable (weak scaling: independent files, index.go:68-95).
+At N = 1 the line also carries `legs`: BASELINE config 2 (1 GiB) and config 3
+(8 GiB, Zipf values), each timed the same way (GiB/s, k_scan_main ms, roofline frac).
+
+Multi-GPU: `python bench.py --gpus N` spawns N rank processes itself (before anything
+touches the GPU); `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
+works as well. No collective on the scan path; after the timed scans the index tuples
+are gathered to rank 0 with one RCCL gather, reported separately as `gather`.
 
 Prints ONE JSON line on rank 0.
 """
@@ -33,7 +38,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
+    ap.add_argument("--config", type=int, default=4, choices=[1, 2, 3, 4, 5],
                     help="BASELINE config: 1 = 500K entries 64/256 in a 512 MiB preallocated file (reopen); 2 = 1 GiB fixed 64/256; 3 = 8 GiB Zipf values; 4 = 4 GiB per GPU; "
                          "5 = merge/GC of 16 x 256 MiB files, half the records stale (a separate bench line)")
     ap.add_argument("--io", type=int, default=0, help="0 FileIO bound rule, 1 Mmap")
@@ -47,7 +52,65 @@ def parse():
     ap.add_argument("--xsim", type=int, default=0,
                     help="config 5 --xmerge: play K ranks in this one process and time each rank's phases")
     ap.add_argument("--e2e", type=int, default=3, help="iterations of the PCIe-inclusive host-API leg (0: skip)")
+    ap.add_argument("--legs", default="2,3",
+                    help="extra single-GPU configs timed after the main line at N = 1 (comma list; '' = none)")
+    ap.add_argument("--leg-steps", type=int, default=20)
+    ap.add_argument("--rehearse-launch", action="store_true",
+                    help="launcher self-test without a GPU: ranks rendezvous over gloo and report")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (children, not
+    an exec: this process never touches the GPU), one per GPU, with the torch.distributed env a
+    torchrun launch would give them. Rank 0 prints the JSON line. Returns the exit code."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(args.gpus),
+                   RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(args.gpus))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c != 0 and rc == 0:
+            rc = c
+            for q in procs:   # one rank failed: the others would wait forever in a collective
+                if q.poll() is None:
+                    q.kill()
+    return rc
+
+
+def rehearse_launch(args):
+    """Launcher self-test (tests/test_bench_launch.py): every rank joins a gloo group and rank 0
+    prints the bench's JSON keys that depend on the launch."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([rank], dtype=torch.int64)
+    seen = [torch.zeros_like(t) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(seen, t)
+    else:
+        seen = [t]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_seen": [int(x.item()) for x in seen],
+                          "local_ranks_distinct": True, "config": {"workload": "launcher rehearsal (no GPU)"}}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def make_image(cfg: int, rank: int):
@@ -70,14 +133,31 @@ def make_image(cfg: int, rank: int):
     return img, n, end, wl
 
 
+def _host_threads() -> int:
+    """Host threads this process may use: its CPU affinity, capped by the box's share when the
+    environment states one (OMP_NUM_THREADS is set to the per-GPU CPU share on the GPU boxes)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(n, 1)
+
+
 def cpu_baseline(img, end, sample_mib: int):
-    """The oracle's faithful port of the reference replay (pread per header and per k+v, heap
-    buffers, CRC verify, EncodeEntry re-encode for the size), single thread, on a bounded
-    sample: the first `sample_mib` MiB of the same log written to a file."""
+    """CPU baselines on a bounded sample (the first `sample_mib` MiB of the same log, cut at an entry
+    boundary), BASELINE.md's two restatements of the reference replay:
+    * faithful port (the `value`): pread per header and per k+v, heap buffers, CRC verify, a second
+      CRC for the EncodeEntry size (log_file.go:116-145, index.go:15-26), one thread, as index.go
+      replays one file at a time per value type;
+    * optimized port: the in-memory scan with carry-less-multiply CRC folding (Go amd64
+      hash/crc32's algorithm class), on one thread and on every host thread this process may use,
+      one file per thread (each thread scans its own pass over the sample)."""
+    import ctypes as C
+    import threading
     from oracle import coracle
     n_bytes = min(end, sample_mib << 20)
     # cut the sample at an entry boundary: scan the prefix with the in-memory port
-    res, tup = coracle.scan(img[: n_bytes + 64])
+    res, tup = coracle.scan(img[: n_bytes + 64], cap=0)
     cut = int(res.end_off) if res.end_off <= n_bytes else n_bytes
     with tempfile.NamedTemporaryFile(dir="/dev/shm" if os.path.isdir("/dev/shm") else None, delete=True) as f:
         f.write(img[:cut].tobytes())
@@ -89,14 +169,37 @@ def cpu_baseline(img, end, sample_mib: int):
             dt = time.perf_counter() - t0
         finally:
             os.close(fd)
+    sample = img[:cut]
+    L = coracle.lib()
+
+    def one_pass(out):
+        rr = coracle.ScanResult()
+        L.ldbo_scan(sample.ctypes.data, cut, 0, 1, 0, None, 0, C.byref(rr))   # ctypes drops the GIL
+        out.append(rr)
+
     t0 = time.perf_counter()
-    r2, _ = coracle.scan(img[:cut], 0, 1, cap=0)
-    dt2 = time.perf_counter() - t0
+    got = []
+    one_pass(got)
+    dt1 = time.perf_counter() - t0
+    nt = _host_threads()
+    got = []
+    ths = [threading.Thread(target=one_pass, args=(got,)) for _ in range(nt)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dtn = time.perf_counter() - t0
+    assert len(got) == nt and all(int(g.end_off) == cut for g in got)
     return {"value": round(r.end_off / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {cut} B ({r.n_entries} entries) of the same log, faithful pread/alloc/2xCRC replay port, "
                       f"1 thread",
             "mentries_per_s": round(r.n_entries / dt / 1e6, 3),
-            "optimized_mmap_port_gibs": round(r2.end_off / dt2 / 2**30, 3),
+            "optimized_port": {"GiB_per_s": round(cut / dt1 / 2**30, 3), "cores": 1,
+                               "mentries_per_s": round(r.n_entries / dt1 / 1e6, 3)},
+            "optimized_port_all_cores": {"GiB_per_s": round(nt * cut / dtn / 2**30, 3), "cores": nt,
+                                         "mentries_per_s": round(nt * r.n_entries / dtn / 1e6, 3),
+                                         "sample": f"{nt} threads, one {cut}-B file pass each"},
             "host_cpu": _cpu_model(), "host_nproc": os.cpu_count()}
 
 
@@ -347,17 +450,107 @@ def main_xmerge(args):
         dist.destroy_process_group()
 
 
+class Resident:
+    """One log-file image in HBM with its output tuple array and result slot."""
+
+    def __init__(self, eng, img, cap, kind, dev):
+        import torch
+        self.d = torch.from_numpy(img).to(dev)
+        self.cap = cap
+        self.out = eng.alloc_out(cap, kind)
+        self.res = eng.alloc_result()
+
+
+def timed_scans(eng, S, fid, args, steps, world, stream):
+    """K device-resident scans of one image between barrier + synchronize, with HIP events around
+    every launch on the scan stream. Returns (wall seconds, avg k_scan_main ms, avg pipeline ms)."""
+    import torch
+    import torch.distributed as dist
+
+    def step():
+        eng.scan_dev_async(S.d, fid=fid, io_type=args.io, kind=args.kind, out=S.out, cap=S.cap, result=S.res,
+                           stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.timing(1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    main_ms, total_ms, _ = eng.timing(0)
+    return t, main_ms, total_ms
+
+
+def prepare(eng, cfg, rank, args, dev, verify: bool):
+    """Synthetic image of config `cfg` on the device plus its output buffers; one scan checked
+    against the oracle before anything is timed. Returns (host image, device image, result, verified,
+    workload text)."""
+    import torch
+    from lazydb_amd import _native as N
+    img, n_expect, end_expect, workload = make_image(cfg, rank)
+    cap = n_expect + 1024
+    S = Resident(eng, img, cap, args.kind, dev)
+    eng.reserve(img.size)
+    stream = torch.cuda.current_stream(dev)
+    eng.scan_dev_async(S.d, fid=1 + rank, io_type=args.io, kind=args.kind, out=S.out, cap=cap, result=S.res,
+                       stream=stream)
+    torch.cuda.synchronize()
+    r = N.ScanResult.from_buffer_copy(S.res.cpu().numpy().tobytes())
+    verified = None
+    if verify:
+        from oracle import coracle   # checker only
+        ref, rt = coracle.scan(img, args.io, fid=1 + rank, tuple_kind=args.kind, cap=cap)
+        n = int(min(r.n_entries, cap))
+        got = S.out[: n * (16 if args.kind == 0 else 48)].cpu().numpy().tobytes()
+        verified = (r.status, r.end_off, r.n_entries) == (ref.status, ref.end_off, ref.n_entries) and \
+            got == rt.tobytes()
+        del rt
+    return img, S, r, verified, workload, end_expect
+
+
+def run_leg(eng, cfg, args, dev):
+    """One extra single-GPU config (N = 1 only): the same timed scans as the main line."""
+    import torch
+    img, S, r, verified, workload, _ = prepare(eng, cfg, 0, args, dev, not args.no_verify)
+    t, main_ms, total_ms = timed_scans(eng, S, 1, args, args.leg_steps, 1, torch.cuda.current_stream(dev))
+    step = t / args.leg_steps
+    achieved = int(r.end_off) / (main_ms * 1e-3) / 1e9 if main_ms > 0 else None
+    leg = {"config": cfg, "workload": workload, "file_bytes": int(img.size), "bytes_scanned": int(r.end_off),
+           "entries": int(r.n_entries), "steps": args.leg_steps, "ms_per_step": round(step * 1e3, 4),
+           "GiB_per_s": round(int(r.end_off) / step / 2**30, 3),
+           "mentries_per_s": round(int(r.n_entries) / step / 1e6, 2),
+           "k_scan_main_ms": round(main_ms, 4), "pipeline_ms": round(total_ms, 4),
+           "roofline_frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
+           "status": int(r.status), "fast_regions": int(r.n_fast), "regions": int(r.n_regions),
+           "verified_vs_oracle": verified}
+    del S, img
+    torch.cuda.empty_cache()
+    return leg
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.rehearse_launch:
+        return rehearse_launch(args)
     if args.config == 5 and (args.xmerge or args.xsim):
         return main_xmerge(args)
     if args.config == 5:
         return main_merge(args)
-    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = init_dist(world, local)
@@ -366,61 +559,24 @@ def main():
     from lazydb_amd import Engine
     from lazydb_amd import _native as N
 
-    img, n_expect, end_expect, workload = make_image(args.config, rank)
-    d_img = torch.from_numpy(img).to(dev)
     eng = Engine(local)
-    eng.reserve(img.size)
-    cap = n_expect + 1024
-    out = eng.alloc_out(cap, args.kind)
-    res_t = eng.alloc_result()
+    img, S, r, verified, workload, end_expect = prepare(eng, args.config, rank, args, dev, not args.no_verify)
     stream = torch.cuda.current_stream(dev)
-
-    def step():
-        eng.scan_dev_async(d_img, fid=1 + rank, io_type=args.io, kind=args.kind, out=out, cap=cap, result=res_t,
-                           stream=stream)
-
-    # one scan, checked against the oracle before anything is timed
-    step()
-    torch.cuda.synchronize()
-    r = N.ScanResult.from_buffer_copy(res_t.cpu().numpy().tobytes())
-    verified = None
-    if not args.no_verify:
-        from oracle import coracle
-        ref, rt = coracle.scan(img, args.io, fid=1 + rank, tuple_kind=args.kind)
-        n = int(min(r.n_entries, cap))
-        got = out[: n * (16 if args.kind == 0 else 48)].cpu().numpy().tobytes()
-        verified = (r.status, r.end_off, r.n_entries) == (ref.status, ref.end_off, ref.n_entries) and \
-            got == rt.tobytes()
-        del rt
-    for _ in range(args.warmup):
-        step()
-    # timed region: K scans; HIP events around every launch on the scan stream (recorded, not
-    # waited on) give the per-kernel device time over the same region
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    eng.timing(1)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t = time.perf_counter() - t0
-    main_ms, total_ms, nt = eng.timing(0)
+    t, main_ms, total_ms = timed_scans(eng, S, 1 + rank, args, args.steps, world, stream)
     # practical HBM-read ceiling on this box: a read-only reduction over the same image, after the
     # timed region
-    ceiling = eng.read_ceiling(d_img, 20) if rank == 0 and hasattr(N.lib(), "ldb_read_ceiling") else None
+    ceiling = eng.read_ceiling(S.d, 20) if rank == 0 else None
 
     bytes_scanned = int(r.end_off)
     entries = int(r.n_entries)
     from lazydb_amd import multi
     t_max = multi.max_over_ranks(t, dev)
     tot_bytes, tot_entries = multi.sum_over_ranks([bytes_scanned, entries], dev)
+    all_ok = multi.sum_over_ranks([1 if verified else 0], dev)[0] if verified is not None else None
     gather = None
     if world > 1 and args.gather:
         # the north star's single exchange: every rank's index tuples to rank 0 over RCCL/xGMI
-        mine = out[: entries * (16 if args.kind == 0 else 48)]
+        mine = S.out[: entries * (16 if args.kind == 0 else 48)]
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
@@ -429,8 +585,11 @@ def main():
         gt = multi.max_over_ranks(time.perf_counter() - g0, dev)
         if rank == 0:
             tot = sum(int(x.numel()) for x in got)
-            gather = {"bytes_to_rank0": tot, "ms": round(gt * 1e3, 3), "GB_per_s": round(tot / gt / 1e9, 2)}
+            gather = {"bytes_to_rank0": tot, "ms": round(gt * 1e3, 3), "GB_per_s": round(tot / gt / 1e9, 2),
+                      "backend": dist.get_backend()}
+            del got
     e2e = None
+    cap = S.cap
     if world == 1 and args.e2e > 0:
         # PCIe-inclusive rate of the host-pointer API (ldb_scan_file: H2D of the image from pageable
         # host memory, scan, D2H of the tuples) -- recorded for DESIGN.md, never the bench value
@@ -442,23 +601,32 @@ def main():
         e2e = {"GiB_per_s": round(int(res_h.end_off) / te / 2**30, 3), "ms": round(te * 1e3, 2),
                "path": "ldb_scan_file: pageable host image -> H2D -> scan -> D2H tuples",
                "status_matches": int(res_h.status) == int(r.status) and int(res_h.n_entries) == entries}
-        if hasattr(N.lib(), "ldb_host_register"):
-            # the same with the image page-locked once (ldb_host_register, as a caller holding an mmap'd
-            # file would): the copy runs as direct DMA
-            eng.host_register(img)
-            try:
-                eng.scan_host(img, fid=1, io_type=args.io, kind=args.kind, cap=cap)
-                t0e = time.perf_counter()
-                for _ in range(args.e2e):
-                    res_h, _ = eng.scan_host(img, fid=1, io_type=args.io, kind=args.kind, cap=cap)
-                te = (time.perf_counter() - t0e) / args.e2e
-            finally:
-                eng.host_unregister(img)
-            e2e["registered"] = {"GiB_per_s": round(int(res_h.end_off) / te / 2**30, 3), "ms": round(te * 1e3, 2),
-                                 "status_matches": int(res_h.n_entries) == entries}
+        # the same with the image page-locked once (ldb_host_register, as a caller holding an mmap'd
+        # file would): the copy runs as direct DMA
+        eng.host_register(img)
+        try:
+            eng.scan_host(img, fid=1, io_type=args.io, kind=args.kind, cap=cap)
+            t0e = time.perf_counter()
+            for _ in range(args.e2e):
+                res_h, _ = eng.scan_host(img, fid=1, io_type=args.io, kind=args.kind, cap=cap)
+            te = (time.perf_counter() - t0e) / args.e2e
+        finally:
+            eng.host_unregister(img)
+        e2e["registered"] = {"GiB_per_s": round(int(res_h.end_off) / te / 2**30, 3), "ms": round(te * 1e3, 2),
+                             "status_matches": int(res_h.n_entries) == entries}
     ms_step = t_max / args.steps * 1e3
     value = tot_bytes / (t_max / args.steps) / 2**30
     traffic, traffic_src = _pmc_traffic(args)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(img, end_expect, args.cpu_sample_mib)
+    legs = []
+    if world == 1 and args.legs:
+        del S
+        torch.cuda.empty_cache()
+        for cfg in [int(x) for x in args.legs.split(",") if x.strip()]:
+            if cfg != args.config and cfg in (1, 2, 3, 4):
+                legs.append(run_leg(eng, cfg, args, dev))
     if rank == 0:
         achieved = bytes_scanned / (main_ms * 1e-3) / 1e9 if main_ms > 0 else None
         line = {
@@ -474,8 +642,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (LazyDB writeLogEntry format, splitmix64 36-char alphabet values)",
-            "config": {"workload": workload, "file_bytes": int(img.size), "bytes_scanned_per_file": bytes_scanned,
-                       "entries_per_file": entries, "io_type": "FileIO" if args.io == 0 else "Mmap",
+            "config": {"workload": workload, "baseline_config": args.config, "file_bytes": int(img.size),
+                       "bytes_scanned_per_file": bytes_scanned, "entries_per_file": entries,
+                       "io_type": "FileIO" if args.io == 0 else "Mmap",
                        "tuple_kind": "index16" if args.kind == 0 else "entry48",
                        "parallelism": f"one file per GPU x{world}"},
             "mentries_per_s": round(tot_entries / (t_max / args.steps) / 1e6, 2),
@@ -496,7 +665,7 @@ def main():
                                       "GB_per_s": round(ceiling, 1) if ceiling else None,
                                       "frac": round(achieved / ceiling, 4) if achieved and ceiling else None},
             },
-            "verified_vs_oracle": verified,
+            "verified_vs_oracle": verified if world == 1 or all_ok is None else bool(all_ok == world),
             "status": int(r.status),
             "repairs": int(r.n_repairs),
             "fast_regions": int(r.n_fast),
@@ -506,9 +675,11 @@ def main():
             line["gather"] = gather
         if e2e:
             line["e2e_host"] = e2e
-        if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(img, end_expect, args.cpu_sample_mib)
-        print(json.dumps(line))
+        if legs:
+            line["legs"] = legs
+        if cpu:
+            line["cpu_baseline"] = cpu
+        print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()

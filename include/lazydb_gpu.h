@@ -42,7 +42,8 @@ typedef enum ldb_status {
   LDB_ERR_CAPACITY = -3, /* output array too small (n_entries still reports the full count) */
   LDB_ERR_ARG = -4,      /* bad argument */
   LDB_ERR_HIP = -5,      /* HIP runtime error */
-  LDB_ERR_NOMEM = -6     /* device workspace allocation failed */
+  LDB_ERR_NOMEM = -6,    /* device workspace allocation failed */
+  LDB_ERR_INTERNAL = -7  /* a device-side bounds guard fired; results must not be used (never expected) */
 } ldb_status;
 
 /* IOController kind of the LogFile being scanned (logfile/log_file.go:35-41).

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("LAZYDB_GPU_LIB") or os.path.join(HERE, "_lib", "libla
 
 LDB_OK = 0
 EOF_WINDOW, EOF_SENTINEL, EOF_KV = 1, 2, 3
-ERR_CRC, ERR_MALFORMED, ERR_CAPACITY, ERR_ARG, ERR_HIP, ERR_NOMEM = -1, -2, -3, -4, -5, -6
+ERR_CRC, ERR_MALFORMED, ERR_CAPACITY, ERR_ARG, ERR_HIP, ERR_NOMEM, ERR_INTERNAL = -1, -2, -3, -4, -5, -6, -7
 FILEIO, MMAP = 0, 1
 TUPLE_INDEX, TUPLE_ENTRY = 0, 1
 

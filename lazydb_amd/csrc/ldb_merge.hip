@@ -901,7 +901,13 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
     rc = ldb_scan_file_dev(odd ? m->aux : ctx, files[i].d_image, files[i].len, files[i].fid, io_type,
                            LDB_TUPLE_INDEX, m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i,
                            odd ? m->aux_s : s);
-    if (rc != LDB_OK) return rc;
+    if (rc != LDB_OK) {
+      // scans already queued on either stream read the caller's images and write m->recs: drain
+      // them before the caller can free or reuse anything
+      if (nf > 1) (void)hipStreamSynchronize(m->aux_s);
+      (void)hipStreamSynchronize(s);
+      return rc;
+    }
   }
   if (nf > 1) {
     MHIP(hipEventRecord(m->join, m->aux_s));

@@ -258,10 +258,9 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   copy_tables(tab, p.gtab);
-  if (blockIdx.x == 0) {  // control words of the later stages (stream-ordered after this kernel)
-    if (threadIdx.x < 3) p.ctr[threadIdx.x] = 0;   // ctr[3] (fast regions) is counted here: k_serial zeroes it
-    if (threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
-  }
+  // ctr[] was zeroed by the hipMemsetAsync that opens every pipeline (enqueue_scan); the terminal
+  // words start at "none" (read only by the later kernels, stream-ordered after this one)
+  if (blockIdx.x == 0 && threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -375,7 +374,11 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
         GpuWave::sync();
         if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
       }
-      if (lane == 0) p.defer[atomicAdd(&p.ctr[4], 1u)] = (uint32_t)r;
+      if (lane == 0) {
+        const uint32_t di = atomicAdd(&p.ctr[4], 1u);
+        if (di < p.nreg) p.defer[di] = (uint32_t)r;   // at most one deferral per region
+        else atomicOr(&p.ctr[5], 1u);                 // unreachable: reported as LDB_ERR_INTERNAL
+      }
       st.on = 0;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
 // any other region. Staging is synchronous (rare regions).
 constexpr int kFbWaves = 4;
 __global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p) {
-  const uint32_t n = p.ctr[4];
+  const uint32_t n = (uint32_t)min((uint64_t)p.ctr[4], p.nreg);
   if ((uint64_t)blockIdx.x * kFbWaves >= n) return;   // no deferred region for this block
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -440,14 +443,15 @@ __global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p) {
 __global__ void k_link(Pipe p) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= p.nreg) return;
+  // fail_src holds nreg + 1 entries: one per region plus region 0's "does not start at 0"
   bool bad = link_broken(p, r);
   if (bad) {
     const uint32_t i = atomicAdd(&p.ctr[0], 1u);
-    p.fail_src[i] = (int64_t)r;
+    if (i <= p.nreg) p.fail_src[i] = (int64_t)r; else atomicOr(&p.ctr[5], 1u);
   }
   if (r == 0 && p.rs[0].start != 0) {
     const uint32_t i = atomicAdd(&p.ctr[0], 1u);
-    p.fail_src[i] = -1;
+    if (i <= p.nreg) p.fail_src[i] = -1; else atomicOr(&p.ctr[5], 1u);
   }
 }
 
@@ -466,7 +470,7 @@ struct CohRd {
 };
 
 __global__ __launch_bounds__(64) void k_repair(Pipe p) {
-  const uint32_t nfail = p.ctr[0];
+  const uint32_t nfail = (uint32_t)min((uint64_t)p.ctr[0], p.nreg + 1);
   if (nfail == 0) return;
   // CRC tables in a static LDS array: its address is a link-time constant, so every table read
   // folds the table base into the ds_read offset field
@@ -648,6 +652,7 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
     res.n_fast = p.ctr[3];
     res.reserved_ = 0;
     if (n > p.cap) res.status = LDB_ERR_CAPACITY;
+    if (p.ctr[5]) res.status = LDB_ERR_INTERNAL;   // a device-side index guard fired (never expected)
     if (p.ctr[1]) res.status = kOverflow;  // k_serial redoes the scan
     *p.result = res;
   }
@@ -671,11 +676,7 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
 // One lane walks the chain exactly like index.go:84-95 (global memory, byte-wise CRC).
 __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   if (threadIdx.x != 0) return;
-  if (only_on_overflow && !p.ctr[1]) {
-    p.ctr[3] = 0;   // last kernel of the pipeline: leave the counters k_scan_main adds to zeroed
-    p.ctr[4] = 0;
-    return;
-  }
+  if (only_on_overflow && !p.ctr[1]) return;
   struct G {
     const uint8_t* q;
     __device__ uint32_t operator()(int i) const { return q[i]; }
@@ -717,8 +718,6 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   res.n_fast = 0;
   res.reserved_ = 0;
   *p.result = res;
-  p.ctr[3] = 0;
-  p.ctr[4] = 0;
 }
 
 // Read-only reduction over the image (ldb_read_ceiling): four 16-B loads in flight per thread.
@@ -753,6 +752,13 @@ struct ldb_ctx {
   uint32_t* d_gsh = nullptr;   // kGsWords register-shift tables (k_combine)
   uint8_t* ws = nullptr;       // workspace
   uint64_t ws_bytes = 0;
+  // Workspace fence: the event recorded after the last pipeline enqueued on this context, and the
+  // stream it went to. A pipeline enqueued on a different stream first waits on it, so two streams
+  // never share the workspace at once (ldb_scan_file_dev only enqueues: the previous scan may still
+  // be running when the next call arrives).
+  hipEvent_t ws_ev = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_ev_live = false;
   // kernel timing: one event triple per timed launch, recorded without host synchronisation and
   // resolved when the timing is queried (or when the pool is full)
   struct EvTriple { hipEvent_t e0, e1, e2; };
@@ -809,7 +815,8 @@ WsLayout layout(uint64_t len) {
     o += (bytes + 255) & ~255ull;
     return at;
   };
-  // control words first (one memset covers ctr, tpos, blk)
+  // control words: ctr (8 x u32, zeroed by a hipMemsetAsync at the start of every pipeline), then
+  // tpos (2 x u64, set by k_scan_main's first workgroup); take() rounds each field to 256 B
   L.o_ctr = take(32);
   L.o_tpos = take(16);
   L.o_blk = take(8 * L.nblk);
@@ -832,8 +839,8 @@ int ensure_ws(ldb_ctx* c, uint64_t bytes) {
   }
   c->ws = nullptr;
   c->ws_bytes = 0;
+  c->ws_ev_live = false;   // nothing in flight uses the new workspace
   if (hipMalloc(&c->ws, bytes) != hipSuccess) return LDB_ERR_NOMEM;
-  if (hipMemset(c->ws, 0, 256) != hipSuccess) return LDB_ERR_HIP;   // control words (layout: ctr first)
   c->ws_bytes = bytes;
   return LDB_OK;
 }
@@ -864,6 +871,15 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   return p;
 }
 
+// Record the end of the pipeline just enqueued on `s` (see ldb_ctx::ws_ev).
+int fence_ws(ldb_ctx* c, hipStream_t s) {
+  if (!c->ws_ev && hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess) return LDB_ERR_HIP;
+  LDB_HIP(hipEventRecord(c->ws_ev, s));
+  c->ws_stream = s;
+  c->ws_ev_live = true;
+  return LDB_OK;
+}
+
 int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, int io, int kind, void* d_out,
                  uint64_t cap, ldb_scan_result* d_res, hipStream_t s, bool serial) {
   if (!c || !d_res || (io != LDB_IO_FILEIO && io != LDB_IO_MMAP) ||
@@ -876,12 +892,16 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   int rc = ensure_ws(c, L.total);
   if (rc != LDB_OK) return rc;
   const Pipe p = make_pipe(c, L, d_img, len, fid, io, kind, d_out, cap, d_res);
+  // the workspace is free once the last pipeline enqueued on another stream has finished
+  if (c->ws_ev_live && c->ws_stream != s) LDB_HIP(hipStreamWaitEvent(s, c->ws_ev, 0));
+  // every pipeline starts from zeroed control words, in stream order: nothing depends on how the
+  // previous pipeline on this workspace ended, or on what a fresh allocation held
+  LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
   if (serial || len < (uint64_t)kMaxHeader) {
-    // control words for k_serial (the parallel pipeline has k_scan_main initialise them)
-    LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
     LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 0);
-    return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+    LDB_HIP(hipGetLastError());
+    return fence_ws(c, s);
   }
   const ldb_ctx::EvTriple* ev = nullptr;
   if (c->timing) {
@@ -915,7 +935,8 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   hipLaunchKernelGGL(k_compact, dim3((unsigned)L.nblk), dim3(kBlkRegions), 0, s, p);
   hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 1);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
-  return hipGetLastError() == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+  LDB_HIP(hipGetLastError());
+  return fence_ws(c, s);
 }
 
 }  // namespace
@@ -936,6 +957,7 @@ const char* ldb_status_str(int s) {
     case LDB_ERR_ARG: return "invalid argument";
     case LDB_ERR_HIP: return "hip runtime error";
     case LDB_ERR_NOMEM: return "out of device memory";
+    case LDB_ERR_INTERNAL: return "internal error (device-side index guard)";
     default: return "unknown status";
   }
 }
@@ -992,6 +1014,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->h_res) (void)hipFree(c->h_res);
   if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
   if (c->merge) ldb_merge_release_(c->merge);
+  if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
   for (const ldb_ctx::EvTriple& t : c->evs) {
     (void)hipEventDestroy(t.e0);
     (void)hipEventDestroy(t.e1);

@@ -30,7 +30,94 @@ static void crc_init_tables(void) {
   crc_ready = 1;
 }
 
+/* Carry-less-multiply folding (PCLMULQDQ), the algorithm class of Go's amd64 hash/crc32 IEEE path
+ * for inputs of 64 bytes and more (ieeeCLMUL): four 128-bit lanes folded by x^512, then by x^128,
+ * reduced to 64 bits and Barrett-reduced to the 32-bit register (Gopal et al., "Fast CRC computation
+ * for generic polynomials using PCLMULQDQ", bit-reflected constants of the IEEE polynomial).
+ * Operates on the raw register like ldbo_crc32_reg; n >= 64, processes n & ~15 bytes. */
+#if defined(__x86_64__)
+#include <immintrin.h>
+__attribute__((target("pclmul,sse4.1"))) static uint32_t crc_clmul(uint32_t crc, const uint8_t* buf, size_t len) {
+  const __m128i k1k2 = _mm_set_epi64x(0x01c6e41596ll, 0x0154442bd4ll);
+  const __m128i k3k4 = _mm_set_epi64x(0x00ccaa009ell, 0x01751997d0ll);
+  const __m128i k5k0 = _mm_set_epi64x(0, 0x0163cd6124ll);
+  const __m128i poly = _mm_set_epi64x(0x01f7011641ll, 0x01db710641ll);
+  __m128i x0, x1, x2, x3, x4, x5, x6, x7, x8;
+  x1 = _mm_loadu_si128((const __m128i*)(buf + 0x00));
+  x2 = _mm_loadu_si128((const __m128i*)(buf + 0x10));
+  x3 = _mm_loadu_si128((const __m128i*)(buf + 0x20));
+  x4 = _mm_loadu_si128((const __m128i*)(buf + 0x30));
+  x1 = _mm_xor_si128(x1, _mm_cvtsi32_si128((int)crc));
+  x0 = k1k2;
+  buf += 64;
+  len -= 64;
+  while (len >= 64) {   /* fold 4 x 128 bits by x^512 */
+    x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+    x6 = _mm_clmulepi64_si128(x2, x0, 0x00);
+    x7 = _mm_clmulepi64_si128(x3, x0, 0x00);
+    x8 = _mm_clmulepi64_si128(x4, x0, 0x00);
+    x1 = _mm_clmulepi64_si128(x1, x0, 0x11);
+    x2 = _mm_clmulepi64_si128(x2, x0, 0x11);
+    x3 = _mm_clmulepi64_si128(x3, x0, 0x11);
+    x4 = _mm_clmulepi64_si128(x4, x0, 0x11);
+    x1 = _mm_xor_si128(_mm_xor_si128(x1, x5), _mm_loadu_si128((const __m128i*)(buf + 0x00)));
+    x2 = _mm_xor_si128(_mm_xor_si128(x2, x6), _mm_loadu_si128((const __m128i*)(buf + 0x10)));
+    x3 = _mm_xor_si128(_mm_xor_si128(x3, x7), _mm_loadu_si128((const __m128i*)(buf + 0x20)));
+    x4 = _mm_xor_si128(_mm_xor_si128(x4, x8), _mm_loadu_si128((const __m128i*)(buf + 0x30)));
+    buf += 64;
+    len -= 64;
+  }
+  x0 = k3k4;   /* fold the four lanes into one by x^128 */
+  x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+  x1 = _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x1, x0, 0x11), x2), x5);
+  x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+  x1 = _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x1, x0, 0x11), x3), x5);
+  x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+  x1 = _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x1, x0, 0x11), x4), x5);
+  while (len >= 16) {
+    x2 = _mm_loadu_si128((const __m128i*)buf);
+    x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+    x1 = _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x1, x0, 0x11), x2), x5);
+    buf += 16;
+    len -= 16;
+  }
+  /* 128 -> 64 bits */
+  x2 = _mm_clmulepi64_si128(x1, x0, 0x10);
+  x3 = _mm_setr_epi32(~0, 0, ~0, 0);
+  x1 = _mm_xor_si128(_mm_srli_si128(x1, 8), x2);
+  x0 = k5k0;
+  x2 = _mm_srli_si128(x1, 4);
+  x1 = _mm_and_si128(x1, x3);
+  x1 = _mm_xor_si128(_mm_clmulepi64_si128(x1, x0, 0x00), x2);
+  /* Barrett reduction to 32 bits */
+  x0 = poly;
+  x2 = _mm_and_si128(x1, x3);
+  x2 = _mm_clmulepi64_si128(x2, x0, 0x10);
+  x2 = _mm_and_si128(x2, x3);
+  x2 = _mm_clmulepi64_si128(x2, x0, 0x00);
+  x1 = _mm_xor_si128(x1, x2);
+  return (uint32_t)_mm_extract_epi32(x1, 1);
+}
+static int clmul_ok = -1;
+#endif
+
+/* Slicing-by-8 only (the fold path off): the independent second formulation the tests compare. */
+uint32_t ldbo_crc32_reg_tables(uint32_t c, const uint8_t* p, size_t n);
+
 uint32_t ldbo_crc32_reg(uint32_t c, const uint8_t* p, size_t n) {
+#if defined(__x86_64__)
+  if (clmul_ok < 0) clmul_ok = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+  if (clmul_ok && n >= 64) {
+    const size_t m = n & ~(size_t)15;
+    c = crc_clmul(c, p, m);
+    p += m;
+    n -= m;
+  }
+#endif
+  return ldbo_crc32_reg_tables(c, p, n);
+}
+
+uint32_t ldbo_crc32_reg_tables(uint32_t c, const uint8_t* p, size_t n) {
   crc_init_tables();
   while (n && ((uintptr_t)p & 7)) {
     c = crc_tab[0][(c ^ *p++) & 0xff] ^ (c >> 8);

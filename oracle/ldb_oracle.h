@@ -47,6 +47,8 @@ typedef struct ldbo_header {
 uint32_t ldbo_crc32_update(uint32_t crc, const uint8_t* p, size_t n);
 /* Raw reflected register update (no pre/post inversion): the GPU engine's unit. */
 uint32_t ldbo_crc32_reg(uint32_t reg, const uint8_t* p, size_t n);
+/* the same register update by slicing-by-8 tables only (no carry-less folding): a second formulation */
+uint32_t ldbo_crc32_reg_tables(uint32_t reg, const uint8_t* p, size_t n);
 
 /* encoding/binary */
 int ldbo_uvarint(const uint8_t* buf, size_t len, uint64_t* x);

@@ -26,11 +26,11 @@ def golden():
     return meta, imgs
 
 
-@pytest.fixture(scope="session")
+@pytest.fixture(scope="module")
 def gpu_engine():
-    """One engine (ldb_ctx) for every GPU test module of the session: the modules used to create and
-    destroy one each, and a fresh context after a destroyed one met a GPU memory fault in its first
-    test."""
+    """A fresh engine (ldb_ctx) per GPU test module, destroyed at module end: the suite creates and
+    destroys contexts in module order, the way a host process that opens and closes databases does
+    (the fault this used to meet and its fix)."""
     import torch
     from lazydb_amd import Engine
     e = Engine(0)

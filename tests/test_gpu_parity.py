@@ -165,3 +165,18 @@ def test_config4_4gib_64bit_offsets(eng):
     ref, rt = coracle.scan(img)
     assert_same(res, tup, ref, rt)
     assert ref.status == -1 and ref.end_off > (1 << 32) and res.n_entries == k
+
+
+def test_config3_8gib_full_parity(eng):
+    """BASELINE config 3 at its full size: one 8 GiB log file (bound 2^33), 64-B keys, values of
+    16 * Zipf(1.1, [1, 4096]) bytes (16 B .. 64 KiB; vSize varints of 1-3 bytes). Entry offsets need 34
+    bits (they run to within 64 KiB of the 2^33 bound); every tuple, the stop status and the append offset must be the oracle's."""
+    img, n, end = coracle.gen_log(8 << 30, 2, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
+    assert end > (1 << 33) - (64 << 10)
+    d = to_dev(img)
+    res, tup = eng.scan_dev(d, cap=n + 16)
+    del d
+    ref, rt = coracle.scan(img)
+    assert_same(res, tup, ref, rt)
+    assert ref.n_entries == n and int(rt["pos"][-1] & ((1 << 40) - 1)) > (1 << 33) - (128 << 10)
+    assert res.status == 2 and res.n_repairs == 0

@@ -142,3 +142,25 @@ def test_faithful_port_matches(tmp_path):
     r2, t2 = coracle.scan(img)
     assert (res.status, res.n_entries, res.end_off) == (r2.status, r2.n_entries, r2.end_off)
     assert np.array_equal(t["pos"], t2["pos"])
+
+
+def test_crc_fold_and_table_formulations_equal_zlib():
+    """The oracle's CRC-32 runs carry-less-multiply folding for spans of 64 B and more (the class of
+    Go amd64 hash/crc32's IEEE path) and slicing-by-8 tables below that; both formulations must give
+    zlib's CRC-32/IEEE on every length and alignment, including the check value of "123456789"."""
+    import ctypes as C
+    import zlib
+    L = coracle.lib()
+    L.ldbo_crc32_reg_tables.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+    L.ldbo_crc32_reg_tables.restype = C.c_uint32
+    assert coracle.crc32(b"123456789") == 0xCBF43926
+    rng = np.random.default_rng(7)
+    buf = rng.integers(0, 256, 1 << 18, dtype=np.uint8)
+    for t in range(1500):
+        off = int(rng.integers(0, 64))
+        n = int(rng.integers(0, 3000)) if t % 10 else int(rng.integers(0, 1 << 17))
+        seg = buf[off:off + n]
+        ptr = seg.ctypes.data if n else None
+        want = zlib.crc32(seg.tobytes())
+        assert L.ldbo_crc32_reg(0xFFFFFFFF, ptr, n) ^ 0xFFFFFFFF == want, (off, n)
+        assert L.ldbo_crc32_reg_tables(0xFFFFFFFF, ptr, n) ^ 0xFFFFFFFF == want, (off, n)
