@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--legs", default="2,3",
                     help="extra single-GPU configs timed after the main line at N = 1 (comma list; '' = none)")
     ap.add_argument("--leg-steps", type=int, default=20)
+    ap.add_argument("--pmc", type=int, default=1,
+                    help="measure roofline.traffic in this run: a rocprofv3 --pmc FETCH_SIZE child process scans "
+                         "the same image (N = 1, rank 0; 0: skip)")
+    ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--rehearse-launch", action="store_true",
                     help="launcher self-test without a GPU: ranks rendezvous over gloo and report")
     return ap.parse_args()
@@ -203,20 +207,60 @@ def cpu_baseline(img, end, sample_mib: int):
             "host_cpu": _cpu_model(), "host_nproc": os.cpu_count()}
 
 
-def _pmc_traffic(args):
-    """HBM read bytes per k_scan_main launch from the committed rocprofv3 PMC pass of this
-    workload (tools/profile.sh -> profiles/<round>_pmc_cfg<N>.json: FETCH_SIZE x 2, the gfx950
-    correction for wide streaming reads). PMC counters cannot be read inside this process."""
+def pmc_child(args):
+    """Child of measure_traffic(), run under rocprofv3 --pmc: scan an image file a few times."""
+    import numpy as np
+    import torch
+    from lazydb_amd import Engine
+    path, cap = args.pmc_child.rsplit(":", 1)
+    img = np.fromfile(path, dtype=np.uint8)
+    eng = Engine(0)
+    S = Resident(eng, img, int(cap), args.kind, torch.device("cuda:0"))
+    eng.reserve(img.size)
+    for _ in range(3):
+        eng.scan_dev_async(S.d, fid=1, io_type=args.io, kind=args.kind, out=S.out, cap=S.cap, result=S.res)
+    torch.cuda.synchronize()
+    eng.close()
+
+
+def measure_traffic(img, cap, args):
+    """HBM bytes per k_scan_main launch, measured in this run: a child process scans the same image
+    under `rocprofv3 --pmc FETCH_SIZE` (a counter-only pass, no other trace), and FETCH_SIZE is
+    doubled, the gfx950 correction for wide streaming reads (MI355X_MICROARCH.md "HBM"). Counters
+    cannot be read inside this process. Returns (bytes or None, how it was obtained)."""
+    import csv
     import glob
-    if args.io != 0 or args.kind != 0:
-        return None, None
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_cfg{args.config}.json")))
-    if not cands:
-        return None, None
-    with open(cands[-1]) as f:
-        pmc = json.load(f)
-    v = pmc.get("k_scan_main", {}).get("hbm_read_bytes_per_launch")
-    return (int(v) if v else None), os.path.relpath(cands[-1], ROOT)
+    import shutil
+    import subprocess
+    if not args.pmc or not shutil.which("rocprofv3"):
+        return None, "not measured (rocprofv3 absent or --pmc 0)"
+    tmp = tempfile.mkdtemp(prefix="ldb_pmc_", dir="/tmp")
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else tmp
+    path = os.path.join(shm, f"ldb_pmc_{os.getpid()}.bin")
+    try:
+        img.tofile(path)
+        cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--pmc", "FETCH_SIZE", "--kernel-include-regex",
+               "k_scan_main", "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
+               "--pmc-child", f"{path}:{cap}", "--io", str(args.io), "--kind", str(args.kind)]
+        p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
+        per = {}
+        for f in glob.glob(os.path.join(tmp, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    if "k_scan_main" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+                        key = r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id")
+                        per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+        if not per:
+            return None, f"rocprofv3 child produced no k_scan_main FETCH_SIZE (rc {p.returncode})"
+        kib = sum(per.values()) / len(per)
+        return int(kib * 1024 * 2), (f"measured in this run: rocprofv3 --pmc FETCH_SIZE over {len(per)} k_scan_main "
+                                     f"launches of the same image, x2 (gfx950 wide-read correction)")
+    except Exception as e:   # the traffic figure is diagnostic: never fail the bench line over it
+        return None, f"not measured ({type(e).__name__}: {e})"
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def _cpu_model():
@@ -544,6 +588,8 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.rehearse_launch:
         return rehearse_launch(args)
+    if args.pmc_child:
+        return pmc_child(args)
     if args.config == 5 and (args.xmerge or args.xsim):
         return main_xmerge(args)
     if args.config == 5:
@@ -616,7 +662,8 @@ def main():
                              "status_matches": int(res_h.n_entries) == entries}
     ms_step = t_max / args.steps * 1e3
     value = tot_bytes / (t_max / args.steps) / 2**30
-    traffic, traffic_src = _pmc_traffic(args)
+    traffic, traffic_src = (measure_traffic(img, cap, args) if rank == 0 and world == 1 and args.io == 0
+                            else (None, "not measured (N > 1 or Mmap rule)"))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(img, end_expect, args.cpu_sample_mib)
