@@ -56,12 +56,36 @@ constexpr uint32_t kOwnerOk = 8u;     // sflag: owner of the region's first star
 constexpr uint32_t kMinFast = kS + 4; // fast path: every entry >= 84 B (one start per slice, one check per lane)
 
 // Chain state carried from one region to the next within a wavefront's run.
+//
+// The header memo (m_*) is a template for predicted starts: the header of an entry the lean decode
+// accepted (its bytes [4, hs): Status and the five varints; decode_lean, log_entry.go:81-107). An
+// entry whose header bytes [4, hs) equal the memo's decodes to the same fields, so it has the same
+// size, and a log of equal-sized entries continues at x, x + size, x + 2 size, ... A chained region
+// first tries exactly that chain (predict_starts); every predicted start is verified by the byte
+// compare (plus its own crc field and IOController bounds), so a wrong guess only costs the compare
+// and the region takes the speculative route. Any memo is a valid hypothesis: results never depend
+// on where it came from.
 struct ChainState {
   uint32_t on;       // 1: x / I / owner are valid
   uint32_t I;        // running CRC register (init-based) of the entry open at the region start
   uint32_t owner;    // stored crc of the entry that ends at x
   uint64_t x;        // absolute offset of the next entry start (>= region start)
+  uint32_t m_ok;     // 1: the memo below holds a lean-decoded header
+  uint32_t m_sz, m_hs, m_k, m_vv, m_stat;   // its entry size, header size, key/value sizes, Status
+  uint32_t m_w[4];   // its header bytes [4, 20), bytes at and past hs zeroed
 };
+
+LDB_HD void chain_reset(ChainState& st) {
+  st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
+  st.m_ok = 0; st.m_sz = 0; st.m_hs = 0; st.m_k = 0; st.m_vv = 0; st.m_stat = 0;
+  st.m_w[0] = st.m_w[1] = st.m_w[2] = st.m_w[3] = 0;
+}
+
+// Mask of the header bytes of dword i (bytes [4 + 4i, 8 + 4i)) that lie before hs.
+LDB_HD uint32_t memo_mask(uint32_t hs, int i) {
+  const int n = (int)hs - 4 - 4 * i;
+  return n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * n)));
+}
 
 // A wave-uniform value in a scalar register on the GPU (table lookups with it become scalar loads,
 // counted on lgkmcnt: a vector load's vmcnt wait would also wait for the region DMA in flight).
@@ -381,6 +405,57 @@ LDB_HD RegionSum zero_summary() {   // covered(false) of an all-zero region
   return r;
 }
 
+// Predicted starts of a chained region (see ChainState): lane l's candidate is the first chain
+// position x + j * m_sz at or after its slice start. Returns true when every candidate inside the
+// region verifies against the memo; then cpriv(l).s / X / crc / k / vv / w1 / hs / stat are set for
+// the starting lanes (kNone32 elsewhere) and sh.s mirrors them. Returns false (nothing else
+// changed) as soon as one candidate does not verify: the region then takes the speculative route.
+template <class WP, class CPriv>
+LDB_HD bool predict_starts(WP& wp, const View& v, WaveSh& sh, const ChainState& st, uint32_t xr, CPriv cpriv) {
+  const uint32_t sz = st.m_sz, hs = st.m_hs, kv = st.m_k + st.m_vv;
+  // floor(n / sz) for n < kW: (n + 0.5) / sz lies at least 0.5 / sz from the integers around it,
+  // far beyond the rounding error of the float reciprocal
+  const float rsz = 1.0f / (float)sz;
+  const uint32_t k0 = memo_mask(hs, 0), k1 = memo_mask(hs, 1), k2 = memo_mask(hs, 2), k3 = memo_mask(hs, 3);
+  const uint64_t bad = wp.ballot([&](int l) {
+    ChainPriv& c = cpriv(l);
+    const uint32_t B = (uint32_t)(l * kS);
+    uint32_t p = kNone32;
+    if (B <= xr) {
+      p = xr < B + (uint32_t)kS ? xr : kNone32;
+    } else {
+      const uint32_t q = (uint32_t)(((float)(B - xr - 1) + 0.5f) * rsz);   // floor((B - xr - 1) / sz)
+      p = xr + (q + 1) * sz;
+      p = p < B + (uint32_t)kS ? p : kNone32;
+    }
+    c.s = kNone32;
+    if (p == kNone32) return false;
+    const int a = (int)p + kPre;
+    const int qd = a & ~3;
+    const uint32_t sh4 = (uint32_t)(a & 3);
+    uint32_t d[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) d[i] = lds32(v, qd + 4 * i);
+    const uint32_t w0 = funnel(d[1], d[0], sh4), w1 = funnel(d[2], d[1], sh4), w2 = funnel(d[3], d[2], sh4);
+    const uint32_t w3 = funnel(d[4], d[3], sh4), w4 = funnel(d[5], d[4], sh4);
+    const uint64_t off = v.R0 + (uint64_t)p;
+    const bool ok = w0 != 0u && ((w1 ^ st.m_w[0]) & k0) == 0u && ((w2 ^ st.m_w[1]) & k1) == 0u &&
+                    ((w3 ^ st.m_w[2]) & k2) == 0u && ((w4 ^ st.m_w[3]) & k3) == 0u &&
+                    !read_eof(v.len, v.io, (int64_t)off, kMaxHeader) &&            // log_file.go:117-122
+                    !read_eof(v.len, v.io, (int64_t)(off + hs), kv);               // log_file.go:130-139
+    if (ok) {
+      c.s = p; c.X = p + sz; c.crc = w0; c.k = st.m_k; c.vv = st.m_vv; c.w1 = w1; c.hs = hs; c.stat = st.m_stat;
+    }
+    return !ok;
+  });
+  if (bad) {
+    wp.each([&](int l) { cpriv(l).s = kNone32; });
+    return false;
+  }
+  wp.each([&](int l) { sh.s[l] = cpriv(l).s; });
+  return true;
+}
+
 // The lean path for one region, in one of two modes:
 //   chained (st.on): the chain enters at st.x with the CRC state st.I / st.owner; the owner of the
 //     region's first start is CRC-checked here (kOwnerOk);
@@ -446,6 +521,18 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     xr = (uint32_t)xr64;
     lt = (int)(xr / kS);
   }
+  // ---- predicted starts (memo of equal headers, see ChainState)
+  const bool predicted = !spec && st.m_ok && predict_starts(wp, v, sh, st, xr, cpriv);
+#ifdef LDB_EMU_COUNTERS
+  if (!spec) ++g_chain_why[predicted ? 14 : 15];   // chained regions with / without a verified prediction
+#endif
+  uint32_t tpos = kNone32;
+  int32_t tstat = kCont;
+  uint64_t starts = 0;
+  if (predicted) {
+    wp.each([&](int l) { cpriv(l).chk = 0; });
+    starts = wp.ballot([&](int l) { return cpriv(l).s != kNone32; });
+  } else {
   // ---- speculation: the entry lane decodes at x, later lanes (all lanes when speculative) at
   // their first candidate
   // chained: each lane decodes its first candidate (the pointer round recovers true starts behind
@@ -477,9 +564,6 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   // A chain may end inside the region on a terminal status (lean_terminal): tpos / tstat. Its last
   // entry's owner check then runs at a check-only "pseudo start" at tpos (rewritten like a start,
   // no tuple, not in `starts`).
-  uint32_t tpos = kNone32;
-  int32_t tstat = kCont;
-  uint64_t starts = 0;
   if (!spec && wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) {
     tstat = lean_terminal(v, xr);
     if (tstat == kCont) return LDB_DECLINE(2);
@@ -556,6 +640,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     }
   }
   }   // tpos == kNone32
+  }   // !predicted
   wp.stamp(11);
   if (!starts && tpos == kNone32) {   // speculative, no plausible header anywhere: a covered region
     covered(false);
@@ -573,6 +658,35 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   const uint32_t sL0 = wp.from(L0, [&](int l) { return cpriv(l).s; });
   const int z = starts ? 63 - (int)__builtin_clzll(starts) : L0;
   const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).s; });
+  // the next regions' memo: the region's last entry (the owner of the next x), read while the
+  // staging buffer still holds this region (a predicted region keeps the memo it verified against)
+  // Only a region whose first and last entries look alike (same size and leading header bytes) sets
+  // a memo to predict with: logs of varying entry sizes then never pay for compares that fail.
+  ChainState nm = st;
+  if (!predicted && tpos == kNone32 && starts) {
+    nm.m_ok = 0;
+    if (z != L0) {
+      const uint32_t esz = wp.from(z, [&](int l) { return cpriv(l).X; }) - sz;
+      const uint32_t hsz = uniform(wp.from(z, [&](int l) { return cpriv(l).hs; }));
+      const uint32_t kz = wp.from(z, [&](int l) { return cpriv(l).k; });
+      const uint32_t vz = wp.from(z, [&](int l) { return cpriv(l).vv; });
+      const uint32_t w1z = wp.from(z, [&](int l) { return cpriv(l).w1; });
+      const bool alike = wp.from(L0, [&](int l) {
+        const ChainPriv& c = cpriv(l);
+        return (uint32_t)(c.X - c.s == esz && c.hs == hsz && c.k == kz && c.vv == vz && c.w1 == w1z);
+      }) != 0u;
+      nm.m_ok = alike && esz >= kMinFast && hsz <= 20u;
+      if (nm.m_ok) {
+        nm.m_sz = esz;
+        nm.m_hs = hsz;
+        nm.m_k = kz;
+        nm.m_vv = vz;
+        nm.m_stat = wp.from(z, [&](int l) { return cpriv(l).stat; });
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nm.m_w[i] = uniform(vword(v, (int)sz + 4 + 4 * i)) & memo_mask(hsz, i);
+      }
+    }
+  }
   // ---- tuples (see emit above)
   wp.each([&](int l) {
     const ChainPriv& c = cpriv(l);
@@ -673,6 +787,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     r.rpre = rpre;
     r.sflag = spec ? 0u : kOwnerOk;
     store(r);
+    st = nm;
     st.on = 0;
     wp.stamp(15);
     return true;
@@ -688,6 +803,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   r.sflag = spec ? kStraddle : (kStraddle | kOwnerOk);
   if (tail <= 4) { r.sflag |= kSkip; r.rout = 0; }
   store(r);
+  st = nm;
   st.on = tail > 4 ? 1u : 0u;   // after a kSkip straddler the next region starts speculative
   st.x = r.exitp;
   st.I = r.rout;

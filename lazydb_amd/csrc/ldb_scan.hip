@@ -276,7 +276,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   const uint64_t count = rb < p.nreg ? (p.nreg - rb < per ? p.nreg - rb : per) : 0;
   GpuWave wp{lane};
   ChainState st;
-  st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
+  chain_reset(st);
   uint32_t n_fast = 0;
   // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
   // has read it for the last time (buffer_free), so the DMA overlaps the summary, its stores and

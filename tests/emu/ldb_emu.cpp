@@ -207,7 +207,7 @@ extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t 
     std::vector<uint64_t> deferred;
     for (uint64_t r0 = 0; r0 < nreg; r0 += run_len) {   // k_scan_main
       ChainState st;
-      st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
+      chain_reset(st);
       for (uint64_t r = r0; r < nreg && r < r0 + run_len; ++r) {
         if (emu.run_chained(p, r, st)) ++n_fast;
         else deferred.push_back(r);

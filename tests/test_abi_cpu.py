@@ -232,3 +232,47 @@ def test_emulated_zero_regions(run_len):
                 assert_same(res, tup, ref, rt)
                 if flip is None and img is tail:
                     assert int(st[2]) == nreg
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_emulated_predicted_starts(seed):
+    """Chained regions of equal-sized entries take the predicted-start route (ChainState memo,
+    ldb_chain.h predict_starts): every chain position is verified by a header-byte compare. Logs
+    whose entry size changes mid-run, corrupted headers (a size varint, the Status byte, a zeroed crc
+    field), corrupted values and cut ends must all give exactly the oracle's result."""
+    from oracle import pyoracle as P
+    rng = random.Random(70 + seed)
+    a = coracle.gen_log(300_000, 80 + seed, ksize=64, vsize=256)
+    b = coracle.gen_log(200_000, 90 + seed, ksize=16, vsize=100)
+    c = coracle.gen_log(150_000, 95 + seed, ksize=64, vsize=256)
+    # three runs of different entry sizes back to back, then the zero tail of a preallocated file
+    img = np.concatenate([a[0][: a[2]], b[0][: b[2]], c[0][: c[2]], np.zeros(9000, np.uint8)])
+    ends = [0, a[2], a[2] + b[2], a[2] + b[2] + c[2]]
+    res, tup, st = emu_scan(img, 0, 64)
+    ref, rt = coracle.scan(img, 0)
+    assert_same(res, tup, ref, rt)
+    starts = rt["pos"] & ((1 << 40) - 1)
+    for trial in range(14):
+        im = img.copy()
+        kind = trial % 7
+        k = rng.randrange(1, len(starts) - 1)
+        s0 = int(starts[k])
+        if kind == 0:
+            im[s0 + 10] ^= 0x02          # a size varint byte: the header no longer equals the memo
+        elif kind == 1:
+            im[s0 + 4] = 1               # Status SDelete: a different (valid-looking) header
+        elif kind == 2:
+            im[s0: s0 + 4] = 0           # zeroed crc field at a predicted start
+        elif kind == 3:
+            im[s0 + 40] ^= 0x10          # a value byte: the owner check fails
+        elif kind == 4:
+            im = im[: s0 + rng.randrange(1, 300)].copy()   # cut inside an entry
+        elif kind == 5:
+            im = np.concatenate([im[: ends[rng.randrange(1, 4)]], np.zeros(rng.choice([0, 10, 38, 5000]), np.uint8)])
+        else:
+            e = P.encode_entry(P.Entry(key=b"k" * 64, value=b"v" * 256, k_size=64, v_size=256, expired_at=5))
+            im[s0: s0 + len(e)] = np.frombuffer(e, np.uint8)   # a valid entry of another header shape
+        for io in (0, 1):
+            res, tup, st = emu_scan(im, io, 64)
+            ref, rt = coracle.scan(im, io)
+            assert_same(res, tup, ref, rt)
