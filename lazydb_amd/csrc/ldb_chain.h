@@ -70,15 +70,19 @@ struct ChainState {
   uint32_t I;        // running CRC register (init-based) of the entry open at the region start
   uint32_t owner;    // stored crc of the entry that ends at x
   uint64_t x;        // absolute offset of the next entry start (>= region start)
-  uint32_t m_ok;     // 1: the memo below holds a lean-decoded header
-  uint32_t m_sz, m_hs, m_k, m_vv, m_stat;   // its entry size, header size, key/value sizes, Status
-  uint32_t m_w[4];   // its header bytes [4, 20), bytes at and past hs zeroed
+  uint32_t m_meta;   // memo: bit 0 valid (a lean-decoded header), bits 1-5 header size hs, 8-15 Status
+  uint32_t m_k, m_vv;   // its key/value sizes (entry size hs + k + vv)
+  uint32_t m_w[3];   // its header bytes [4, 16), bytes at and past hs zeroed (hs <= 16)
+  LDB_HD uint32_t m_ok() const { return m_meta & 1u; }
+  LDB_HD uint32_t m_hs() const { return (m_meta >> 1) & 31u; }
+  LDB_HD uint32_t m_stat() const { return (m_meta >> 8) & 0xFFu; }
+  LDB_HD uint32_t m_sz() const { return m_hs() + m_k + m_vv; }
 };
 
 LDB_HD void chain_reset(ChainState& st) {
   st.on = 0; st.I = 0; st.owner = 0; st.x = 0;
-  st.m_ok = 0; st.m_sz = 0; st.m_hs = 0; st.m_k = 0; st.m_vv = 0; st.m_stat = 0;
-  st.m_w[0] = st.m_w[1] = st.m_w[2] = st.m_w[3] = 0;
+  st.m_meta = 0; st.m_k = 0; st.m_vv = 0;
+  st.m_w[0] = st.m_w[1] = st.m_w[2] = 0;
 }
 
 // Mask of the header bytes of dword i (bytes [4 + 4i, 8 + 4i)) that lie before hs.
@@ -377,6 +381,29 @@ LDB_HD void lane_scan(WP& wp, const uint32_t* tab, CPriv cpriv, int seg = 0) {
   scan_step_seg<5>(wp, tab, cpriv, seg);
 }
 
+// Tree reduction of the G-chain (the up-sweep of a scan): after step i, every lane l with its low
+// i + 1 bits set holds the register of slices [l - 2^(i+1) + 1, l]; lane 63 ends with the whole
+// region. A covered region needs only that total: the 63 combines cost 1/5 of the scan's lookups
+// (lanes that do not combine stay off the LDS).
+template <int I, class WP, class CPriv>
+LDB_HD void reduce_step(WP& wp, const uint32_t* tab, CPriv cpriv) {
+  constexpr int off = I == 0 ? kZCOff : kSCOff + (I - 1) * kShW;
+  constexpr int d = 1 << I;
+  wp.template shfl_up<d>([&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
+    if (valid && (l & (2 * d - 1)) == 2 * d - 1) cpriv(l).O ^= shift_tab(tab, off, t);
+  });
+}
+
+template <class WP, class CPriv>
+LDB_HD void lane_reduce(WP& wp, const uint32_t* tab, CPriv cpriv) {
+  reduce_step<0>(wp, tab, cpriv);
+  reduce_step<1>(wp, tab, cpriv);
+  reduce_step<2>(wp, tab, cpriv);
+  reduce_step<3>(wp, tab, cpriv);
+  reduce_step<4>(wp, tab, cpriv);
+  reduce_step<5>(wp, tab, cpriv);
+}
+
 // Zero-region shortcut (k_scan_main and the emulator call it before region_chained): a speculative
 // region (!st.on) whose bytes and halo are all zero -- the preallocated tail of a log file,
 // iocontroller/fileio.go:66-68 -- has no plausible start (every candidate decodes with kSize == 0),
@@ -412,11 +439,11 @@ LDB_HD RegionSum zero_summary() {   // covered(false) of an all-zero region
 // changed) as soon as one candidate does not verify: the region then takes the speculative route.
 template <class WP, class CPriv>
 LDB_HD bool predict_starts(WP& wp, const View& v, WaveSh& sh, const ChainState& st, uint32_t xr, CPriv cpriv) {
-  const uint32_t sz = st.m_sz, hs = st.m_hs, kv = st.m_k + st.m_vv;
+  const uint32_t hs = st.m_hs(), kv = st.m_k + st.m_vv, sz = hs + kv, stat = st.m_stat();
   // floor(n / sz) for n < kW: (n + 0.5) / sz lies at least 0.5 / sz from the integers around it,
   // far beyond the rounding error of the float reciprocal
   const float rsz = 1.0f / (float)sz;
-  const uint32_t k0 = memo_mask(hs, 0), k1 = memo_mask(hs, 1), k2 = memo_mask(hs, 2), k3 = memo_mask(hs, 3);
+  const uint32_t k0 = memo_mask(hs, 0), k1 = memo_mask(hs, 1), k2 = memo_mask(hs, 2);
   const uint64_t bad = wp.ballot([&](int l) {
     ChainPriv& c = cpriv(l);
     const uint32_t B = (uint32_t)(l * kS);
@@ -433,18 +460,18 @@ LDB_HD bool predict_starts(WP& wp, const View& v, WaveSh& sh, const ChainState& 
     const int a = (int)p + kPre;
     const int qd = a & ~3;
     const uint32_t sh4 = (uint32_t)(a & 3);
-    uint32_t d[6];
+    uint32_t d[5];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) d[i] = lds32(v, qd + 4 * i);
+    for (int i = 0; i < 5; ++i) d[i] = lds32(v, qd + 4 * i);
     const uint32_t w0 = funnel(d[1], d[0], sh4), w1 = funnel(d[2], d[1], sh4), w2 = funnel(d[3], d[2], sh4);
-    const uint32_t w3 = funnel(d[4], d[3], sh4), w4 = funnel(d[5], d[4], sh4);
+    const uint32_t w3 = funnel(d[4], d[3], sh4);
     const uint64_t off = v.R0 + (uint64_t)p;
     const bool ok = w0 != 0u && ((w1 ^ st.m_w[0]) & k0) == 0u && ((w2 ^ st.m_w[1]) & k1) == 0u &&
-                    ((w3 ^ st.m_w[2]) & k2) == 0u && ((w4 ^ st.m_w[3]) & k3) == 0u &&
+                    ((w3 ^ st.m_w[2]) & k2) == 0u &&
                     !read_eof(v.len, v.io, (int64_t)off, kMaxHeader) &&            // log_file.go:117-122
                     !read_eof(v.len, v.io, (int64_t)(off + hs), kv);               // log_file.go:130-139
     if (ok) {
-      c.s = p; c.X = p + sz; c.crc = w0; c.k = st.m_k; c.vv = st.m_vv; c.w1 = w1; c.hs = hs; c.stat = st.m_stat;
+      c.s = p; c.X = p + sz; c.crc = w0; c.k = st.m_k; c.vv = st.m_vv; c.w1 = w1; c.hs = hs; c.stat = stat;
     }
     return !ok;
   });
@@ -491,7 +518,9 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       release();
       cpriv(l).O = crc_slice_raw2(v.tab, rows);
     });
-    lane_scan(wp, v.tab, cpriv);
+    // the region's register is lane 63's; a partial region (the file's last) needs a prefix as well
+    if (v.rlen == (uint32_t)kW) lane_reduce(wp, v.tab, cpriv);
+    else lane_scan(wp, v.tab, cpriv);
     const uint32_t raw = wp.from(kLanes - 1, [&](int l) { return cpriv(l).O; });
     wp.stamp(16);
     RegionSum r;
@@ -522,9 +551,10 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     lt = (int)(xr / kS);
   }
   // ---- predicted starts (memo of equal headers, see ChainState)
-  const bool predicted = !spec && st.m_ok && predict_starts(wp, v, sh, st, xr, cpriv);
+  const bool predicted = !spec && st.m_ok() && predict_starts(wp, v, sh, st, xr, cpriv);
 #ifdef LDB_EMU_COUNTERS
   if (!spec) ++g_chain_why[predicted ? 14 : 15];   // chained regions with / without a verified prediction
+  if (!spec && st.m_ok()) ++g_chain_why[13];          // ... of which a prediction was tried
 #endif
   uint32_t tpos = kNone32;
   int32_t tstat = kCont;
@@ -664,7 +694,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   // a memo to predict with: logs of varying entry sizes then never pay for compares that fail.
   ChainState nm = st;
   if (!predicted && tpos == kNone32 && starts) {
-    nm.m_ok = 0;
+    nm.m_meta = 0;
     if (z != L0) {
       const uint32_t esz = wp.from(z, [&](int l) { return cpriv(l).X; }) - sz;
       const uint32_t hsz = uniform(wp.from(z, [&](int l) { return cpriv(l).hs; }));
@@ -675,15 +705,12 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
         const ChainPriv& c = cpriv(l);
         return (uint32_t)(c.X - c.s == esz && c.hs == hsz && c.k == kz && c.vv == vz && c.w1 == w1z);
       }) != 0u;
-      nm.m_ok = alike && esz >= kMinFast && hsz <= 20u;
-      if (nm.m_ok) {
-        nm.m_sz = esz;
-        nm.m_hs = hsz;
-        nm.m_k = kz;
-        nm.m_vv = vz;
-        nm.m_stat = wp.from(z, [&](int l) { return cpriv(l).stat; });
+      if (alike && esz >= kMinFast && hsz <= 16u) {
+        nm.m_meta = uniform(1u | (hsz << 1) | (wp.from(z, [&](int l) { return cpriv(l).stat; }) << 8));
+        nm.m_k = uniform(kz);
+        nm.m_vv = uniform(vz);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) nm.m_w[i] = uniform(vword(v, (int)sz + 4 + 4 * i)) & memo_mask(hsz, i);
+        for (int i = 0; i < 3; ++i) nm.m_w[i] = uniform(vword(v, (int)sz + 4 + 4 * i)) & memo_mask(hsz, i);
       }
     }
   }
