@@ -8,7 +8,7 @@ Default workload, at every N = BASELINE config 4's per-GPU file: one 4 GiB log f
 entries, 4 294 967 136 valid bytes each. The same per-GPU file at N = 1, 2, 4, 8 makes
 the 1 -> N curve comparable (weak scaling: independent files, index.go:68-95).
 At N = 1 the line also carries `legs`: BASELINE config 2 (1 GiB) and config 3
-(8 GiB, Zipf values), each timed the same way (GiB/s, k_scan_main ms, roofline frac).
+(8 GiB, Zipf values), each timed the same way (GiB/s, kernel ms, roofline frac).
 
 Multi-GPU: `python bench.py --gpus N` spawns N rank processes itself (before anything
 touches the GPU); `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
@@ -223,8 +223,8 @@ def pmc_child(args):
     eng.close()
 
 
-def measure_traffic(img, cap, args):
-    """HBM bytes per k_scan_main launch, measured in this run: a child process scans the same image
+def measure_traffic(img, cap, args, kernel):
+    """HBM bytes per launch of `kernel` (the dominant one), measured in this run: a child process scans the same image
     under `rocprofv3 --pmc FETCH_SIZE` (a counter-only pass, no other trace), and FETCH_SIZE is
     doubled, the gfx950 correction for wide streaming reads (MI355X_MICROARCH.md "HBM"). Counters
     cannot be read inside this process. Returns (bytes or None, how it was obtained)."""
@@ -240,20 +240,20 @@ def measure_traffic(img, cap, args):
     try:
         img.tofile(path)
         cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--pmc", "FETCH_SIZE", "--kernel-include-regex",
-               "k_scan_main", "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
+               kernel, "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", f"{path}:{cap}", "--io", str(args.io), "--kind", str(args.kind)]
         p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
         per = {}
         for f in glob.glob(os.path.join(tmp, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    if "k_scan_main" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+                    if kernel in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
                         key = r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id")
                         per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
         if not per:
-            return None, f"rocprofv3 child produced no k_scan_main FETCH_SIZE (rc {p.returncode})"
+            return None, f"rocprofv3 child produced no {kernel} FETCH_SIZE (rc {p.returncode})"
         kib = sum(per.values()) / len(per)
-        return int(kib * 1024 * 2), (f"measured in this run: rocprofv3 --pmc FETCH_SIZE over {len(per)} k_scan_main "
+        return int(kib * 1024 * 2), (f"measured in this run: rocprofv3 --pmc FETCH_SIZE over {len(per)} {kernel} "
                                      f"launches of the same image, x2 (gfx950 wide-read correction)")
     except Exception as e:   # the traffic figure is diagnostic: never fail the bench line over it
         return None, f"not measured ({type(e).__name__}: {e})"
@@ -507,7 +507,7 @@ class Resident:
 
 def timed_scans(eng, S, fid, args, steps, world, stream):
     """K device-resident scans of one image between barrier + synchronize, with HIP events around
-    every launch on the scan stream. Returns (wall seconds, avg k_scan_main ms, avg pipeline ms)."""
+    every launch on the scan stream. Returns (wall seconds, avg k_uniform ms, avg k_scan_main ms, avg pipeline ms)."""
     import torch
     import torch.distributed as dist
 
@@ -528,8 +528,25 @@ def timed_scans(eng, S, fid, args, steps, world, stream):
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
-    main_ms, total_ms, _ = eng.timing(0)
-    return t, main_ms, total_ms
+    run_ms, main_ms, total_ms, _ = eng.timing_split(0)
+    return t, run_ms, main_ms, total_ms
+
+
+def dominant_kernel(S, r, kind, run_ms, main_ms):
+    """The scan's dominant kernel and its algorithmic bytes per launch (the bytes of
+    the accepted entries it verified). k_uniform (the run prefix) verified entries [0, n_run), i.e.
+    bytes [0, x0); k_scan_main (the region pipeline) the rest, [x0, end_off)."""
+    n_run, n, end = int(r.n_run), int(r.n_entries), int(r.end_off)
+    if n_run == 0:
+        x0 = 0
+    elif n_run >= n:
+        x0 = end
+    else:
+        tsz = 16 if kind == 0 else 48
+        x0 = int.from_bytes(S.out[n_run * tsz: n_run * tsz + 8].cpu().numpy().tobytes(), "little") & ((1 << 40) - 1)
+    if run_ms >= main_ms:
+        return "k_uniform", x0, run_ms
+    return "k_scan_main", end - x0, main_ms
 
 
 def prepare(eng, cfg, rank, args, dev, verify: bool):
@@ -563,14 +580,16 @@ def run_leg(eng, cfg, args, dev):
     """One extra single-GPU config (N = 1 only): the same timed scans as the main line."""
     import torch
     img, S, r, verified, workload, _ = prepare(eng, cfg, 0, args, dev, not args.no_verify)
-    t, main_ms, total_ms = timed_scans(eng, S, 1, args, args.leg_steps, 1, torch.cuda.current_stream(dev))
+    t, run_ms, main_ms, total_ms = timed_scans(eng, S, 1, args, args.leg_steps, 1, torch.cuda.current_stream(dev))
+    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms)
     step = t / args.leg_steps
-    achieved = int(r.end_off) / (main_ms * 1e-3) / 1e9 if main_ms > 0 else None
+    achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else None
     leg = {"config": cfg, "workload": workload, "file_bytes": int(img.size), "bytes_scanned": int(r.end_off),
            "entries": int(r.n_entries), "steps": args.leg_steps, "ms_per_step": round(step * 1e3, 4),
            "GiB_per_s": round(int(r.end_off) / step / 2**30, 3),
            "mentries_per_s": round(int(r.n_entries) / step / 1e6, 2),
-           "k_scan_main_ms": round(main_ms, 4), "pipeline_ms": round(total_ms, 4),
+           "k_uniform_ms": round(run_ms, 4), "k_scan_main_ms": round(main_ms, 4), "pipeline_ms": round(total_ms, 4),
+           "run_entries": int(r.n_run), "roofline_kernel": kname, "roofline_bytes": kbytes,
            "roofline_frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
            "status": int(r.status), "fast_regions": int(r.n_fast), "regions": int(r.n_regions),
            "verified_vs_oracle": verified}
@@ -608,7 +627,8 @@ def main():
     eng = Engine(local)
     img, S, r, verified, workload, end_expect = prepare(eng, args.config, rank, args, dev, not args.no_verify)
     stream = torch.cuda.current_stream(dev)
-    t, main_ms, total_ms = timed_scans(eng, S, 1 + rank, args, args.steps, world, stream)
+    t, run_ms, main_ms, total_ms = timed_scans(eng, S, 1 + rank, args, args.steps, world, stream)
+    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms)
     # practical HBM-read ceiling on this box: a read-only reduction over the same image, after the
     # timed region
     ceiling = eng.read_ceiling(S.d, 20) if rank == 0 else None
@@ -662,7 +682,7 @@ def main():
                              "status_matches": int(res_h.n_entries) == entries}
     ms_step = t_max / args.steps * 1e3
     value = tot_bytes / (t_max / args.steps) / 2**30
-    traffic, traffic_src = (measure_traffic(img, cap, args) if rank == 0 and world == 1 and args.io == 0
+    traffic, traffic_src = (measure_traffic(img, cap, args, kname) if rank == 0 and world == 1 and args.io == 0
                             else (None, "not measured (N > 1 or Mmap rule)"))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -675,7 +695,7 @@ def main():
             if cfg != args.config and cfg in (1, 2, 3, 4):
                 legs.append(run_leg(eng, cfg, args, dev))
     if rank == 0:
-        achieved = bytes_scanned / (main_ms * 1e-3) / 1e9 if main_ms > 0 else None
+        achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else None
         line = {
             "metric": "device-resident log decode+CRC32: GiB/s and Mentries/s at 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -698,16 +718,19 @@ def main():
             "hbm_read_frac_of_8TBs": round(tot_bytes / world / (t_max / args.steps) / 1e9 / PEAK_HBM_GBS, 4),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_scan_main",
+                "kernel": kname,
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "avg_kernel_ms": round(main_ms, 4),
+                "avg_kernel_ms": round(kms, 4),
+                "avg_k_uniform_ms": round(run_ms, 4),
+                "avg_k_scan_main_ms": round(main_ms, 4),
+                "run_entries": int(r.n_run),
                 "avg_pipeline_ms": round(total_ms, 4),
-                "algorithmic_bytes_per_launch": bytes_scanned,
+                "algorithmic_bytes_per_launch": kbytes,
                 "practical_ceiling": {"kernel": "read-only reduction over the image (ldb_read_ceiling)",
                                       "GB_per_s": round(ceiling, 1) if ceiling else None,
                                       "frac": round(achieved / ceiling, 4) if achieved and ceiling else None},

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define LDB_ABI_VERSION 1
+#define LDB_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------
  * Normal terminations of the replay loop (index.go:86-88 `break`) are > 0;
@@ -100,9 +100,11 @@ typedef struct ldb_scan_result {
   uint64_t end_off;      /* offset at which ReadLogEntry returned `status`; for EOF statuses this is the
                             append position index.go:97-99 stores into LogFile.Offset */
   uint32_t n_repairs;    /* diagnostics: speculative-walk repairs performed (0 on well-formed logs) */
-  uint32_t n_regions;    /* diagnostics: parallel regions the image was cut into */
-  uint32_t n_fast;       /* diagnostics: regions verified by the chained fast path (ldb_chain.h) */
+  uint32_t n_regions;    /* diagnostics: regions the region pipeline replayed (after the run prefix) */
+  uint32_t n_fast;       /* diagnostics: of those, regions verified by the chained fast path (ldb_chain.h) */
   uint32_t reserved_;
+  uint64_t n_run;        /* diagnostics: leading entries verified as one run of equal-sized entries
+                            (k_uniform); they are tuples [0, n_run) */
 } ldb_scan_result;
 
 /* ---- context ---------------------------------------------------------------
@@ -156,6 +158,10 @@ int ldb_scan_file_dev_serial(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len,
  * the scan stream around each launch (no host synchronisation while enabled; the query waits
  * for the recorded events). enable: 1 on + reset, 0 off + reset, -1 query only. */
 int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n);
+/* The same with the run-prefix kernel (k_uniform, the equal-sized entries at the file start) timed on
+ * its own: avg_run_ms; avg_main_ms is then the region pipeline's main kernel after it. */
+int ldb_kernel_timing_split(ldb_ctx* ctx, int enable, double* avg_run_ms, double* avg_main_ms, double* avg_total_ms,
+                            uint64_t* n);
 
 /* Practical HBM-read ceiling for the roofline report: a read-only XOR
  * reduction over the device image d_image[0, len), 16-B loads, `iters` timed launches after one

@@ -28,7 +28,7 @@ ENTRY_TUPLE = np.dtype([("offset", "<u8"), ("expired_at", "<i8"), ("tx_id", "<u8
 class ScanResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("fid", C.c_uint32), ("n_entries", C.c_uint64), ("end_off", C.c_uint64),
                 ("n_repairs", C.c_uint32), ("n_regions", C.c_uint32),
-                ("n_fast", C.c_uint32), ("reserved_", C.c_uint32)]
+                ("n_fast", C.c_uint32), ("reserved_", C.c_uint32), ("n_run", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -60,7 +60,7 @@ assert C.sizeof(MergeFile) == 24 and C.sizeof(MergeResult) == 56 and ENCODE_ITEM
 assert MERGE_POS.itemsize == 32 and MERGE_SEGMENT.itemsize == 32 and MERGE_FILE_STAT.itemsize == 40
 
 RESULT_BYTES = C.sizeof(ScanResult)
-assert RESULT_BYTES == 40
+assert RESULT_BYTES == 48
 
 _lib = None
 
@@ -89,6 +89,9 @@ def lib():
         L.ldb_scan_file.argtypes = [vp, vp, u64, u32, i32, i32, vp, u64, C.POINTER(ScanResult)]
         L.ldb_scan_files_dev.argtypes = [vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]
         L.ldb_kernel_timing.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)]
+        L.ldb_kernel_timing_split.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                              C.POINTER(C.c_double), C.POINTER(u64)]
+        L.ldb_kernel_timing_split.restype = i32
         for fn in ("ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve", "ldb_scan_file_dev",
                    "ldb_scan_file_dev_serial", "ldb_scan_file", "ldb_scan_files_dev", "ldb_kernel_timing"):
             getattr(L, fn).restype = i32
@@ -113,7 +116,7 @@ def lib():
             L.ldb_encode_entries_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u64, vp, u64, vp, u32,
                                                  C.POINTER(MergeResult), vp]
             L.ldb_encode_entries_dev.restype = i32
-        if L.ldb_abi_version() != 1:
+        if L.ldb_abi_version() != 2:
             raise LdbError("liblazydb_gpu ABI version mismatch")
         _lib = L
     return _lib
@@ -121,7 +124,7 @@ def lib():
 
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
-           "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_read_ceiling", "ldb_merge_files_dev",
+           "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_kernel_timing_split", "ldb_read_ceiling", "ldb_merge_files_dev",
            "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_merge_repack_dev", "ldb_host_register", "ldb_host_unregister")
 
 

@@ -506,8 +506,11 @@ LDB_HD bool predict_starts(WP& wp, const View& v, WaveSh& sh, const ChainState& 
 template <class WP, class CPriv, class Emit, class Free, class Restage, class Store>
 LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainState& st, CPriv cpriv, Emit emit,
                            Free release, Restage restage, Store store) {
-  const bool spec = !st.on;
-  if (!spec && st.x < v.R0) return LDB_DECLINE(1);
+  // st.on: 0 = speculative (entry and owner unknown), 1 = chained (entry x, owner's CRC state I),
+  // 2 = entry x known but its owner verified elsewhere (the replay's first region after the run
+  // prefix, or region 0 with x = 0): start discovery as chained, CRC handling as speculative
+  const bool known = st.on != 0, spec = st.on != 1;
+  if (known && st.x < v.R0) return LDB_DECLINE(1);
   // covered region: raw register of the whole region (rpre); chained mode also advances st.I
   auto covered = [&](bool chained) {
     const uint32_t Ishift = chained ? shift_tab_uniform(v.gsh, st.I) : 0u;   // build_gshift kGsW: one region
@@ -541,9 +544,10 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   };
   uint32_t xr = 0;
   int lt = -1;
-  if (!spec) {
+  if (known) {
     const uint64_t xr64 = st.x - v.R0;
     if (xr64 >= (uint64_t)kW) {   // the open entry runs through the region: no header can start here
+      if (spec) return LDB_DECLINE(1);
       covered(true);
       return true;
     }
@@ -551,10 +555,10 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     lt = (int)(xr / kS);
   }
   // ---- predicted starts (memo of equal headers, see ChainState)
-  const bool predicted = !spec && st.m_ok() && predict_starts(wp, v, sh, st, xr, cpriv);
+  const bool predicted = known && st.m_ok() && predict_starts(wp, v, sh, st, xr, cpriv);
 #ifdef LDB_EMU_COUNTERS
-  if (!spec) ++g_chain_why[predicted ? 14 : 15];   // chained regions with / without a verified prediction
-  if (!spec && st.m_ok()) ++g_chain_why[13];          // ... of which a prediction was tried
+  if (known) ++g_chain_why[predicted ? 14 : 15];   // chained regions with / without a verified prediction
+  if (known && st.m_ok()) ++g_chain_why[13];          // ... of which a prediction was tried
 #endif
   uint32_t tpos = kNone32;
   int32_t tstat = kCont;
@@ -574,7 +578,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     c.chk = 0;
     c.X = l == lt ? xr : (l > lt ? first_cand(v, l * kS) : kNone32);   // candidate (X reused)
   });
-  for (int it = 0; it < (spec ? 6 : 1); ++it) {
+  for (int it = 0; it < (known ? 1 : 6); ++it) {
     wp.each([&](int l) {
       ChainPriv& c = cpriv(l);
       const uint32_t p = c.s == kNone32 ? c.X : kNone32;
@@ -584,17 +588,17 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
         c.s = p; c.X = e.X; c.crc = e.crc; c.k = e.k; c.vv = e.vv; c.w1 = e.w1; c.hs = e.hs; c.stat = e.stat;
       } else {
         const uint32_t nxt = p + 1 - (uint32_t)(l * kS);
-        c.X = (spec && nxt < (uint32_t)kS) ? first_cand(v, l * kS, nxt) : kNone32;
+        c.X = (!known && nxt < (uint32_t)kS) ? first_cand(v, l * kS, nxt) : kNone32;
       }
     });
-    if (!spec || !wp.ballot([&](int l) { return cpriv(l).s == kNone32 && cpriv(l).X != kNone32; })) break;
+    if (known || !wp.ballot([&](int l) { return cpriv(l).s == kNone32 && cpriv(l).X != kNone32; })) break;
   }
   wp.each([&](int l) { sh.s[l] = cpriv(l).s; });
   wp.stamp(10);
   // A chain may end inside the region on a terminal status (lean_terminal): tpos / tstat. Its last
   // entry's owner check then runs at a check-only "pseudo start" at tpos (rewritten like a start,
   // no tuple, not in `starts`).
-  if (!spec && wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) {
+  if (known && wp.from(lt, [&](int l) { return cpriv(l).s; }) == kNone32) {
     tstat = lean_terminal(v, xr);
     if (tstat == kCont) return LDB_DECLINE(2);
     tpos = xr;   // the chain enters on its terminal: nothing in the region is on it
@@ -684,7 +688,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       sh.s[l] = c.s;
     });
   }
-  const int L0 = spec ? (int)__builtin_ctzll(starts) : lt;
+  const int L0 = known ? lt : (int)__builtin_ctzll(starts);
   const uint32_t sL0 = wp.from(L0, [&](int l) { return cpriv(l).s; });
   const int z = starts ? 63 - (int)__builtin_clzll(starts) : L0;
   const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).s; });

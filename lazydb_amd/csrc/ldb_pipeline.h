@@ -32,6 +32,7 @@ struct Pipe {
   uint32_t* ctr;              // [0] fail count, [1] overflow, [2] repairs, [3] fast regions, [4] deferred
   uint64_t* tpos;             // [0] min terminal position, [1] its status (packed with position)
   uint64_t* blk;              // per kBlkRegions-region block: count sum (k_combine)
+  uint64_t* dyn;              // [0] K: entries of the equal-sized run k_uniform verified, [1] their size
   void* out;
   uint64_t cap;
   int kind;
@@ -39,6 +40,23 @@ struct Pipe {
 };
 
 constexpr int kBlkRegions = 256;   // regions per k_combine / k_compact workgroup
+
+// ---------------------------------------------------------------- the run prefix (k_uniform)
+// k_uniform verifies, in parallel, that the log starts with K entries that all have entry 0's header
+// bytes (so its size sz) and a correct CRC: the chain's first K entries are at k * sz. The region
+// pipeline then replays only from x0 = K * sz on, as if the file started there: it skips every
+// region before x0's region, takes x0 as the chain's entry point (where it used to take offset 0),
+// and emits its tuples after the K the run wrote. K = 0 (no run) is the plain pipeline.
+LDB_HD uint64_t run_k(const Pipe& p) { return p.dyn[0] == ~0ull ? 0ull : p.dyn[0]; }
+LDB_HD uint64_t chain_x0(const Pipe& p) { return run_k(p) * p.dyn[1]; }
+// first region of the replay; nreg when the header window at x0 is already unreadable (the replay
+// stops there with io.EOF, log_file.go:117-122, and no region has work)
+LDB_HD uint64_t first_region(const Pipe& p) {
+  const uint64_t x0 = chain_x0(p);
+  if (x0 && read_eof(p.len, p.io, (int64_t)x0, kMaxHeader)) return p.nreg;
+  const uint64_t r = x0 / kW;
+  return r < p.nreg ? r : p.nreg;
+}
 
 // Register-shift byte tables for k_combine (global memory, L2-resident): table t holds
 // T[q * 256 + b] = shift(b << 8q, n_t bytes) = (b << 8q) * x^(8 n_t) mod P, so a shift by n_t is
@@ -95,8 +113,72 @@ LDB_HD uint32_t region_len(const Pipe& p, uint64_t r) {
   return (uint32_t)((p.len - R0) < (uint64_t)kW ? (p.len - R0) : (uint64_t)kW);
 }
 
-// Link check of region r. Returns true when r's outgoing link is broken (or r == 0 does not
-// start at offset 0, reported by the caller as source -1).
+// The run's template: entry 0's header, decoded exactly as decodeHeader does (classify_entry,
+// log_entry.go:81-107 / log_file.go:116-139). An entry whose header bytes [4, hs) equal these decodes
+// to the same fields (every varint of a canonical header ends inside [5, hs)), so it has the same size.
+struct UniMemo {
+  uint32_t ok;          // entry 0 is a canonical, readable, non-sentinel entry with a CRC span
+  uint32_t hs, enc, stat, tx_stat, k, v;
+  uint32_t nw;          // header dwords compared (bytes [4, 4 + 4 nw) cover [4, hs))
+  int64_t expired_at;
+  uint64_t tx_id;
+  uint64_t sz;          // entry size hs + k + v
+  uint32_t w[9], msk[9];   // header bytes [4, 40) and the mask of those before hs
+};
+
+constexpr uint64_t kUniMaxSize = 1ull << 24;   // larger entries never form a run (32-bit batch offsets)
+
+template <class Fetch>
+LDB_HD UniMemo uni_memo(Fetch fetch, uint64_t len, int io) {
+  UniMemo m;
+  m.ok = 0;
+  const EntryInfo e = classify_entry(fetch, len, io, 0);
+  if (e.status != kCont || !e.h.canonical || e.h.size < 10 || e.h.size > kMaxHeader) return m;
+  if (e.size > kUniMaxSize || e.size < 16) return m;
+  m.hs = (uint32_t)e.h.size;
+  m.enc = (uint32_t)e.h.enc_size;
+  m.stat = e.h.stat;
+  m.tx_stat = e.h.tx_stat;
+  m.k = e.h.k_size;
+  m.v = e.h.v_size;
+  m.expired_at = e.h.expired_at;
+  m.tx_id = e.h.tx_id;
+  m.sz = e.size;
+  m.nw = (m.hs - 4 + 3) / 4;
+  for (int i = 0; i < 9; ++i) {
+    const int n = (int)m.hs - 4 - 4 * i;
+    m.msk[i] = n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * n)));
+    uint32_t w = 0;
+    for (int b = 0; b < 4; ++b) w |= (4 + 4 * i + b < kMaxHeader ? fetch(4 + 4 * i + b) : 0u) << (8 * b);
+    m.w[i] = w & m.msk[i];
+  }
+  m.ok = 1;
+  return m;
+}
+
+// ReadLogEntry(x) of a run member up to the CRC: the header window and key/value are readable
+// (log_file.go:117-122, 130-139), the header bytes equal the template's and the entry is not the
+// zero sentinel (:124-126). word(i) = little-endian dword at x + 4 i (i = 0: the stored crc).
+template <class Word>
+LDB_HD bool uni_header_ok(const UniMemo& m, Word word, uint64_t x, uint64_t len, int io) {
+  if (read_eof(len, io, (int64_t)x, kMaxHeader)) return false;
+  if (m.k || m.v) {
+    if (read_eof(len, io, (int64_t)(x + m.hs), (uint64_t)m.k + m.v)) return false;
+  } else if (word(0) == 0u) {
+    return false;   // crc == 0 && kSize == 0 && vSize == 0: ErrLogEndOfFile
+  }
+  uint32_t d = 0;
+  for (uint32_t i = 0; i < m.nw; ++i) d |= (word(1 + i) ^ m.w[i]) & m.msk[i];
+  return d == 0u;
+}
+
+LDB_HD uint64_t uni_pos(const UniMemo& m, uint64_t x) {
+  return (x & 0xFFFFFFFFFFull) | ((uint64_t)(m.hs & 0x3F) << 40) | ((uint64_t)(m.enc & 0x3F) << 46) |
+         ((uint64_t)(m.stat & 0xFF) << 52);
+}
+
+// Link check of region r. Returns true when r's outgoing link is broken (or the first region does not
+// start at the chain's entry point x0, reported by the caller as the virtual source first_region - 1).
 LDB_HD bool link_broken(const Pipe& p, uint64_t r) {
   if (p.rs[r].start == kNone64 || p.rs[r].status != kCont) return false;
   const uint64_t x = p.rs[r].exitp;
@@ -181,7 +263,8 @@ namespace ldb {
 // returns its new summary.  Returns the number of regions re-processed.
 template <class Rd, class FirstTerm, class Run>
 LDB_HD uint32_t repair(const Pipe& p, uint32_t nfail, Rd rd, FirstTerm first_term, Run run) {
-  int64_t done = -2;
+  const int64_t rf = (int64_t)first_region(p);   // source rf - 1: the chain's entry point x0
+  int64_t done = rf - 2;
   uint32_t repairs = 0;
   for (;;) {
     int64_t src = INT64_MAX;
@@ -191,7 +274,7 @@ LDB_HD uint32_t repair(const Pipe& p, uint32_t nfail, Rd rd, FirstTerm first_ter
     }
     if (src == INT64_MAX) break;
     if (first_term(done, src) >= 0) break;  // a verified region before src already ends the scan
-    uint64_t x = src < 0 ? 0 : rd.exitp((uint64_t)src);
+    uint64_t x = src < rf ? chain_x0(p) : rd.exitp((uint64_t)src);
     int64_t cur = src;
     bool stop = false;
     for (;;) {

@@ -251,6 +251,116 @@ __device__ __forceinline__ void copy_tables(uint32_t* tab, const uint32_t* gtab)
 #ifdef LDB_STAMPS
 __device__ uint64_t g_stamps[kStampSlots];
 #endif
+
+// ---------------------------------------------------------------- k_uniform
+// The run prefix (ldb_pipeline.h): lane = entry. Entry k of a run of equal-sized entries starts at
+// k * sz; each lane checks entry k's header against entry 0's (uni_header_ok) and CRC-32s its span
+// [x + 4, x + sz) in 8-byte steps from the span start (S-table steps, a byte-table tail), then
+// writes its tuple at out[k]. No region summary, link, scan or owner check is involved: each entry
+// is verified on its own, and K = the first entry that is not (atomicMin) bounds the prefix. The
+// region pipeline replays from K * sz. Bytes are read with buffer loads from a wave-uniform base:
+// out-of-range dwords read as zero, so nothing past the image is touched (a run member whose bytes
+// would cross `len` just fails and is left to the pipeline).
+constexpr int kUniWaves = 8;
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  const v4u32_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p) {
+  __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + 256];   // S table + byte table T8
+  __shared__ UniMemo sm;
+  {
+    const uint4* g = reinterpret_cast<const uint4*>(p.gtab + kTBOff);
+    uint4* t = reinterpret_cast<uint4*>(stab);
+    for (int i = threadIdx.x; i < 5120 / 4; i += blockDim.x) t[i] = g[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) stab[5120 + i] = p.gtab[kT8Off + i];
+  }
+  if (threadIdx.x == 0) {
+    struct G {
+      const uint8_t* q;
+      uint64_t len;
+      __device__ uint32_t operator()(int i) const { return (uint64_t)i < len ? q[i] : 0u; }
+    };
+    sm = uni_memo(G{p.img, p.len}, p.len, p.io);
+    if (!sm.ok) atomicMin((unsigned long long*)&p.dyn[0], 0ull);
+    else if (blockIdx.x == 0) p.dyn[1] = sm.sz;
+  }
+  __syncthreads();
+  if (!sm.ok) return;
+  const UniMemo& m = sm;
+  const uint32_t sz = (uint32_t)m.sz;
+  const uint64_t ncand = p.len / sz + 1;            // entry ncand - 1 always fails (its bytes pass len)
+  const uint64_t nbatch = (ncand + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t L = sz - 4, n8 = L >> 3, rem = L & 7;   // CRC span: n8 8-byte steps, then rem bytes
+  const uint32_t* T8 = stab + 5120;
+  for (uint64_t b = (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
+    if (b * 64 >= __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    const uint64_t k = b * 64 + (uint64_t)lane;
+    const uint64_t base = (b * 64 * (uint64_t)sz) & ~3ull;   // wave-uniform, dword aligned, <= x
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)min(p.len - base, (uint64_t)0xFFFFFFFFu));
+    const uint64_t x = k * sz;
+    const uint32_t rel = (uint32_t)(x - base);   // < 64 sz <= 2^30
+    const uint32_t hal = rel & ~3u, sh = rel & 3u;
+    bool ok = k < ncand;
+    uint32_t crc = 0;
+    if (ok) {
+      const uint4 h0 = ld16(rs, hal), h1 = ld16(rs, hal + 16), h2 = ld16(rs, hal + 32);
+      const uint32_t d[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
+      crc = funnel(d[1], d[0], sh);
+      ok = uni_header_ok(m, [&](int i) { return funnel(d[i + 1], d[i], sh); }, x, p.len, p.io);
+    }
+    const uint64_t okm = __ballot(ok ? 1 : 0);
+    if (okm) {
+      // CRC-32 of [x + 4, x + sz): register ~0, 8-byte steps, then the rem tail bytes
+      const uint32_t cal = hal + 4;   // dword-aligned start of the span's words (same byte shift sh)
+      uint32_t reg = 0xFFFFFFFFu;
+      uint4 cur = ld16(rs, cal);
+      const uint32_t nq = (n8 + 1) >> 1;
+      for (uint32_t q = 0; q < nq; ++q) {
+        const uint4 nx = ld16(rs, cal + 16 * (q + 1));
+        const uint32_t w0 = funnel(cur.y, cur.x, sh), w1 = funnel(cur.z, cur.y, sh);
+        const uint32_t w2 = funnel(cur.w, cur.z, sh), w3 = funnel(nx.x, cur.w, sh);
+        reg = crc_step8(stab, reg, w0, w1);
+        if (2 * q + 1 < n8) reg = crc_step8(stab, reg, w2, w3);
+        cur = nx;
+      }
+      if (rem) {   // bytes [8 n8, L) of the span: word pair at dword 2 n8 (uniform branch)
+        const uint4 t0 = ld16(rs, cal + 8 * n8);
+        uint64_t w = ((uint64_t)funnel(t0.z, t0.y, sh) << 32) | funnel(t0.y, t0.x, sh);
+        for (uint32_t i = 0; i < rem; ++i) {
+          reg = crc_byte(T8, reg, (uint32_t)(w & 0xFFu));
+          w >>= 8;
+        }
+      }
+      ok = ok && ~reg == crc;   // getEntryCrc == stored crc (log_file.go:141-143)
+    }
+    const uint64_t bad = __ballot((k < ncand && !ok) ? 1 : 0);
+    if (bad && lane == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * 64 + __builtin_ctzll(bad)));
+    if (ok && k < p.cap) {
+      if (p.kind == LDB_TUPLE_ENTRY) {
+        ldb_entry e;
+        e.offset = x;
+        e.expired_at = m.expired_at;
+        e.tx_id = m.tx_id;
+        e.crc = crc;
+        e.k_size = m.k;
+        e.v_size = m.v;
+        e.tx_stat = (uint16_t)m.tx_stat;
+        e.stat = (uint8_t)m.stat;
+        e.hdr_size = (uint8_t)m.hs;
+        e.enc_hdr_size = (uint8_t)m.enc;
+        e.pad_[0] = e.pad_[1] = e.pad_[2] = 0;
+        e.fid = p.fid;
+        reinterpret_cast<ldb_entry*>(p.out)[k] = e;
+      } else {
+        store_tuple(reinterpret_cast<ldb_index_tuple*>(p.out) + k, uni_pos(m, x), m.k, m.v);
+      }
+    }
+  }
+}
 // ---------------------------------------------------------------- k_scan_main
 __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   // CRC tables in a static LDS array: its address is a link-time constant, so every table read
@@ -270,13 +380,19 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   const uint32_t ring_lds = (uint32_t)(uintptr_t)smem + (uint32_t)(ring - smem);
   // each wavefront scans a contiguous run of regions in file order, so the chain state of one
   // region (ldb_chain.h) carries into the next
+  // the replay covers regions [rf, nreg): the run prefix (k_uniform) took everything before x0
+  const uint64_t rf = first_region(p), nr = p.nreg - rf;
   const uint64_t gw = (uint64_t)blockIdx.x * kWPB + wave, nw = (uint64_t)gridDim.x * kWPB;
-  const uint64_t per = (p.nreg + nw - 1) / nw;
-  const uint64_t rb = gw * per;
+  const uint64_t per = (nr + nw - 1) / nw;
+  const uint64_t rb = rf + gw * per;
   const uint64_t count = rb < p.nreg ? (p.nreg - rb < per ? p.nreg - rb : per) : 0;
   GpuWave wp{lane};
   ChainState st;
   chain_reset(st);
+  if (rb == rf && count) {   // the replay's entry point: known, its owner verified by the run prefix
+    st.on = 2;
+    st.x = chain_x0(p);
+  }
   uint32_t n_fast = 0;
   // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
   // has read it for the last time (buffer_free), so the DMA overlaps the summary, its stores and
@@ -442,16 +558,18 @@ __global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p) {
 // ---------------------------------------------------------------- k_link
 __global__ void k_link(Pipe p) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= p.nreg) return;
-  // fail_src holds nreg + 1 entries: one per region plus region 0's "does not start at 0"
+  const uint64_t rf = first_region(p);
+  if (r >= p.nreg || r < rf) return;
+  // fail_src holds nreg + 1 entries: one per region plus the first region's "does not start at the
+  // chain's entry point x0" (virtual source rf - 1)
   bool bad = link_broken(p, r);
   if (bad) {
     const uint32_t i = atomicAdd(&p.ctr[0], 1u);
     if (i <= p.nreg) p.fail_src[i] = (int64_t)r; else atomicOr(&p.ctr[5], 1u);
   }
-  if (r == 0 && p.rs[0].start != 0) {
+  if (r == rf && p.rs[rf].start != chain_x0(p)) {
     const uint32_t i = atomicAdd(&p.ctr[0], 1u);
-    if (i <= p.nreg) p.fail_src[i] = -1; else atomicOr(&p.ctr[5], 1u);
+    if (i <= p.nreg) p.fail_src[i] = (int64_t)rf - 1; else atomicOr(&p.ctr[5], 1u);
   }
 }
 
@@ -483,8 +601,9 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
   const int lane = threadIdx.x;
   GpuWave wp{lane};
   CohRd rd{&p};
+  const int64_t rf = (int64_t)first_region(p);
   auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
-    for (int64_t b = lo + 1; b <= hi; b += 64) {
+    for (int64_t b = lo + 1 > rf ? lo + 1 : rf; b <= hi; b += 64) {
       const int64_t r = b + lane;
       bool t = false;
       if (r >= 0 && r <= hi && (uint64_t)r < p.nreg) {
@@ -539,7 +658,7 @@ __global__ __launch_bounds__(256) void k_combine(Pipe p) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ uint64_t s_sum[256];
   uint64_t cnt = 0;
-  if (r < p.nreg) {
+  if (r < p.nreg && r >= first_region(p)) {
     const int32_t st = p.rs[r].status;
     const uint64_t start = p.rs[r].start;
     cnt = p.rs[r].count;
@@ -603,9 +722,27 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
   uint64_t tp = term_pos(T);
   int32_t ts = term_status(T);
   if (T == ~0ull) { tp = p.len; ts = LDB_ERR_MALFORMED; }  // unreachable: the chain always stops
+  const uint64_t rf = first_region(p), K = run_k(p);      // the run prefix's tuples are out[0, K)
+  const uint64_t b = blockIdx.x, r0 = b * kBlkRegions;
+  if (rf >= p.nreg) {   // the replay stops right after the run: io.EOF at x0 (log_file.go:117-122)
+    if (b == 0 && tid == 0) {
+      ldb_scan_result res;
+      res.status = LDB_EOF_WINDOW;
+      res.fid = p.fid;
+      res.n_entries = K;
+      res.end_off = chain_x0(p);
+      res.n_repairs = 0;
+      res.n_regions = 0;
+      res.n_fast = 0;
+      res.reserved_ = 0;
+      res.n_run = K;
+      if (K > p.cap) res.status = LDB_ERR_CAPACITY;
+      *p.result = res;
+    }
+    return;
+  }
   const uint64_t regT = tp / kW;                          // may be nreg when tp == len == nreg * kW
   const uint64_t lastR = regT < p.nreg ? regT : p.nreg - 1;
-  const uint64_t b = blockIdx.x, r0 = b * kBlkRegions;
   if (r0 > lastR) return;
   // base = sum of the counts of every earlier block (all their regions precede the terminal)
   uint64_t part = 0;
@@ -616,7 +753,7 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
   // this block's effective counts, exclusive scan
   const uint64_t r = r0 + tid;
   uint32_t c = 0;
-  if (r < p.nreg && r <= regT) {
+  if (r < p.nreg && r <= regT && r >= rf) {
     c = p.rs[r].count;
     // the terminal is this region's straddle-out entry failing its CRC
     if (r == regT && p.rs[r].status == kCont && (p.rs[r].sflag & kStraddle) && p.rs[r].soff == tp && c > 0) c -= 1;
@@ -640,6 +777,7 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
   if (tid == kBlkRegions - 1) s_off[kBlkRegions] = wbase + x;
   __syncthreads();
   const uint32_t total = s_off[kBlkRegions];
+  base += K;
   if (b == lastR / kBlkRegions && tid == 0) {
     const uint64_t n = base + total;
     ldb_scan_result res;
@@ -648,9 +786,10 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
     res.n_entries = n;
     res.end_off = tp;
     res.n_repairs = p.ctr[2];
-    res.n_regions = (uint32_t)p.nreg;
+    res.n_regions = (uint32_t)(p.nreg - rf);
     res.n_fast = p.ctr[3];
     res.reserved_ = 0;
+    res.n_run = K;
     if (n > p.cap) res.status = LDB_ERR_CAPACITY;
     if (p.ctr[5]) res.status = LDB_ERR_INTERNAL;   // a device-side index guard fired (never expected)
     if (p.ctr[1]) res.status = kOverflow;  // k_serial redoes the scan
@@ -681,7 +820,7 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
     const uint8_t* q;
     __device__ uint32_t operator()(int i) const { return q[i]; }
   };
-  uint64_t off = 0, n = 0;
+  uint64_t off = chain_x0(p), n = run_k(p);   // after the run prefix (0, 0 on the serial test path)
   int st;
   for (;;) {
     EntryInfo e;
@@ -717,6 +856,7 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
   res.n_regions = (uint32_t)p.nreg;
   res.n_fast = 0;
   res.reserved_ = 0;
+  res.n_run = run_k(p);
   *p.result = res;
 }
 
@@ -761,7 +901,7 @@ struct ldb_ctx {
   bool ws_ev_live = false;
   // kernel timing: one event triple per timed launch, recorded without host synchronisation and
   // resolved when the timing is queried (or when the pool is full)
-  struct EvTriple { hipEvent_t e0, e1, e2; };
+  struct EvTriple { hipEvent_t e0, eu, e1, e2; };   // start, after k_uniform, after k_scan_main, end
   std::vector<EvTriple> evs;
   size_t ev_used = 0;
   bool timing = false;
@@ -772,7 +912,7 @@ struct ldb_ctx {
   uint64_t h_out_cap = 0;
   ldb_scan_result* h_res = nullptr;
   hipStream_t h_stream = nullptr;
-  double t_main = 0, t_total = 0;
+  double t_run = 0, t_main = 0, t_total = 0;
   uint64_t t_n = 0;
   void* merge = nullptr;       // merge/GC workspace (ldb_merge.hip), created on first use
 };
@@ -786,9 +926,11 @@ static int resolve_timing(ldb_ctx* c) {
   for (size_t i = 0; i < c->ev_used; ++i) {
     const ldb_ctx::EvTriple& t = c->evs[i];
     if (hipEventSynchronize(t.e2) != hipSuccess) return LDB_ERR_HIP;
-    float a = 0, b = 0;
-    if (hipEventElapsedTime(&a, t.e0, t.e1) != hipSuccess || hipEventElapsedTime(&b, t.e0, t.e2) != hipSuccess)
+    float u = 0, a = 0, b = 0;
+    if (hipEventElapsedTime(&u, t.e0, t.eu) != hipSuccess || hipEventElapsedTime(&a, t.eu, t.e1) != hipSuccess ||
+        hipEventElapsedTime(&b, t.e0, t.e2) != hipSuccess)
       return LDB_ERR_HIP;
+    c->t_run += u;
     c->t_main += a;
     c->t_total += b;
     c->t_n += 1;
@@ -801,7 +943,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -819,6 +961,7 @@ WsLayout layout(uint64_t len) {
   // tpos (2 x u64, set by k_scan_main's first workgroup); take() rounds each field to 256 B
   L.o_ctr = take(32);
   L.o_tpos = take(16);
+  L.o_dyn = take(16);   // run prefix: K, entry size (k_uniform)
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1));
@@ -864,6 +1007,7 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.ctr = reinterpret_cast<uint32_t*>(w + L.o_ctr);
   p.tpos = reinterpret_cast<uint64_t*>(w + L.o_tpos);
   p.blk = reinterpret_cast<uint64_t*>(w + L.o_blk);
+  p.dyn = reinterpret_cast<uint64_t*>(w + L.o_dyn);
   p.out = out;
   p.cap = cap;
   p.kind = kind;
@@ -899,6 +1043,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
   if (serial || len < (uint64_t)kMaxHeader) {
     LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
+    LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0, 16, s));   // no run prefix: the walk starts at 0
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 0);
     LDB_HIP(hipGetLastError());
     return fence_ws(c, s);
@@ -909,6 +1054,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
       if (c->evs.size() < 4096) {
         ldb_ctx::EvTriple t{};
         LDB_HIP(hipEventCreate(&t.e0));
+        LDB_HIP(hipEventCreate(&t.eu));
         LDB_HIP(hipEventCreate(&t.e1));
         LDB_HIP(hipEventCreate(&t.e2));
         c->evs.push_back(t);
@@ -920,6 +1066,14 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
     ev = &c->evs[c->ev_used++];
     LDB_HIP(hipEventRecord(ev->e0, s));
   }
+  // the run prefix: K = ~0 until k_uniform lowers it to the first entry outside the run
+  LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0xFF, 16, s));
+  {
+    const uint64_t batches = len / 16 / 64 + 1;   // entries are >= 16 B in a run
+    const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 8);
+    hipLaunchKernelGGL(k_uniform, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p);
+  }
+  if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
   // persistent waves: exactly the workgroups that are resident at once (LDS-limited), so no
   // second dispatch round leaves a tail
   const int per_cu = LDB_BLOCKS_PER_CU > 0 ? LDB_BLOCKS_PER_CU
@@ -1017,6 +1171,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
   for (const ldb_ctx::EvTriple& t : c->evs) {
     (void)hipEventDestroy(t.e0);
+    (void)hipEventDestroy(t.eu);
     (void)hipEventDestroy(t.e1);
     (void)hipEventDestroy(t.e2);
   }
@@ -1167,10 +1322,20 @@ int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_t
   if (n) *n = c->t_n;
   if (enable >= 0) {
     c->timing = enable != 0;
-    c->t_main = c->t_total = 0;
+    c->t_run = c->t_main = c->t_total = 0;
     c->t_n = 0;
   }
   return LDB_OK;
+}
+
+int ldb_kernel_timing_split(ldb_ctx* c, int enable, double* avg_run_ms, double* avg_main_ms, double* avg_total_ms,
+                            uint64_t* n) {
+  if (!c) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  const int rc = resolve_timing(c);
+  if (rc != LDB_OK) return rc;
+  if (avg_run_ms) *avg_run_ms = c->t_n ? c->t_run / c->t_n : 0.0;
+  return ldb_kernel_timing(c, enable, avg_main_ms, avg_total_ms, n);
 }
 
 }  // extern "C"

@@ -242,3 +242,10 @@ class Engine:
         a, b, n = C.c_double(), C.c_double(), C.c_uint64()
         N.check(N.lib().ldb_kernel_timing(self.ctx, enable, C.byref(a), C.byref(b), C.byref(n)), "timing")
         return a.value, b.value, n.value
+
+    def timing_split(self, enable: int = -1):
+        """(avg k_uniform ms, avg k_scan_main ms, avg pipeline ms, launches) since the last reset."""
+        u, a, b, n = C.c_double(), C.c_double(), C.c_double(), C.c_uint64()
+        N.check(N.lib().ldb_kernel_timing_split(self.ctx, enable, C.byref(u), C.byref(a), C.byref(b), C.byref(n)),
+                "timing_split")
+        return u.value, a.value, b.value, n.value

@@ -175,14 +175,50 @@ struct Rd {
 
 }  // namespace
 
+// k_uniform on the CPU: the same template and header checks (ldb_pipeline.h), byte-wise CRC-32.
+// Writes the run's tuples and dyn = {K, size}.
+static void emu_uniform(const Emu& emu, const uint8_t* img, uint64_t len, int io, ldb_index_tuple* out, uint64_t cap,
+                        uint64_t* dyn) {
+  struct F {
+    const uint8_t* q;
+    uint64_t len;
+    uint32_t operator()(int i) const { return (uint64_t)i < len ? q[i] : 0u; }
+  };
+  const UniMemo m = uni_memo(F{img, len}, len, io);
+  dyn[0] = 0;
+  dyn[1] = 0;
+  if (!m.ok) return;
+  dyn[1] = m.sz;
+  const uint64_t ncand = len / m.sz + 1;
+  const uint32_t* T8 = emu.tab.data() + kT8Off;
+  uint64_t k = 0;
+  for (; k < ncand; ++k) {
+    const uint64_t x = k * m.sz;
+    auto word = [&](int i) -> uint32_t {
+      uint32_t w = 0;
+      for (int b = 0; b < 4; ++b) {
+        const uint64_t a = x + 4 * (uint64_t)i + b;
+        w |= (a < len ? (uint32_t)img[a] : 0u) << (8 * b);
+      }
+      return w;
+    };
+    if (!uni_header_ok(m, word, x, len, io)) break;
+    uint32_t reg = 0xFFFFFFFFu;
+    for (uint64_t a = x + 4; a < x + m.sz; ++a) reg = crc_byte(T8, reg, img[a]);
+    if (~reg != word(0)) break;
+    if (k < cap) { out[k].pos = uni_pos(m, x); out[k].k_size = m.k; out[k].v_size = m.v; }
+  }
+  dyn[0] = k;
+}
+
 // run_len: regions per wavefront run (k_scan_main gives each wave a contiguous run); 0 = every
-// region speculative (the pre-chain pipeline).
-extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
-                             ldb_scan_result* res, uint32_t* stats, uint64_t run_len) {
+// region speculative (the pre-chain pipeline). use_run: the run prefix (k_uniform) first.
+extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                           ldb_scan_result* res, uint32_t* stats, uint64_t run_len, int use_run) {
   Emu emu;
   const uint64_t nreg = std::max<uint64_t>(1, (len + kW - 1) / kW);
   const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
-  std::vector<uint64_t> blk(nblk, 0), tpos(2, ~0ull);
+  std::vector<uint64_t> blk(nblk, 0), tpos(2, ~0ull), dyn(2, 0);
   std::vector<RegionSum> rs(nreg);
   std::vector<uint32_t> ctr(4, 0);
   std::vector<ldb_index_tuple> scratch(nreg * (uint64_t)kRegionCap);
@@ -192,22 +228,33 @@ extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t 
   p.gtab = emu.tab.data(); p.xw = emu.xw.data(); p.gsh = emu.gsh.data();
   p.rs = rs.data();
   p.scratch = scratch.data(); p.fail_src = fail.data(); p.ctr = ctr.data(); p.tpos = tpos.data();
-  p.blk = blk.data(); p.out = out; p.cap = cap; p.kind = LDB_TUPLE_INDEX; p.result = res;
+  p.blk = blk.data(); p.out = out; p.cap = cap; p.kind = LDB_TUPLE_INDEX; p.result = res; p.dyn = dyn.data();
+  res->n_run = 0;
   if (len < (uint64_t)kMaxHeader) {
     // the kernels route tiny images to k_serial; mirror it
     res->status = LDB_EOF_WINDOW; res->fid = fid; res->n_entries = 0; res->end_off = 0; res->n_repairs = 0;
     res->n_regions = (uint32_t)nreg;
     return 0;
   }
+  if (use_run) emu_uniform(emu, img, len, io, out, cap, dyn.data());
+  const uint64_t rf = first_region(p), K = run_k(p), x0 = chain_x0(p);
+  res->n_run = K;
+  if (rf >= nreg) {   // k_compact: io.EOF right after the run
+    res->status = K > cap ? LDB_ERR_CAPACITY : LDB_EOF_WINDOW; res->fid = fid; res->n_entries = K; res->end_off = x0;
+    res->n_repairs = 0; res->n_regions = 0;
+    if (stats) { stats[0] = 0; stats[1] = 0; stats[2] = 0; }
+    return 0;
+  }
   // k_scan_main
   uint32_t n_fast = 0;
   if (run_len == 0) {
-    for (uint64_t r = 0; r < nreg; ++r) emu.run(p, r, kForceSpec);
+    for (uint64_t r = rf; r < nreg; ++r) emu.run(p, r, kForceSpec);
   } else {
     std::vector<uint64_t> deferred;
-    for (uint64_t r0 = 0; r0 < nreg; r0 += run_len) {   // k_scan_main
+    for (uint64_t r0 = rf; r0 < nreg; r0 += run_len) {   // k_scan_main
       ChainState st;
       chain_reset(st);
+      if (r0 == rf) { st.on = 2; st.x = x0; }   // as k_scan_main: the replay's entry point
       for (uint64_t r = r0; r < nreg && r < r0 + run_len; ++r) {
         if (emu.run_chained(p, r, st)) ++n_fast;
         else deferred.push_back(r);
@@ -216,7 +263,7 @@ extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t 
     for (uint64_t r : deferred) emu.run(p, r, kForceSpec);   // k_fallback
   }
   // k_link
-  for (uint64_t r = 0; r < nreg; ++r) {
+  for (uint64_t r = rf; r < nreg; ++r) {
     if (link_broken(p, r)) {
       fail[ctr[0]++] = (int64_t)r;
       if (getenv("LDB_EMU_DEBUG")) {
@@ -226,20 +273,20 @@ extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t 
                 (unsigned long long)m, (unsigned long long)rs[m].start, (long long)(rs[m].start - m * kW), rs[m].status);
       }
     }
-    if (r == 0 && rs[0].start != 0) fail[ctr[0]++] = -1;
+    if (r == rf && rs[rf].start != x0) fail[ctr[0]++] = (int64_t)rf - 1;
   }
   const uint32_t nfail = ctr[0];
   // k_repair
   if (nfail) {
     auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
-      for (int64_t r = std::max<int64_t>(lo + 1, 0); r <= hi && (uint64_t)r < nreg; ++r)
+      for (int64_t r = std::max<int64_t>(lo + 1, (int64_t)rf); r <= hi && (uint64_t)r < nreg; ++r)
         if (rs[r].status != kCont && rs[r].start != kNone64) return r;
       return -1;
     };
     ctr[2] = repair(p, nfail, Rd{&p}, first_term, [&](uint64_t r, uint32_t enter) { return emu.run(p, r, enter); });
   }
   // k_combine
-  for (uint64_t r = 0; r < nreg; ++r) {
+  for (uint64_t r = rf; r < nreg; ++r) {
     const int32_t st = rs[r].status;
     if (st == kOverflow) { ctr[1] = 1; continue; }
     blk[r / kBlkRegions] += rs[r].count;
@@ -257,8 +304,8 @@ extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t 
   if (T == ~0ull) return -101;
   const uint64_t tp = term_pos(T);
   const uint64_t regT = tp / kW;
-  uint64_t n = 0;
-  for (uint64_t r = 0; r < nreg && r <= regT; ++r) {
+  uint64_t n = K;
+  for (uint64_t r = rf; r < nreg && r <= regT; ++r) {
     uint64_t c = rs[r].count;
     if (r == regT && rs[r].status == kCont && (rs[r].sflag & kStraddle) && rs[r].soff == tp && c > 0) c -= 1;
     for (uint64_t j = 0; j < c; ++j)
@@ -270,9 +317,14 @@ extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t 
   res->n_entries = n;
   res->end_off = tp;
   res->n_repairs = ctr[2];
-  res->n_regions = (uint32_t)nreg;
+  res->n_regions = (uint32_t)(nreg - rf);
   if (stats) { stats[0] = nfail; stats[1] = ctr[2]; stats[2] = n_fast; }
   return 0;
+}
+
+extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                             ldb_scan_result* res, uint32_t* stats, uint64_t run_len) {
+  return emu_scan_ex(img, len, io, fid, out, cap, res, stats, run_len, 0);
 }
 
 extern "C" int emu_scan(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,

@@ -27,13 +27,13 @@ def test_library_exports_header_symbols():
     for sym in declared:
         assert hasattr(L, sym), sym
     assert set(N.EXPORTS) == declared
-    assert L.ldb_abi_version() == 1
+    assert L.ldb_abi_version() == 2
     assert N.status_str(-1) == "invalid crc"
 
 
 def test_struct_layouts_match_header():
     from lazydb_amd import _native as N
-    assert C.sizeof(N.ScanResult) == 40
+    assert C.sizeof(N.ScanResult) == 48
     assert N.INDEX_TUPLE.itemsize == 16 and N.ENTRY_TUPLE.itemsize == 48
     assert N.INDEX_TUPLE == coracle.INDEX_TUPLE and N.ENTRY_TUPLE == coracle.ENTRY_TUPLE
 
@@ -276,3 +276,77 @@ def test_emulated_predicted_starts(seed):
             res, tup, st = emu_scan(im, io, 64)
             ref, rt = coracle.scan(im, io)
             assert_same(res, tup, ref, rt)
+
+
+def emu_scan_run(img: np.ndarray, io: int, run_len: int = 64):
+    """The emulated pipeline with the run prefix (k_uniform) first."""
+    L = _emu()
+    if not hasattr(L.emu_scan_ex, "_typed"):
+        L.emu_scan_ex.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_uint32, C.c_void_p, C.c_uint64,
+                                  C.POINTER(coracle.ScanResult), C.c_void_p, C.c_uint64, C.c_int]
+        L.emu_scan_ex._typed = True
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    cap = img.size // 5 + 8
+    out = np.zeros(cap, coracle.INDEX_TUPLE)
+    res = coracle.ScanResult()
+    st = np.zeros(4, np.uint32)
+    rc = L.emu_scan_ex(img.ctypes.data if img.size else None, img.size, io, 0, out.ctypes.data, cap, C.byref(res),
+                       st.ctypes.data, run_len, 1)
+    assert rc == 0, rc
+    return res, out[: res.n_entries], st
+
+
+def _fixed_log(n, klen, vlen, seed, expired_at=0, tx_id=0, stat=0):
+    from oracle import pyoracle as P
+    rng = random.Random(seed)
+    out = bytearray()
+    for i in range(n):
+        out += P.encode_entry(P.Entry(key=bytes(rng.randrange(97, 123) for _ in range(klen)),
+                                      value=bytes(rng.randrange(48, 58) for _ in range(vlen)), k_size=klen,
+                                      v_size=vlen, expired_at=expired_at, tx_id=tx_id, stat=stat))
+    return out
+
+
+@pytest.mark.parametrize("shape", [(64, 256, 0, 0), (16, 100, 0, 0), (13, 70, 0, 0), (20, 33, 1700000000, 7),
+                                   (9, 9, 0, 0), (5, 0, 0, 0), (64, 256, 0, 1 << 40)])
+def test_emulated_run_prefix(shape):
+    """The run prefix (k_uniform, ldb_pipeline.h uni_*): equal-sized entries at the file start are
+    verified one per lane, and the region pipeline resumes at the first entry outside the run. Entry
+    sizes with every span length mod 8, long headers (a 5-byte ExpiredAt), a 6-byte TxID, tiny
+    entries; clean ends (exact, zero tail, short tail), corrupted entries at the run's start, middle
+    and end, a run followed by entries of another size, and both IOController rules."""
+    klen, vlen, exp, txid = shape
+    rng = random.Random(klen * 1000 + vlen)
+    run = _fixed_log(300, klen, vlen, rng.randrange(1 << 30), expired_at=exp, tx_id=txid)
+    esz = len(run) // 300
+    other = coracle.gen_log(40_000, 5, ksize=16, vsize=40)
+    tails = [b"", bytes(10), bytes(37), bytes(38), bytes(9000), bytes(other[0][: other[2]]) + bytes(300)]
+    for tail in tails:
+        base = np.frombuffer(bytes(run) + tail, np.uint8).copy()
+        variants = [base]
+        for k in (0, 150, 299):
+            for off in (0, 5, esz - 1):
+                im = base.copy()
+                im[k * esz + off] ^= 0x40
+                variants.append(im)
+        variants.append(base[: 150 * esz + 3].copy())
+        variants.append(base[: 299 * esz + 30].copy())
+        for im in variants:
+            for io in (0, 1):
+                res, tup, st = emu_scan_run(im, io)
+                ref, rt = coracle.scan(im, io)
+                assert_same(res, tup, ref, rt)
+
+
+def test_emulated_run_prefix_counts():
+    """A clean config-2-shaped log is covered by the run: every entry but none of the regions."""
+    img, n, end = coracle.gen_log(1 << 20, 3, ksize=64, vsize=256)
+    res, tup, st = emu_scan_run(img, 0)
+    ref, rt = coracle.scan(img, 0)
+    assert_same(res, tup, ref, rt)
+    assert res.n_run == n and res.n_regions <= 1
+    zipf = coracle.gen_log(1 << 20, 3, ksize=64, value_mode=1, zipf_max=512)[0]
+    res, tup, st = emu_scan_run(zipf, 0)
+    ref, rt = coracle.scan(zipf, 0)
+    assert_same(res, tup, ref, rt)
+    assert res.n_run < 50

@@ -106,8 +106,10 @@ def test_config2_1gib_full_parity(eng):
     ref, rt = coracle.scan(img)
     assert_same(res, tup, ref, rt)
     assert res.status == 2 and res.n_repairs == 0
-    # the chained fast path (ldb_chain.h) must carry the scan: a broken lane shuffle or check would
-    # only show up here, as every region silently falling back to the exact general routine
+    # the run prefix (k_uniform) must carry the equal-sized entries, and the chained fast path
+    # (ldb_chain.h) the rest: a broken check would only show up here, as the scan silently falling
+    # back to the exact general routine
+    assert res.n_run == n, (res.n_run, n)
     assert res.n_fast >= 0.9 * res.n_regions, (res.n_fast, res.n_regions)
 
 
@@ -180,3 +182,53 @@ def test_config3_8gib_full_parity(eng):
     assert_same(res, tup, ref, rt)
     assert ref.n_entries == n and int(rt["pos"][-1] & ((1 << 40) - 1)) > (1 << 33) - (128 << 10)
     assert res.status == 2 and res.n_repairs == 0
+
+
+def _fixed_log(n, klen, vlen, seed, expired_at=0, tx_id=0):
+    from oracle import pyoracle as P
+    rng = random.Random(seed)
+    out = bytearray()
+    for i in range(n):
+        out += P.encode_entry(P.Entry(key=bytes(rng.randrange(97, 123) for _ in range(klen)),
+                                      value=bytes(rng.randrange(48, 58) for _ in range(vlen)), k_size=klen,
+                                      v_size=vlen, expired_at=expired_at, tx_id=tx_id))
+    return bytes(out)
+
+
+@pytest.mark.parametrize("shape", [(64, 256, 0, 0), (16, 100, 0, 0), (13, 70, 0, 0), (20, 33, 1700000000, 7),
+                                   (9, 9, 0, 0), (64, 256, 0, 1 << 40)])
+def test_run_prefix_shapes(eng, shape):
+    """The run prefix (k_uniform): equal-sized entries at the file start, one per lane, then the
+    region pipeline from the first entry outside the run. Every span length mod 8, long headers,
+    clean and cut ends, corrupted entries at the run's start / middle / end, a run followed by
+    other entries; both IOController rules and both tuple kinds (k_uniform writes ldb_entry too)."""
+    klen, vlen, exp, txid = shape
+    rng = random.Random(klen * 7 + vlen)
+    n = 3000
+    run = _fixed_log(n, klen, vlen, rng.randrange(1 << 30), expired_at=exp, tx_id=txid)
+    esz = len(run) // n
+    other = coracle.gen_log(200_000, 6, ksize=16, vsize=40)
+    for tail in (b"", bytes(37), bytes(9000), bytes(other[0][: other[2]]) + bytes(300)):
+        base = np.frombuffer(run + tail, np.uint8).copy()
+        variants = [base, base[: 1500 * esz + 3].copy(), base[: (n - 1) * esz + 30].copy()]
+        for k in (0, 1, 700, n - 1):
+            im = base.copy()
+            im[k * esz + rng.choice([0, 5, esz - 1])] ^= 0x40
+            variants.append(im)
+        for im in variants:
+            d = to_dev(im)
+            for io in (0, 1):
+                for kind in (0, 1):
+                    res, tup = eng.scan_dev(d, io_type=io, kind=kind)
+                    ref, rt = coracle.scan(im, io, tuple_kind=kind)
+                    assert_same(res, tup, ref, rt, kind=kind)
+
+
+def test_run_prefix_capacity(eng):
+    """Fewer output slots than run entries: LDB_ERR_CAPACITY with the full count, the first cap
+    tuples exact."""
+    img, n, end = coracle.gen_log(4 << 20, 9, ksize=64, vsize=256)
+    res, tup = eng.scan_dev(to_dev(img), cap=1000)
+    ref, rt = coracle.scan(img)
+    assert res.status == -3 and res.n_entries == n and res.n_run == n
+    assert np.array_equal(tup["pos"], rt["pos"][:1000])

@@ -12,7 +12,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for k in ("k_scan_main", "k_link", "k_repair", "k_combine", "k_final", "k_compact", "k_serial", "k_fallback",
+    for k in ("k_uniform", "k_scan_main", "k_link", "k_repair", "k_combine", "k_final", "k_compact", "k_serial", "k_fallback",
               "k_locate", "k_insert", "k_live", "k_scan_reduce", "k_scan_tiles", "k_scan_write", "k_pack",
               "k_emit_copy"):
         if k in name:
@@ -49,8 +49,9 @@ def main(d: str) -> None:
                 extra = f"  -> {v * 1024 / 1e6:.1f} MB"
             print(f"  {cname:24s} {v:16.1f}{extra}")
             pmc.setdefault(k, {})[cname] = v
-    if "k_scan_main" in pmc and "FETCH_SIZE" in pmc["k_scan_main"]:
-        pmc["k_scan_main"]["hbm_read_bytes_per_launch"] = pmc["k_scan_main"]["FETCH_SIZE"] * 2 * 1024
+    for k in ("k_uniform", "k_scan_main"):
+        if k in pmc and "FETCH_SIZE" in pmc[k]:
+            pmc[k]["hbm_read_bytes_per_launch"] = pmc[k]["FETCH_SIZE"] * 2 * 1024
     with open(os.path.join(d, "pmc.json"), "w") as f:
         json.dump(pmc, f, indent=1, sort_keys=True)
 
