@@ -179,8 +179,8 @@ LDB_HD uint32_t multmodp(uint32_t a, uint32_t b) {
   return p;
 }
 
-// x^(8n) mod P (reflected); host side, used to build the shift tables.
-inline uint32_t x8n_modp(uint64_t n) {
+// x^(8n) mod P (reflected): the shift tables (host), the run prefix's combine tables (device).
+LDB_HD uint32_t x8n_modp(uint64_t n) {
   uint32_t p = 1u << 31;      // x^0
   uint32_t sq = 1u << 23;     // x^8
   while (n) {

@@ -126,7 +126,45 @@ struct UniMemo {
   uint32_t w[9], msk[9];   // header bytes [4, 40) and the mask of those before hs
 };
 
-constexpr uint64_t kUniMaxSize = 1ull << 24;   // larger entries never form a run (32-bit batch offsets)
+// k_uniform's slicing of a run member's CRC span [x + 4, x + sz), L = sz - 4 bytes: G lanes per entry
+// (a power of 2), lane j CRC-32s the P-byte window [x + 4 - t + j P, + P) from register 0 in S = P / 8
+// table steps, where t = G P - L. The windows tile [x + 4 - t, x + sz); every byte before the span
+// start is masked to zero (lane j masks its first min(P, max(0, t - j P)) bytes), and leading zeros
+// leave a zero register unchanged, so each lane holds the raw register of its piece of the span and a
+// tree combine over the group shifts by d P bytes at level d. The span's register from ~0 is then the
+// combined raw register ^ KL, KL = shift(~0, L). G is the smallest that keeps P <= 8 kUniSteps (a
+// lane's bytes stay in registers): fewer, longer windows amortise a batch's fixed cost best.
+constexpr int kUniSteps = 12;                            // 8-byte steps per lane at most
+constexpr int kUniLevels = 6;                            // combine levels (G <= 64)
+constexpr uint64_t kUniMaxSize = 4 + 64ull * 8 * kUniSteps;   // larger entries never form a run
+static_assert(kUniMaxSize - 4 < 2ull * kW && 8ull * kUniSteps << (kUniLevels - 1) <= (uint64_t)kW,
+              "uni_geometry reads its shifts from the x^(8n) table");
+
+struct UniGeo {
+  uint32_t ok, G, lg, P, S, t, KL, pad;
+};
+
+// xw[n] = x^(8n) mod P for n = 0..kW (the pipeline's table); L < 2 kW
+LDB_HD UniGeo uni_geometry(const uint32_t* xw, uint32_t L) {
+  UniGeo g{};
+  for (uint32_t lg = 0; lg < kUniLevels + 1; ++lg) {
+    const uint32_t G = 1u << lg;
+    const uint32_t P = ((L + G - 1) / G + 7) & ~7u;
+    if (P <= 8 * kUniSteps) {
+      g.ok = 1; g.G = G; g.lg = lg; g.P = P; g.S = P / 8; g.t = G * P - L;
+      const uint32_t xl = L <= (uint32_t)kW ? xw[L] : multmodp(xw[kW], xw[L - kW]);
+      g.KL = multmodp(xl, 0xFFFFFFFFu);
+      return g;
+    }
+  }
+  return g;
+}
+
+// bytes lane j of a group masks at its window's start
+LDB_HD uint32_t uni_lead(const UniGeo& g, uint32_t j) {
+  const uint32_t o = j * g.P;
+  return g.t > o ? (g.t - o < g.P ? g.t - o : g.P) : 0u;
+}
 
 template <class Fetch>
 LDB_HD UniMemo uni_memo(Fetch fetch, uint64_t len, int io) {

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -253,114 +254,253 @@ __device__ uint64_t g_stamps[kStampSlots];
 #endif
 
 // ---------------------------------------------------------------- k_uniform
-// The run prefix (ldb_pipeline.h): lane = entry. Entry k of a run of equal-sized entries starts at
-// k * sz; each lane checks entry k's header against entry 0's (uni_header_ok) and CRC-32s its span
-// [x + 4, x + sz) in 8-byte steps from the span start (S-table steps, a byte-table tail), then
-// writes its tuple at out[k]. No region summary, link, scan or owner check is involved: each entry
-// is verified on its own, and K = the first entry that is not (atomicMin) bounds the prefix. The
-// region pipeline replays from K * sz. Bytes are read with buffer loads from a wave-uniform base:
-// out-of-range dwords read as zero, so nothing past the image is touched (a run member whose bytes
-// would cross `len` just fails and is left to the pipeline).
-constexpr int kUniWaves = 8;
-typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
+// The run prefix (ldb_pipeline.h). Entry e of a run of equal-sized entries starts at e * sz; it is a
+// run member when its header bytes equal entry 0's (uni_header_ok) and its CRC is right. k_uniform
+// verifies all candidates in parallel and K = the first that fails (atomicMin) bounds the prefix; the
+// region pipeline replays from K * sz. No region summary, link, scan or owner check is involved.
+//
+// Entry-aligned slices (uni_geometry): a wave holds E = 64 / G whole entries, G lanes each. Lane j of
+// an entry loads its P-byte window [x + 4 - t + j P, + P) as <= kUniRows 16-B rows, all in flight at
+// once (a wave's rows cover its E entries' bytes contiguously, so every fetched line is consumed while
+// it is in L1), and runs S = P / 8 S-table steps from register 0 (lane 0 masks its first t bytes).
+// The group's registers are combined by a tree: at level d, lanes j = 2d - 1 (mod 2d) take the value
+// of lane j - d by DPP / permlane and shift it by d P bytes (a 4-lookup byte table built by
+// k_uniform_setup). The group's last lane ends with the raw register of the whole span, checks
+// raw ^ KL == ~crc and the header, and writes the tuple at out[e].
+//
+// Bytes are read with buffer loads from a wave-uniform base 512 B before the wave's first entry (so
+// no masked lead reaches below it), ranged to len rounded up to a dword: dwords past the
+// image read as zero, and the dword holding the image's last byte is real (the same 16-B granule the
+// staging DMA reads, ldb_scan.hip stage_dma). The first waves of the file (base 0) load dword by
+// dword, as their lead may start before byte 0 (those dwords read as zero, and are masked anyway).
+#ifndef LDB_UNI_WAVES
+#define LDB_UNI_WAVES 16
+#endif
+constexpr int kUniWaves = LDB_UNI_WAVES;
+struct UniSetup {
+  UniMemo m;
+  UniGeo g;
+};
+constexpr uint64_t kUniSetupBytes = 1024;   // UniSetup, then kUniLevels combine tables of 1024 words
+constexpr uint64_t kUniTabWords = kUniLevels * 1024;
+static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
+static_assert(kTBOff == 0, "k_uniform stages the S table at LDS word 0");
 __device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-  const v4u32_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
-__global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p) {
-  __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + 256];   // S table + byte table T8
-  __shared__ UniMemo sm;
-  {
-    const uint4* g = reinterpret_cast<const uint4*>(p.gtab + kTBOff);
-    uint4* t = reinterpret_cast<uint4*>(stab);
-    for (int i = threadIdx.x; i < 5120 / 4; i += blockDim.x) t[i] = g[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) stab[5120 + i] = p.gtab[kT8Off + i];
-  }
+__device__ __forceinline__ uint32_t ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+}
+
+// One workgroup: entry 0's memo, the slicing, KL and the combine tables (shift by 2^i P bytes). Entry
+// 0's and entry 1's header windows are staged into LDS by one coalesced load each (the decode is a
+// chain of dependent byte reads); when entry 1 is not a run member the prefix is skipped outright
+// (K = 0: the region pipeline from offset 0 -- the same scan, without a run of one). Shifts come from
+// the x^(8n) table (n <= kW) instead of a serial square-and-multiply.
+__global__ __launch_bounds__(1024) void k_uniform_setup(Pipe p, UniSetup* us, uint32_t* utab) {
+  __shared__ UniSetup su;
+  __shared__ uint32_t xn[kUniLevels];
+  __shared__ uint32_t win[2][16];   // bytes [0, 64) and [sz, sz + 64) of the image, zero past len
+  struct F {
+    const uint8_t* q;
+    uint64_t len;
+    __device__ uint32_t operator()(int i) const { return (uint64_t)i < len ? q[i] : 0u; }
+  };
+  auto stage = [&](int w, uint64_t at) {   // dword-granular, exact at len
+    if (threadIdx.x < 64) {
+      const uint64_t a = at + threadIdx.x;
+      reinterpret_cast<uint8_t*>(win[w])[threadIdx.x] = a < p.len ? p.img[a] : 0;
+    }
+  };
+  stage(0, 0);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    struct G {
-      const uint8_t* q;
-      uint64_t len;
-      __device__ uint32_t operator()(int i) const { return (uint64_t)i < len ? q[i] : 0u; }
-    };
-    sm = uni_memo(G{p.img, p.len}, p.len, p.io);
-    if (!sm.ok) atomicMin((unsigned long long*)&p.dyn[0], 0ull);
-    else if (blockIdx.x == 0) p.dyn[1] = sm.sz;
+    const uint8_t* h = reinterpret_cast<const uint8_t*>(win[0]);
+    su.m = uni_memo([&](int i) -> uint32_t { return i < 64 ? h[i] : 0u; }, p.len, p.io);
+    su.g = su.m.ok ? uni_geometry(p.xw, (uint32_t)(su.m.sz - 4)) : UniGeo{};
   }
   __syncthreads();
-  if (!sm.ok) return;
-  const UniMemo& m = sm;
-  const uint32_t sz = (uint32_t)m.sz;
-  const uint64_t ncand = p.len / sz + 1;            // entry ncand - 1 always fails (its bytes pass len)
-  const uint64_t nbatch = (ncand + 63) / 64;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t L = sz - 4, n8 = L >> 3, rem = L & 7;   // CRC span: n8 8-byte steps, then rem bytes
-  const uint32_t* T8 = stab + 5120;
+  if (su.g.ok) stage(1, su.m.sz);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (su.g.ok) {
+      const uint8_t* h = reinterpret_cast<const uint8_t*>(win[1]);
+      auto word = [&](int i) -> uint32_t {
+        return (uint32_t)h[4 * i] | ((uint32_t)h[4 * i + 1] << 8) | ((uint32_t)h[4 * i + 2] << 16) |
+               ((uint32_t)h[4 * i + 3] << 24);
+      };
+      if (!uni_header_ok(su.m, word, su.m.sz, p.len, p.io)) su.g.ok = 0;
+    }
+    if (su.g.ok) {
+      p.dyn[1] = su.m.sz;
+      for (uint32_t i = 0; i < su.g.lg; ++i) xn[i] = p.xw[su.g.P << i];
+    } else {
+      p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
+    }
+    *us = su;
+  }
+  __syncthreads();
+  if (!su.g.ok) return;
+  for (uint32_t e = threadIdx.x; e < su.g.lg * 1024u; e += blockDim.x)
+    utab[e] = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
+}
+
+// Combine level D of the group's tree: lanes j = 2D - 1 (mod 2D) (bit log2 D of `sel`) take lane
+// j - D's register shifted by D P bytes. Branch-free per lane: the shifted value is masked in.
+// Combine level D of the group's tree: lanes j = 2D - 1 (mod 2D) take lane j - D's register shifted
+// by D P bytes. c = ~j & (j + 1) is 2^(trailing ones of j): lane j combines at level D iff c > D.
+// Branch-free per lane (the shifted value is masked in).
+template <int D>
+__device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32_t G, uint32_t c, uint32_t& reg) {
+  if ((uint32_t)D >= G) return;   // wave-uniform
+  wp.shfl_up<D>([&](int) { return reg; }, [&](int, uint32_t y, bool) {
+    const int32_t q = (int32_t)(c / (2 * D));   // > 0 iff c > D (c is a power of 2)
+    const uint32_t z = T[y & 0xFFu] ^ T[256 + ((y >> 8) & 0xFFu)] ^ T[512 + ((y >> 16) & 0xFFu)] ^ T[768 + (y >> 24)];
+    reg ^= z & (uint32_t)((q | -q) >> 31);
+  });
+}
+
+// One wave's share of the run prefix, S steps per lane (a compile-time count: the rows stay in
+// registers with static indices and the step loop has no per-step branch).
+template <int S>
+__device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint32_t* stab, int lane, int wave) {
+  constexpr int R = (2 * S + 1 + 3) / 4;   // 16-B rows per lane
+  const uint32_t sz = (uint32_t)su.m.sz, G = su.g.G, lg = su.g.lg, P = su.g.P, t = su.g.t, KL = su.g.KL;
+  const uint32_t E = 64u >> lg;
+  const uint64_t ncand = p.len / sz + 1;   // entry ncand - 1 always fails (its bytes pass len)
+  const uint64_t nbatch = (ncand + E - 1) / E;
+  const uint32_t j = (uint32_t)lane & (G - 1);
+  const bool last = j == G - 1;
+  const uint32_t lead0 = uni_lead(su.g, j);   // bytes lane j masks at its window's start
+  const uint32_t* T = stab + 5120;
+  GpuWave wp{lane};
   for (uint64_t b = (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
-    if (b * 64 >= __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-    const uint64_t k = b * 64 + (uint64_t)lane;
-    const uint64_t base = (b * 64 * (uint64_t)sz) & ~3ull;   // wave-uniform, dword aligned, <= x
-    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)min(p.len - base, (uint64_t)0xFFFFFFFFu));
-    const uint64_t x = k * sz;
-    const uint32_t rel = (uint32_t)(x - base);   // < 64 sz <= 2^30
-    const uint32_t hal = rel & ~3u, sh = rel & 3u;
-    bool ok = k < ncand;
+    if (b * E >= __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    // Opaque per-batch copies: the uniform step / level conditions and the lane masks derived from
+    // them are evaluated inside the batch, not hoisted out of the loop as a bank of held SGPR masks.
+    uint32_t tt = __builtin_amdgcn_readfirstlane(t), GG = __builtin_amdgcn_readfirstlane(G), c = ~j & (j + 1), lead = lead0;
+    asm volatile("" : "+s"(tt), "+s"(GG), "+v"(c), "+v"(lead));
+    const uint64_t e = b * E + ((uint32_t)lane >> lg);
+    const uint64_t x = e * sz;
+    const uint64_t b0 = b * E * sz;
+    const uint64_t base = b0 >= 512 ? (b0 - 512) & ~15ull : 0;   // wave-uniform; the lead t < 8 G <= 512
+    const uint64_t nrec = (p.len - base + 3) & ~3ull;
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)min(nrec, (uint64_t)0xFFFFFFFFu));
+    // the group's last lane: the header (stored crc and bytes [4, 40)), in flight with the rows
+    const uint32_t hx = (uint32_t)(x - base), ha = hx & ~3u, hsh = hx & 3u;
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
+    if (last) { h0 = ld16(rs, ha); h1 = ld16(rs, ha + 16); h2 = ld16(rs, ha + 32); }
+    const int32_t ws = (int32_t)hx + 4 - (int32_t)t + (int32_t)(j * P);   // < 0 only when base = 0
+    const uint32_t a = (uint32_t)ws & ~3u, sh = (uint32_t)ws & 3u;
+    uint32_t d[4 * R];
+    if (base) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint4 q = ld16(rs, a + 16 * r);
+        d[4 * r] = q.x; d[4 * r + 1] = q.y; d[4 * r + 2] = q.z; d[4 * r + 3] = q.w;
+      }
+    } else {   // dwords before byte 0 get an out-of-range offset (no folded immediate can wrap them back)
+#pragma unroll
+      for (int i = 0; i < 4 * R; ++i) {
+        const int32_t o = (int32_t)a + 4 * i;
+        d[i] = ld4(rs, o < 0 ? kDrop : (uint32_t)o);
+      }
+    }
+    // lane j's window: S steps from register 0, lane 0's first t bytes masked
+    uint32_t reg = 0;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      uint32_t w0 = funnel(d[2 * k + 1], d[2 * k], sh), w1 = funnel(d[2 * k + 2], d[2 * k + 1], sh);
+      if ((uint32_t)(8 * k) < tt) {   // wave-uniform
+        // masked bytes from this step's start (lane 0 only): keep bytes >= n of the 8. The opaque
+        // copy keeps the compiler from hoisting every step's mask out of the batch loop.
+        uint32_t ld = lead;
+        asm volatile("" : "+v"(ld));
+        const uint32_t n = ld > 8u * k ? ld - 8u * k : 0u;
+        w0 &= n >= 4 ? 0u : 0xFFFFFFFFu << (8 * n);
+        w1 &= n >= 8 ? 0u : (n > 4 ? 0xFFFFFFFFu << (8 * (n - 4)) : 0xFFFFFFFFu);
+      }
+      reg = crc_step8(stab, reg, w0, w1);
+    }
+    uni_level<1>(wp, T, GG, c, reg);
+    uni_level<2>(wp, T + 1024, GG, c, reg);
+    uni_level<4>(wp, T + 2048, GG, c, reg);
+    uni_level<8>(wp, T + 3072, GG, c, reg);
+    uni_level<16>(wp, T + 4096, GG, c, reg);
+    uni_level<32>(wp, T + 5120, GG, c, reg);
+    // the header: bytes [4, hs) against the memo's (uni_header_ok). The memo is read from LDS through
+    // an opaque offset, so its words stay per-batch VGPR loads instead of SGPRs held across the loop.
+    bool ok = false;
     uint32_t crc = 0;
-    if (ok) {
-      const uint4 h0 = ld16(rs, hal), h1 = ld16(rs, hal + 16), h2 = ld16(rs, hal + 32);
-      const uint32_t d[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
-      crc = funnel(d[1], d[0], sh);
-      ok = uni_header_ok(m, [&](int i) { return funnel(d[i + 1], d[i], sh); }, x, p.len, p.io);
+    if (last && e < ncand) {
+      const uint32_t hd[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
+      uint32_t z = 0;
+      asm volatile("" : "+v"(z));
+      const UniMemo* mv = &su.m + z;
+      crc = funnel(hd[1], hd[0], hsh);
+      ok = !read_eof(p.len, p.io, (int64_t)x, kMaxHeader);
+      if (mv->k || mv->v) ok = ok && !read_eof(p.len, p.io, (int64_t)(x + mv->hs), (uint64_t)mv->k + mv->v);
+      else ok = ok && crc != 0u;   // crc == 0 && kSize == 0 && vSize == 0: ErrLogEndOfFile
+      uint32_t diff = 0;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) diff |= (funnel(hd[i + 2], hd[i + 1], hsh) ^ mv->w[i]) & mv->msk[i];
+      ok = ok && diff == 0u && (reg ^ KL) == ~crc;   // getEntryCrc == stored crc (log_file.go:141-143)
     }
-    const uint64_t okm = __ballot(ok ? 1 : 0);
-    if (okm) {
-      // CRC-32 of [x + 4, x + sz): register ~0, 8-byte steps, then the rem tail bytes
-      const uint32_t cal = hal + 4;   // dword-aligned start of the span's words (same byte shift sh)
-      uint32_t reg = 0xFFFFFFFFu;
-      uint4 cur = ld16(rs, cal);
-      const uint32_t nq = (n8 + 1) >> 1;
-      for (uint32_t q = 0; q < nq; ++q) {
-        const uint4 nx = ld16(rs, cal + 16 * (q + 1));
-        const uint32_t w0 = funnel(cur.y, cur.x, sh), w1 = funnel(cur.z, cur.y, sh);
-        const uint32_t w2 = funnel(cur.w, cur.z, sh), w3 = funnel(nx.x, cur.w, sh);
-        reg = crc_step8(stab, reg, w0, w1);
-        if (2 * q + 1 < n8) reg = crc_step8(stab, reg, w2, w3);
-        cur = nx;
-      }
-      if (rem) {   // bytes [8 n8, L) of the span: word pair at dword 2 n8 (uniform branch)
-        const uint4 t0 = ld16(rs, cal + 8 * n8);
-        uint64_t w = ((uint64_t)funnel(t0.z, t0.y, sh) << 32) | funnel(t0.y, t0.x, sh);
-        for (uint32_t i = 0; i < rem; ++i) {
-          reg = crc_byte(T8, reg, (uint32_t)(w & 0xFFu));
-          w >>= 8;
-        }
-      }
-      ok = ok && ~reg == crc;   // getEntryCrc == stored crc (log_file.go:141-143)
-    }
-    const uint64_t bad = __ballot((k < ncand && !ok) ? 1 : 0);
-    if (bad && lane == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * 64 + __builtin_ctzll(bad)));
-    if (ok && k < p.cap) {
+    const uint64_t bad = __ballot((last && e < ncand && !ok) ? 1 : 0);
+    if (bad && lane == 0)
+      atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
+    if (ok && e < p.cap) {
+      uint32_t z = 0;
+      asm volatile("" : "+v"(z));
+      const UniMemo& m = *(&su.m + z);
       if (p.kind == LDB_TUPLE_ENTRY) {
-        ldb_entry e;
-        e.offset = x;
-        e.expired_at = m.expired_at;
-        e.tx_id = m.tx_id;
-        e.crc = crc;
-        e.k_size = m.k;
-        e.v_size = m.v;
-        e.tx_stat = (uint16_t)m.tx_stat;
-        e.stat = (uint8_t)m.stat;
-        e.hdr_size = (uint8_t)m.hs;
-        e.enc_hdr_size = (uint8_t)m.enc;
-        e.pad_[0] = e.pad_[1] = e.pad_[2] = 0;
-        e.fid = p.fid;
-        reinterpret_cast<ldb_entry*>(p.out)[k] = e;
+        ldb_entry en;
+        en.offset = x;
+        en.expired_at = m.expired_at;
+        en.tx_id = m.tx_id;
+        en.crc = crc;
+        en.k_size = m.k;
+        en.v_size = m.v;
+        en.tx_stat = (uint16_t)m.tx_stat;
+        en.stat = (uint8_t)m.stat;
+        en.hdr_size = (uint8_t)m.hs;
+        en.enc_hdr_size = (uint8_t)m.enc;
+        en.pad_[0] = en.pad_[1] = en.pad_[2] = 0;
+        en.fid = p.fid;
+        reinterpret_cast<ldb_entry*>(p.out)[e] = en;
       } else {
-        store_tuple(reinterpret_cast<ldb_index_tuple*>(p.out) + k, uni_pos(m, x), m.k, m.v);
+        store_tuple(reinterpret_cast<ldb_index_tuple*>(p.out) + e, uni_pos(m, x), m.k, m.v);
       }
     }
   }
 }
+
+__global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, const UniSetup* us, const uint32_t* utab) {
+  __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + kUniTabWords];   // S table, combine tables
+  __shared__ UniSetup su;
+  if (threadIdx.x == 0) su = *us;
+  __syncthreads();
+  if (!su.g.ok) return;
+  {
+    const uint4* g = reinterpret_cast<const uint4*>(p.gtab);
+    uint4* t = reinterpret_cast<uint4*>(stab);
+    for (int i = threadIdx.x; i < 5120 / 4; i += blockDim.x) t[i] = g[i];
+    const uint4* u = reinterpret_cast<const uint4*>(utab);
+    for (int i = threadIdx.x; i < (int)su.g.lg * 256; i += blockDim.x) t[5120 / 4 + i] = u[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
+#define LDB_UNI_CASE(n) case n: uni_waves<n>(p, su, stab, lane, wave); break;
+    LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
+    LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
+#undef LDB_UNI_CASE
+    default: break;
+  }
+}
+static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
 // ---------------------------------------------------------------- k_scan_main
 __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   // CRC tables in a static LDS array: its address is a link-time constant, so every table read
@@ -912,6 +1052,12 @@ struct ldb_ctx {
   uint64_t h_out_cap = 0;
   ldb_scan_result* h_res = nullptr;
   hipStream_t h_stream = nullptr;
+  // host-image copies (ldb_scan_file): chunks dealt round-robin over n_cp streams, so several DMA
+  // engines pull from a registered mapping at once (LDB_H2D_STREAMS, default 2)
+  static constexpr int kMaxCp = 4;
+  int n_cp = 0;
+  hipStream_t cp[kMaxCp] = {};
+  hipEvent_t cp_ev[kMaxCp] = {};
   double t_run = 0, t_main = 0, t_total = 0;
   uint64_t t_n = 0;
   void* merge = nullptr;       // merge/GC workspace (ldb_merge.hip), created on first use
@@ -943,7 +1089,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_uni, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -962,6 +1108,7 @@ WsLayout layout(uint64_t len) {
   L.o_ctr = take(32);
   L.o_tpos = take(16);
   L.o_dyn = take(16);   // run prefix: K, entry size (k_uniform)
+  L.o_uni = take(kUniSetupBytes + 4 * kUniTabWords);   // run prefix: memo, slicing, combine tables
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1));
@@ -1069,9 +1216,13 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   // the run prefix: K = ~0 until k_uniform lowers it to the first entry outside the run
   LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0xFF, 16, s));
   {
-    const uint64_t batches = len / 16 / 64 + 1;   // entries are >= 16 B in a run
-    const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 8);
-    hipLaunchKernelGGL(k_uniform, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p);
+    UniSetup* us = reinterpret_cast<UniSetup*>(c->ws + L.o_uni);
+    uint32_t* utab = reinterpret_cast<uint32_t*>(c->ws + L.o_uni + kUniSetupBytes);
+    hipLaunchKernelGGL(k_uniform_setup, dim3(1), dim3(1024), 0, s, p, us, utab);
+    const uint64_t batches = len / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
+    const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2);
+    hipLaunchKernelGGL(k_uniform, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, (const UniSetup*)us,
+                       (const uint32_t*)utab);
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
   // persistent waves: exactly the workgroups that are resident at once (LDS-limited), so no
@@ -1167,6 +1318,10 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->h_out) (void)hipFree(c->h_out);
   if (c->h_res) (void)hipFree(c->h_res);
   if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
+  for (int i = 0; i < c->n_cp; ++i) {
+    if (c->cp[i]) (void)hipStreamDestroy(c->cp[i]);
+    if (c->cp_ev[i]) (void)hipEventDestroy(c->cp_ev[i]);
+  }
   if (c->merge) ldb_merge_release_(c->merge);
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
   for (const ldb_ctx::EvTriple& t : c->evs) {
@@ -1256,16 +1411,44 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
   }
   if (!c->h_res && hipMalloc(&c->h_res, sizeof(ldb_scan_result)) != hipSuccess) return LDB_ERR_NOMEM;
   hipStream_t s = c->h_stream;
-  // Host buffers are caller-owned pageable memory (a Go slice / mmap): only synchronous copies
-  // touch them, so no runtime staging work can outlive this call.
-  if (len && hipMemcpy(c->h_img, h_image, len, hipMemcpyHostToDevice) != hipSuccess) return LDB_ERR_HIP;
-  int rc = enqueue_scan(c, c->h_img, len, fid, io_type, tuple_kind, c->h_out, cap, c->h_res, s, false);
-  if (rc != LDB_OK) return rc;
-  if (hipStreamSynchronize(s) != hipSuccess) return LDB_ERR_HIP;
+  if (!c->n_cp) {
+    const char* e = getenv("LDB_H2D_STREAMS");
+    const int want = std::min(std::max(e ? atoi(e) : 2, 1), (int)ldb_ctx::kMaxCp);
+    for (int i = 0; i < want; ++i) {
+      if (hipStreamCreateWithFlags(&c->cp[i], hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&c->cp_ev[i], hipEventDisableTiming) != hipSuccess)
+        return LDB_ERR_HIP;
+      c->n_cp = i + 1;
+    }
+  }
+  // The image goes up in 64 MiB chunks dealt over the copy streams; the scan stream waits for all
+  // of them. Every stream is drained before the call returns, so no copy outlives the caller's
+  // buffer (a Go slice or an mmap'd file).
+  constexpr uint64_t kChunk = 64ull << 20;
+  int rc = LDB_OK;
+  uint64_t i = 0;
+  for (uint64_t off = 0; off < len && rc == LDB_OK; off += kChunk, ++i) {
+    const uint64_t nb = std::min(kChunk, len - off);
+    if (hipMemcpyAsync(c->h_img + off, h_image + off, nb, hipMemcpyHostToDevice, c->cp[i % c->n_cp]) != hipSuccess)
+      rc = LDB_ERR_HIP;
+  }
+  for (int j = 0; j < c->n_cp && rc == LDB_OK; ++j)
+    if (hipEventRecord(c->cp_ev[j], c->cp[j]) != hipSuccess || hipStreamWaitEvent(s, c->cp_ev[j], 0) != hipSuccess)
+      rc = LDB_ERR_HIP;
+  if (rc == LDB_OK) rc = enqueue_scan(c, c->h_img, len, fid, io_type, tuple_kind, c->h_out, cap, c->h_res, s, false);
+  for (int j = 0; j < c->n_cp; ++j) (void)hipStreamSynchronize(c->cp[j]);
+  if (rc != LDB_OK) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
   ldb_scan_result res;
-  if (hipMemcpy(&res, c->h_res, sizeof(res), hipMemcpyDeviceToHost) != hipSuccess) return LDB_ERR_HIP;
+  if (hipMemcpyAsync(&res, c->h_res, sizeof(res), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return LDB_ERR_HIP;
   const uint64_t n = std::min<uint64_t>(res.n_entries, cap);
-  if (n && hipMemcpy(h_out, c->h_out, n * tsz, hipMemcpyDeviceToHost) != hipSuccess) return LDB_ERR_HIP;
+  if (n && (hipMemcpyAsync(h_out, c->h_out, n * tsz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess))
+    return LDB_ERR_HIP;
   *h_result = res;
   return LDB_OK;
 }

@@ -177,6 +177,10 @@ struct Rd {
 
 // k_uniform on the CPU: the same template and header checks (ldb_pipeline.h), byte-wise CRC-32.
 // Writes the run's tuples and dyn = {K, size}.
+// k_uniform: the same verdicts, CRC-32 by the kernel's entry-aligned slices (uni_geometry): lane j's
+// window from register 0 with its masked lead, then the group's tree combine with byte-table shifts,
+// then raw ^ KL against ~crc. Bytes of the image's last partial dword are real (the kernel's buffer
+// range is len rounded up to a dword); bytes past len read as zero and are never used by a member.
 static void emu_uniform(const Emu& emu, const uint8_t* img, uint64_t len, int io, ldb_index_tuple* out, uint64_t cap,
                         uint64_t* dyn) {
   struct F {
@@ -188,24 +192,53 @@ static void emu_uniform(const Emu& emu, const uint8_t* img, uint64_t len, int io
   dyn[0] = 0;
   dyn[1] = 0;
   if (!m.ok) return;
+  const UniGeo g = uni_geometry(emu.xw.data(), (uint32_t)(m.sz - 4));
+  if (!g.ok) return;
   dyn[1] = m.sz;
+  std::vector<uint32_t> ct((size_t)g.lg * 1024);   // k_uniform_setup's combine tables
+  for (uint32_t i = 0; i < g.lg; ++i) {
+    const uint32_t xn = x8n_modp((uint64_t)g.P << i);
+    for (uint32_t e = 0; e < 1024; ++e) ct[i * 1024 + e] = multmodp(xn, (e & 255u) << (8 * (e >> 8)));
+  }
+  auto byte = [&](int64_t a) -> uint32_t { return a >= 0 && (uint64_t)a < len ? img[a] : 0u; };
+  {   // k_uniform_setup: no run unless entry 1 has the memo's header too
+    auto word1 = [&](int i) -> uint32_t {
+      uint32_t w = 0;
+      for (int b = 0; b < 4; ++b) w |= byte((int64_t)(m.sz + 4 * (uint64_t)i + b)) << (8 * b);
+      return w;
+    };
+    if (!uni_header_ok(m, word1, m.sz, len, io)) return;
+  }
   const uint64_t ncand = len / m.sz + 1;
-  const uint32_t* T8 = emu.tab.data() + kT8Off;
   uint64_t k = 0;
+  std::vector<uint32_t> v(g.G);
   for (; k < ncand; ++k) {
     const uint64_t x = k * m.sz;
     auto word = [&](int i) -> uint32_t {
       uint32_t w = 0;
-      for (int b = 0; b < 4; ++b) {
-        const uint64_t a = x + 4 * (uint64_t)i + b;
-        w |= (a < len ? (uint32_t)img[a] : 0u) << (8 * b);
-      }
+      for (int b = 0; b < 4; ++b) w |= byte((int64_t)(x + 4 * (uint64_t)i + b)) << (8 * b);
       return w;
     };
     if (!uni_header_ok(m, word, x, len, io)) break;
-    uint32_t reg = 0xFFFFFFFFu;
-    for (uint64_t a = x + 4; a < x + m.sz; ++a) reg = crc_byte(T8, reg, img[a]);
-    if (~reg != word(0)) break;
+    for (uint32_t j = 0; j < g.G; ++j) {
+      const int64_t ws = (int64_t)x + 4 - (int64_t)g.t + (int64_t)j * g.P;
+      const uint32_t lead = uni_lead(g, j);
+      uint32_t reg = 0;
+      for (uint32_t s = 0; s < g.S; ++s) {
+        uint32_t w[2] = {0, 0};
+        for (int b = 0; b < 8; ++b)
+          if (8 * s + b >= lead) w[b >> 2] |= byte(ws + 8 * s + b) << (8 * (b & 3));
+        reg = crc_step8(emu.tab.data(), reg, w[0], w[1]);
+      }
+      v[j] = reg;
+    }
+    for (uint32_t i = 0, d = 1; d < g.G; ++i, d <<= 1)
+      for (uint32_t j = 0; j < g.G; ++j)
+        if ((j & (2 * d - 1)) == 2 * d - 1) {
+          const uint32_t y = v[j - d], *T = ct.data() + i * 1024;
+          v[j] ^= T[y & 0xFFu] ^ T[256 + ((y >> 8) & 0xFFu)] ^ T[512 + ((y >> 16) & 0xFFu)] ^ T[768 + (y >> 24)];
+        }
+    if ((v[g.G - 1] ^ g.KL) != ~word(0)) break;
     if (k < cap) { out[k].pos = uni_pos(m, x); out[k].k_size = m.k; out[k].v_size = m.v; }
   }
   dyn[0] = k;

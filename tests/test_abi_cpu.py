@@ -338,6 +338,34 @@ def test_emulated_run_prefix(shape):
                 assert_same(res, tup, ref, rt)
 
 
+# value lengths whose CRC spans (L = sz - 4, header 10 B for these keys) land on every slicing of
+# uni_geometry: G = 1..64 lanes per entry, span lengths at each G's bounds, leads longer than a window
+# (t > P: whole windows masked), and just past the largest run size (no run)
+_GEOM_VLENS = [0, 1, 7, 8, 30, 31, 32, 33, 34, 90, 91, 120, 121, 122, 300, 310, 311, 312, 313, 315, 330, 361, 362, 363, 400, 700,
+               760, 761, 1000, 1500, 1520, 1521, 2900, 3000, 3040, 3041, 4000, 6000, 6090, 6091, 6092, 7000]
+
+
+def test_emulated_run_geometries():
+    """The run prefix's entry-aligned slices (uni_geometry, uni_lead, the group's tree combine) over
+    span lengths that exercise every lanes-per-entry count and the masked-lead cases; a clean run is
+    covered whole, a corrupted member ends it, and the pipeline agrees with the oracle throughout."""
+    for vlen in _GEOM_VLENS:
+        rng = random.Random(vlen)
+        n = 120 if vlen < 2000 else 40
+        run = _fixed_log(n, 16, vlen, rng.randrange(1 << 30))
+        esz = len(run) // n
+        base = np.frombuffer(bytes(run), np.uint8).copy()
+        bad = base.copy()
+        bad[(n // 2) * esz + rng.randrange(4, esz)] ^= 0x08
+        for im, k in ((base, n), (bad, n // 2)):
+            res, tup, st = emu_scan_run(im, 0)
+            ref, rt = coracle.scan(im, 0)
+            assert_same(res, tup, ref, rt)
+            # a member needs its whole header window readable (kMaxHeader bytes, log_file.go:117-122)
+            want = min(k, ref.n_entries) if esz - 4 <= 6144 else 0
+            assert res.n_run == want, (vlen, esz, res.n_run, want)
+
+
 def test_emulated_run_prefix_counts():
     """A clean config-2-shaped log is covered by the run: every entry but none of the regions."""
     img, n, end = coracle.gen_log(1 << 20, 3, ksize=64, vsize=256)

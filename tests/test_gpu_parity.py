@@ -196,7 +196,8 @@ def _fixed_log(n, klen, vlen, seed, expired_at=0, tx_id=0):
 
 
 @pytest.mark.parametrize("shape", [(64, 256, 0, 0), (16, 100, 0, 0), (13, 70, 0, 0), (20, 33, 1700000000, 7),
-                                   (9, 9, 0, 0), (64, 256, 0, 1 << 40)])
+                                   (9, 9, 0, 0), (64, 256, 0, 1 << 40), (16, 361, 0, 0), (40, 1000, 0, 0),
+                                   (16, 3041, 0, 0), (64, 5000, 0, 0), (16, 362, 0, 0)])
 def test_run_prefix_shapes(eng, shape):
     """The run prefix (k_uniform): equal-sized entries at the file start, one per lane, then the
     region pipeline from the first entry outside the run. Every span length mod 8, long headers,
@@ -204,14 +205,14 @@ def test_run_prefix_shapes(eng, shape):
     other entries; both IOController rules and both tuple kinds (k_uniform writes ldb_entry too)."""
     klen, vlen, exp, txid = shape
     rng = random.Random(klen * 7 + vlen)
-    n = 3000
+    n = 3000 if vlen < 1000 else 600
     run = _fixed_log(n, klen, vlen, rng.randrange(1 << 30), expired_at=exp, tx_id=txid)
     esz = len(run) // n
     other = coracle.gen_log(200_000, 6, ksize=16, vsize=40)
     for tail in (b"", bytes(37), bytes(9000), bytes(other[0][: other[2]]) + bytes(300)):
         base = np.frombuffer(run + tail, np.uint8).copy()
-        variants = [base, base[: 1500 * esz + 3].copy(), base[: (n - 1) * esz + 30].copy()]
-        for k in (0, 1, 700, n - 1):
+        variants = [base, base[: (n // 2) * esz + 3].copy(), base[: (n - 1) * esz + 30].copy()]
+        for k in (0, 1, n // 4, n - 1):
             im = base.copy()
             im[k * esz + rng.choice([0, 5, esz - 1])] ^= 0x40
             variants.append(im)

@@ -55,6 +55,9 @@ def build(name: str) -> str:
                 "trackers": ["-amdgpu-use-amdgpu-trackers=1"], "relaxocc": ["-amdgpu-schedule-relaxed-occupancy"],
                 "bias100": ["-amdgpu-schedule-metric-bias=100"], "bias0": ["-amdgpu-schedule-metric-bias=0"]}[name[5:]]
         defs = [x for o in opts for x in ("-mllvm", o)]
+    elif name.startswith("def_"):   # def_NAME=VALUE[,NAME=VALUE...]: plain -D switches
+        defs = ["-D" + d for d in name[4:].split(",")]
+        name = re.sub(r"[^A-Za-z0-9_]", "_", name)
     elif name == "stamps":
         defs = ["-DLDB_STAMPS=1"]
     elif name == "stamps1":   # one wave per SIMD: phase stamps measure each wave's own critical path
