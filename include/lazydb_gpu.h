@@ -124,8 +124,12 @@ int ldb_ctx_reserve(ldb_ctx* ctx, uint64_t max_len);
 uint64_t ldb_workspace_bytes(uint64_t len);
 
 /* Device-resident scan (the hot path).  d_image: `len` bytes in device memory, len = bound
- * (FileIO: the file size; Mmap: the mapping length).  d_out: device array of `cap` tuples of
- * `tuple_kind`.  d_result: device ldb_scan_result written at the end of the stream work.
+ * (FileIO: the file size; Mmap: the mapping length), 16-byte aligned (LDB_ERR_ARG otherwise).
+ * The kernels load whole 16-byte granules, so they may read up to 15 bytes past `len`, inside the
+ * granule that holds byte len-1: never past a page boundary, so no allocation that holds the `len`
+ * bytes can fault. The values of those bytes never affect any result (tests/test_gpu_abi_contract.py
+ * poisons them).  d_out: device array of `cap` tuples of `tuple_kind`.  d_result: device
+ * ldb_scan_result written at the end of the stream work.
  * Asynchronous with respect to the host: enqueues work on `stream` and returns. */
 int ldb_scan_file_dev(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, uint32_t fid, int io_type,
                       int tuple_kind, void* d_out, uint64_t cap, ldb_scan_result* d_result, void* stream);

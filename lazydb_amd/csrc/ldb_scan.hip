@@ -265,7 +265,7 @@ __device__ uint64_t g_stamps[kStampSlots];
 // it is in L1), and runs S = P / 8 S-table steps from register 0 (lane 0 masks its first t bytes).
 // The group's registers are combined by a tree: at level d, lanes j = 2d - 1 (mod 2d) take the value
 // of lane j - d by DPP / permlane and shift it by d P bytes (a 4-lookup byte table built by
-// k_uniform_setup). The group's last lane ends with the raw register of the whole span, checks
+// each workgroup, uni_prepare). The group's last lane ends with the raw register of the whole span, checks
 // raw ^ KL == ~crc and the header, and writes the tuple at out[e].
 //
 // Bytes are read with buffer loads from a wave-uniform base 512 B before the wave's first entry (so
@@ -281,9 +281,7 @@ struct UniSetup {
   UniMemo m;
   UniGeo g;
 };
-constexpr uint64_t kUniSetupBytes = 1024;   // UniSetup, then kUniLevels combine tables of 1024 words
-constexpr uint64_t kUniTabWords = kUniLevels * 1024;
-static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
+constexpr uint64_t kUniTabWords = kUniLevels * 1024;   // combine tables in LDS
 static_assert(kTBOff == 0, "k_uniform stages the S table at LDS word 0");
 __device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
   const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
@@ -293,21 +291,21 @@ __device__ __forceinline__ uint32_t ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
   return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
 }
 
-// One workgroup: entry 0's memo, the slicing, KL and the combine tables (shift by 2^i P bytes). Entry
-// 0's and entry 1's header windows are staged into LDS by one coalesced load each (the decode is a
-// chain of dependent byte reads); when entry 1 is not a run member the prefix is skipped outright
-// (K = 0: the region pipeline from offset 0 -- the same scan, without a run of one). Shifts come from
-// the x^(8n) table (n <= kW) instead of a serial square-and-multiply.
-__global__ __launch_bounds__(1024) void k_uniform_setup(Pipe p, UniSetup* us, uint32_t* utab) {
-  __shared__ UniSetup su;
+#ifndef LDB_UNI_ABL
+#define LDB_UNI_ABL 0   // ablations for attribution only (results wrong): 1 rows loaded, no CRC (xor of the
+                        // words); 2 CRC steps on words made from x, no row loads; both skip the CRC check
+#endif
+// Every k_uniform workgroup first derives the run's parameters itself (no separate setup launch):
+// entry 0's memo, the slicing, KL and the combine tables (shift by 2^i P bytes, built straight into
+// LDS). Entry 0's and entry 1's header windows are staged into LDS by one coalesced load each (the
+// decode is a chain of dependent byte reads; all workgroups read the same L2-resident 128 bytes).
+// When entry 1 is not a run member the prefix is skipped outright (K = 0: the region pipeline from
+// offset 0 -- the same scan, without a run of one). Shifts come from the x^(8n) table (n <= kW).
+// Workgroup 0 publishes K = 0 or the entry size for the pipeline. Returns false when there is no run.
+__device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
   __shared__ uint32_t xn[kUniLevels];
   __shared__ uint32_t win[2][16];   // bytes [0, 64) and [sz, sz + 64) of the image, zero past len
-  struct F {
-    const uint8_t* q;
-    uint64_t len;
-    __device__ uint32_t operator()(int i) const { return (uint64_t)i < len ? q[i] : 0u; }
-  };
-  auto stage = [&](int w, uint64_t at) {   // dword-granular, exact at len
+  auto stage = [&](int w, uint64_t at) {
     if (threadIdx.x < 64) {
       const uint64_t a = at + threadIdx.x;
       reinterpret_cast<uint8_t*>(win[w])[threadIdx.x] = a < p.len ? p.img[a] : 0;
@@ -333,21 +331,19 @@ __global__ __launch_bounds__(1024) void k_uniform_setup(Pipe p, UniSetup* us, ui
       if (!uni_header_ok(su.m, word, su.m.sz, p.len, p.io)) su.g.ok = 0;
     }
     if (su.g.ok) {
-      p.dyn[1] = su.m.sz;
       for (uint32_t i = 0; i < su.g.lg; ++i) xn[i] = p.xw[su.g.P << i];
-    } else {
+      if (blockIdx.x == 0) p.dyn[1] = su.m.sz;
+    } else if (blockIdx.x == 0) {
       p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
     }
-    *us = su;
   }
   __syncthreads();
-  if (!su.g.ok) return;
+  if (!su.g.ok) return false;
   for (uint32_t e = threadIdx.x; e < su.g.lg * 1024u; e += blockDim.x)
-    utab[e] = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
+    T[e] = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
+  return true;
 }
 
-// Combine level D of the group's tree: lanes j = 2D - 1 (mod 2D) (bit log2 D of `sel`) take lane
-// j - D's register shifted by D P bytes. Branch-free per lane: the shifted value is masked in.
 // Combine level D of the group's tree: lanes j = 2D - 1 (mod 2D) take lane j - D's register shifted
 // by D P bytes. c = ~j & (j + 1) is 2^(trailing ones of j): lane j combines at level D iff c > D.
 // Branch-free per lane (the shifted value is masked in).
@@ -394,7 +390,17 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     const int32_t ws = (int32_t)hx + 4 - (int32_t)t + (int32_t)(j * P);   // < 0 only when base = 0
     const uint32_t a = (uint32_t)ws & ~3u, sh = (uint32_t)ws & 3u;
     uint32_t d[4 * R];
-    if (base) {
+    if (LDB_UNI_ABL == 2) {
+#pragma unroll
+      for (int i = 0; i < 4 * R; ++i) d[i] = (uint32_t)x * (2u * i + 1u) + j;
+    } else if (LDB_UNI_ABL == 3) {   // the same rows' worth of bytes, lane-contiguous (coalesced)
+      const uint32_t cb = (uint32_t)(b0 - base) + 16u * (uint32_t)lane;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint4 q = ld16(rs, cb + 1024u * r);
+        d[4 * r] = q.x; d[4 * r + 1] = q.y; d[4 * r + 2] = q.z; d[4 * r + 3] = q.w;
+      }
+    } else if (base) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const uint4 q = ld16(rs, a + 16 * r);
@@ -421,8 +427,10 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
         w0 &= n >= 4 ? 0u : 0xFFFFFFFFu << (8 * n);
         w1 &= n >= 8 ? 0u : (n > 4 ? 0xFFFFFFFFu << (8 * (n - 4)) : 0xFFFFFFFFu);
       }
-      reg = crc_step8(stab, reg, w0, w1);
+      if (LDB_UNI_ABL == 1 || LDB_UNI_ABL == 3) reg ^= w0 ^ w1;
+      else reg = crc_step8(stab, reg, w0, w1);
     }
+    if (LDB_UNI_ABL) asm volatile("" ::"v"(reg));
     uni_level<1>(wp, T, GG, c, reg);
     uni_level<2>(wp, T + 1024, GG, c, reg);
     uni_level<4>(wp, T + 2048, GG, c, reg);
@@ -445,7 +453,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
       uint32_t diff = 0;
 #pragma unroll
       for (int i = 0; i < 9; ++i) diff |= (funnel(hd[i + 2], hd[i + 1], hsh) ^ mv->w[i]) & mv->msk[i];
-      ok = ok && diff == 0u && (reg ^ KL) == ~crc;   // getEntryCrc == stored crc (log_file.go:141-143)
+      ok = ok && diff == 0u && ((reg ^ KL) == ~crc || LDB_UNI_ABL);   // getEntryCrc == stored crc (log_file.go:141-143)
     }
     const uint64_t bad = __ballot((last && e < ncand && !ok) ? 1 : 0);
     if (bad && lane == 0)
@@ -476,18 +484,14 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
   }
 }
 
-__global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, const UniSetup* us, const uint32_t* utab) {
+__global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p) {
   __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + kUniTabWords];   // S table, combine tables
   __shared__ UniSetup su;
-  if (threadIdx.x == 0) su = *us;
-  __syncthreads();
-  if (!su.g.ok) return;
+  if (!uni_prepare(p, su, stab + 5120)) return;
   {
     const uint4* g = reinterpret_cast<const uint4*>(p.gtab);
     uint4* t = reinterpret_cast<uint4*>(stab);
     for (int i = threadIdx.x; i < 5120 / 4; i += blockDim.x) t[i] = g[i];
-    const uint4* u = reinterpret_cast<const uint4*>(utab);
-    for (int i = threadIdx.x; i < (int)su.g.lg * 256; i += blockDim.x) t[5120 / 4 + i] = u[i];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -507,10 +511,14 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
   // folds the table base into the ds_read offset field
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  copy_tables(tab, p.gtab);
   // ctr[] was zeroed by the hipMemsetAsync that opens every pipeline (enqueue_scan); the terminal
   // words start at "none" (read only by the later kernels, stream-ordered after this one)
   if (blockIdx.x == 0 && threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
+  {   // a workgroup whose waves have no region (the run prefix took them) leaves before the table copy
+    const uint64_t rf0 = first_region(p), nr0 = p.nreg - rf0, nw0 = (uint64_t)gridDim.x * kWPB;
+    if (rf0 + (uint64_t)blockIdx.x * kWPB * ((nr0 + nw0 - 1) / nw0) >= p.nreg) return;
+  }
+  copy_tables(tab, p.gtab);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1089,7 +1097,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_uni, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -1108,7 +1116,6 @@ WsLayout layout(uint64_t len) {
   L.o_ctr = take(32);
   L.o_tpos = take(16);
   L.o_dyn = take(16);   // run prefix: K, entry size (k_uniform)
-  L.o_uni = take(kUniSetupBytes + 4 * kUniTabWords);   // run prefix: memo, slicing, combine tables
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1));
@@ -1216,13 +1223,9 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   // the run prefix: K = ~0 until k_uniform lowers it to the first entry outside the run
   LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0xFF, 16, s));
   {
-    UniSetup* us = reinterpret_cast<UniSetup*>(c->ws + L.o_uni);
-    uint32_t* utab = reinterpret_cast<uint32_t*>(c->ws + L.o_uni + kUniSetupBytes);
-    hipLaunchKernelGGL(k_uniform_setup, dim3(1), dim3(1024), 0, s, p, us, utab);
     const uint64_t batches = len / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
     const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2);
-    hipLaunchKernelGGL(k_uniform, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, (const UniSetup*)us,
-                       (const uint32_t*)utab);
+    hipLaunchKernelGGL(k_uniform, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p);
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
   // persistent waves: exactly the workgroups that are resident at once (LDS-limited), so no

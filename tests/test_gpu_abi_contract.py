@@ -78,6 +78,32 @@ def test_scan_files_dev_batch(gpu_engine):
         same(r, tup, *coracle.scan(im, 0))
 
 
+def test_bytes_past_len_ignored(gpu_engine):
+    """include/lazydb_gpu.h: the kernels may load up to 15 bytes past `len` (whole 16-B granules);
+    those bytes must never change a result. Each image sits at the start of a larger device buffer
+    whose bytes past `len` are random, 0x00 or 0xFF; cut lengths cover every residue mod 16, cuts
+    inside an entry and on entry boundaries, for the run prefix (equal-sized entries) and the
+    region pipeline (Zipf values), both IO rules."""
+    import torch
+    eng = gpu_engine
+    run = coracle.gen_log(3 << 20, 51, ksize=64, vsize=256)
+    zipf = coracle.gen_log(3 << 20, 52, ksize=64, value_mode=1, zipf_max=512)
+    rng = np.random.default_rng(53)
+    for img, n, end in (run, zipf):
+        cuts = [end - 16 * 40 + r for r in range(16)] + [end, end - 1, end // 2 + 7, 4096 + 3]
+        for fill in ("rand", 0x00, 0xFF):
+            buf = rng.integers(0, 256, img.size + 64, dtype=np.uint8) if fill == "rand" else \
+                np.full(img.size + 64, fill, np.uint8)
+            for cut in cuts:
+                host = buf.copy()
+                host[:cut] = img[:cut]
+                d = to_dev(host)
+                for io in (0, 1):
+                    res, tup = eng.scan_dev(d[:cut], io_type=io)   # a view: the poisoned bytes follow it
+                    ref, rt = coracle.scan(np.ascontiguousarray(img[:cut]), io)
+                    same(res, tup, ref, rt)
+
+
 def test_five_contexts_five_threads():
     """index.go:103-108: one replay per value type, concurrently; each thread owns a context and a
     stream and scans its fids in ascending order (index.go:68)."""

@@ -1,4 +1,5 @@
-# Extra PMC passes on k_scan_main (instruction mix, I-cache, LDS); one pass per counter group.
+# Extra PMC passes on one kernel (KREGEX, default k_scan_main): instruction mix, I-cache, LDS, HBM
+# bytes; one pass per counter group.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/pmcx_${1:-x}
@@ -7,9 +8,10 @@ SHORT="--steps 5 --warmup 1 --no-cpu --no-verify --e2e 0 ${BENCH_ARGS:-}"
 i=0
 for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES" \
            "SQC_ICACHE_MISSES SQC_ICACHE_HITS" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
-           "SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_FLAT GRBM_GUI_ACTIVE"; do
+           "SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_FLAT GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex 'k_scan_main' -d $OUT/p$i -o pmc -f csv -- python3 bench.py $SHORT > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; }
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "${KREGEX:-k_scan_main}" -d $OUT/p$i -o pmc -f csv -- python3 bench.py $SHORT > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; }
 done
 python3 - "$OUT" <<'PY'
 import csv, glob, sys
