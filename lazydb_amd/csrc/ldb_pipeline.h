@@ -32,7 +32,9 @@ struct Pipe {
   uint32_t* ctr;              // [0] fail count, [1] overflow, [2] repairs, [3] fast regions, [4] deferred
   uint64_t* tpos;             // [0] min terminal position, [1] its status (packed with position)
   uint64_t* blk;              // per kBlkRegions-region block: count sum (k_combine)
-  uint64_t* dyn;              // [0] K: entries of the equal-sized run k_uniform verified, [1] their size
+  uint64_t* dyn;              // [0] K: entries of the equal-sized run k_uniform verified, [1] their size,
+                              // [2] kUniReady once a k_uniform launch published its setup to `uni`
+  uint8_t* uni;               // the run prefix's published setup (memo, slicing, combine tables)
   void* out;
   uint64_t cap;
   int kind;

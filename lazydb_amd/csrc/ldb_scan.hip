@@ -310,7 +310,12 @@ __device__ __forceinline__ uint32_t ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 #define LDB_UNI_ABL 0   // ablations for attribution only (results wrong): 1 rows loaded, no CRC (xor of the
                         // words); 2 CRC steps on words made from x, no row loads; both skip the CRC check
 #endif
-// Every k_uniform workgroup first derives the run's parameters itself (no separate setup launch):
+constexpr uint64_t kUniReady = 0x5E7A11ED5E7A11EDull;   // dyn[2]: the setup in p.uni is complete
+constexpr uint64_t kUniSetupBytes = 1024;                // UniSetup, then the combine tables
+static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
+// The first k_uniform launch of a pipeline derives the run's parameters in every workgroup (no
+// separate setup launch) and its workgroup 0 publishes them to p.uni, so the later launches of a
+// chunked scan (ChunkPlan) only copy them:
 // entry 0's memo, the slicing, KL and the combine tables (shift by 2^i P bytes, built straight into
 // LDS). Entry 0's and entry 1's header windows are staged into LDS by one coalesced load each (the
 // decode is a chain of dependent byte reads; all workgroups read the same L2-resident 128 bytes).
@@ -320,6 +325,19 @@ __device__ __forceinline__ uint32_t ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 __device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
   __shared__ uint32_t xn[kUniLevels];
   __shared__ uint32_t win[2][16];   // bytes [0, 64) and [sz, sz + 64) of the image, zero past len
+  __shared__ int published;
+  UniSetup* gsu = reinterpret_cast<UniSetup*>(p.uni);
+  const uint32_t* gT = reinterpret_cast<const uint32_t*>(p.uni + kUniSetupBytes);
+  if (threadIdx.x == 0) {
+    published = __hip_atomic_load(&p.dyn[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == kUniReady;
+    if (published) su = *gsu;
+  }
+  __syncthreads();
+  if (published) {
+    if (!su.g.ok) return false;
+    for (uint32_t e = threadIdx.x; e < su.g.lg * 1024u; e += blockDim.x) T[e] = gT[e];
+    return true;
+  }
   auto stage = [&](int w, uint64_t at) {
     if (threadIdx.x < 64) {
       const uint64_t a = at + threadIdx.x;
@@ -353,10 +371,19 @@ __device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
     }
   }
   __syncthreads();
-  if (!su.g.ok) return false;
-  for (uint32_t e = threadIdx.x; e < su.g.lg * 1024u; e += blockDim.x)
-    T[e] = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
-  return true;
+  if (su.g.ok)
+    for (uint32_t e = threadIdx.x; e < su.g.lg * 1024u; e += blockDim.x) {
+      const uint32_t v = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
+      T[e] = v;
+      if (blockIdx.x == 0) const_cast<uint32_t*>(gT)[e] = v;
+    }
+  if (blockIdx.x == 0) {   // publish: the tables and the setup, then the flag (release)
+    if (threadIdx.x == 0) *gsu = su;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&p.dyn[2], kUniReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return su.g.ok != 0;
 }
 
 // Combine level D of the group's tree: lanes j = 2D - 1 (mod 2D) take lane j - D's register shifted
@@ -374,19 +401,32 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 
 // One wave's share of the run prefix, S steps per lane (a compile-time count: the rows stay in
 // registers with static indices and the step loop has no per-step branch).
-template <int S>
-__device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint32_t* stab, int lane, int wave) {
+template <int S, bool kChunk>
+__device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint32_t* stab, int lane, int wave,
+                                          uint64_t a_lo, uint64_t a_hi) {
+  if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
+    a_lo = 0;
+    a_hi = p.len;
+  }
   constexpr int R = (2 * S + 1 + 3) / 4;   // 16-B rows per lane
   const uint32_t sz = (uint32_t)su.m.sz, G = su.g.G, lg = su.g.lg, P = su.g.P, t = su.g.t, KL = su.g.KL;
   const uint32_t E = 64u >> lg;
-  const uint64_t ncand = p.len / sz + 1;   // entry ncand - 1 always fails (its bytes pass len)
-  const uint64_t nbatch = (ncand + E - 1) / E;
+  // This launch's candidates, by bytes rather than entry indices (no 64-bit division): entry e at
+  // x = e sz is a candidate when x <= len (the one at len or past it fails, so the run stops there),
+  // and, for a launch over an image still being copied in (ChunkPlan), when its bytes and the 48
+  // header bytes its last lane loads lie in [0, a_hi) but not in [0, a_lo) (the earlier launch's).
+  const uint64_t need = sz > 48 ? sz : 48, Esz = (uint64_t)E * sz;
+  const bool all_hi = a_hi >= p.len;
+  // first batch: an underestimate (float quotient, minus 2) is harmless, its entries are not ours
+  const uint64_t b_first = a_lo > need ? (uint64_t)max(0.0f, (float)(a_lo - need) / (float)Esz - 2.0f) : 0;
   const uint32_t j = (uint32_t)lane & (G - 1);
   const bool last = j == G - 1;
   const uint32_t lead0 = uni_lead(su.g, j);   // bytes lane j masks at its window's start
   const uint32_t* T = stab + 5120;
   GpuWave wp{lane};
-  for (uint64_t b = (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
+  const uint64_t nbatch = kChunk ? ~0ull : (p.len / sz + E) / E;   // !kChunk: ceil(ncand / E), ncand = len / sz + 1
+  for (uint64_t b = b_first + (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
+    if (kChunk && b * Esz > (all_hi ? p.len : a_hi)) break;   // wave-uniform: no candidate of this launch from here on
     if (b * E >= __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     // Opaque per-batch copies: the uniform step / level conditions and the lane masks derived from
     // them are evaluated inside the batch, not hoisted out of the loop as a bank of held SGPR masks.
@@ -394,6 +434,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     asm volatile("" : "+s"(tt), "+s"(GG), "+v"(c), "+v"(lead));
     const uint64_t e = b * E + ((uint32_t)lane >> lg);
     const uint64_t x = e * sz;
+    if (kChunk && (b + 1) * Esz + need <= a_lo) continue;   // wave-uniform: below the launch's range (b_first's slack)
     const uint64_t b0 = b * E * sz;
     const uint64_t base = b0 >= 512 ? (b0 - 512) & ~15ull : 0;   // wave-uniform; the lead t < 8 G <= 512
     const uint64_t nrec = (p.len - base + 3) & ~3ull;
@@ -456,7 +497,13 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     // an opaque offset, so its words stay per-batch VGPR loads instead of SGPRs held across the loop.
     bool ok = false;
     uint32_t crc = 0;
-    if (last && e < ncand) {
+    bool mine = x <= p.len;
+    if (kChunk) {
+      uint64_t lo_ = a_lo, hi_ = all_hi ? ~0ull : a_hi;   // opaque per batch: not held across the loop
+      asm volatile("" : "+s"(lo_), "+s"(hi_));
+      mine = mine && (lo_ == 0 || x + need > lo_) && x + need <= hi_;
+    }
+    if (last && mine) {
       const uint32_t hd[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
       uint32_t z = 0;
       asm volatile("" : "+v"(z));
@@ -470,7 +517,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
       for (int i = 0; i < 9; ++i) diff |= (funnel(hd[i + 2], hd[i + 1], hsh) ^ mv->w[i]) & mv->msk[i];
       ok = ok && diff == 0u && ((reg ^ KL) == ~crc || LDB_UNI_ABL);   // getEntryCrc == stored crc (log_file.go:141-143)
     }
-    const uint64_t bad = __ballot((last && e < ncand && !ok) ? 1 : 0);
+    const uint64_t bad = __ballot((last && mine && !ok) ? 1 : 0);
     if (bad && lane == 0)
       atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
     if (ok && e < p.cap) {
@@ -499,7 +546,10 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
   }
 }
 
-__global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p) {
+// kChunk: a_lo, a_hi: image bytes [0, a_hi) are in place; candidates not already taken by a launch
+// with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
+template <bool kChunk>
+__global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_lo, uint64_t a_hi) {
   __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + kUniTabWords];   // S table, combine tables
   __shared__ UniSetup su;
   if (!uni_prepare(p, su, stab + 5120)) return;
@@ -512,7 +562,7 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n) case n: uni_waves<n>(p, su, stab, lane, wave); break;
+#define LDB_UNI_CASE(n) case n: uni_waves<n, kChunk>(p, su, stab, lane, wave, a_lo, a_hi); break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
 #undef LDB_UNI_CASE
@@ -1081,12 +1131,13 @@ struct ldb_ctx {
   uint64_t h_out_cap = 0;
   ldb_scan_result* h_res = nullptr;
   hipStream_t h_stream = nullptr;
-  // host-image copies (ldb_scan_file): chunks dealt round-robin over n_cp streams, so several DMA
-  // engines pull from a registered mapping at once (LDB_H2D_STREAMS, default 2)
+  // host-image copies (ldb_scan_file): 64 MiB chunks dealt round-robin over n_cp streams
+  // (LDB_H2D_STREAMS, default 2: the e2e timings of gpurun_out/e2e_streams.log), one
+  // event per chunk for the chunked run prefix (ChunkPlan)
   static constexpr int kMaxCp = 4;
   int n_cp = 0;
   hipStream_t cp[kMaxCp] = {};
-  hipEvent_t cp_ev[kMaxCp] = {};
+  std::vector<hipEvent_t> chunk_ev;
   double t_run = 0, t_main = 0, t_total = 0;
   uint64_t t_n = 0;
   void* merge = nullptr;       // merge/GC workspace (ldb_merge.hip), created on first use
@@ -1118,7 +1169,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_uni, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -1136,7 +1187,8 @@ WsLayout layout(uint64_t len) {
   // tpos (2 x u64, set by k_scan_main's first workgroup); take() rounds each field to 256 B
   L.o_ctr = take(32);
   L.o_tpos = take(16);
-  L.o_dyn = take(16);   // run prefix: K, entry size (k_uniform)
+  L.o_dyn = take(32);   // run prefix: K, entry size, setup-published flag (k_uniform)
+  L.o_uni = take(kUniSetupBytes + 4 * kUniTabWords);   // run prefix: the published setup
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1));
@@ -1183,6 +1235,7 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.tpos = reinterpret_cast<uint64_t*>(w + L.o_tpos);
   p.blk = reinterpret_cast<uint64_t*>(w + L.o_blk);
   p.dyn = reinterpret_cast<uint64_t*>(w + L.o_dyn);
+  p.uni = w + L.o_uni;
   p.out = out;
   p.cap = cap;
   p.kind = kind;
@@ -1199,8 +1252,21 @@ int fence_ws(ldb_ctx* c, hipStream_t s) {
   return LDB_OK;
 }
 
+// An image that is still being copied in: bytes [0, avail[i]) are in place once ev[i] has fired
+// (avail ascending, the last = len). The run prefix then verifies its candidates chunk by chunk,
+// each launch waiting only for its chunk, so it overlaps the copy; the region pipeline waits for all.
+struct ChunkPlan {
+  int n;
+  const uint64_t* avail;
+  const hipEvent_t* ev;
+};
+
+// no_run: skip the run prefix (k_uniform), e.g. for an image read in place from host memory, where
+// its per-lane gathered rows would cross PCIe several times; the region pipeline's LDS-DMA staging
+// reads every byte once in 1 KiB pieces.
 int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, int io, int kind, void* d_out,
-                 uint64_t cap, ldb_scan_result* d_res, hipStream_t s, bool serial) {
+                 uint64_t cap, ldb_scan_result* d_res, hipStream_t s, bool serial, bool no_run = false,
+                 const ChunkPlan* plan = nullptr) {
   if (!c || !d_res || (io != LDB_IO_FILEIO && io != LDB_IO_MMAP) ||
       (kind != LDB_TUPLE_INDEX && kind != LDB_TUPLE_ENTRY) || (cap && !d_out))
     return LDB_ERR_ARG;
@@ -1216,9 +1282,12 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   // every pipeline starts from zeroed control words, in stream order: nothing depends on how the
   // previous pipeline on this workspace ended, or on what a fresh allocation held
   LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
+  const bool chunked = plan && plan->n > 0 && !serial && len >= (uint64_t)kMaxHeader && !no_run;
+  if (plan && !chunked)   // nothing overlaps the copy: the whole image first
+    for (int i = 0; i < plan->n; ++i) LDB_HIP(hipStreamWaitEvent(s, plan->ev[i], 0));
   if (serial || len < (uint64_t)kMaxHeader) {
     LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
-    LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0, 16, s));   // no run prefix: the walk starts at 0
+    LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0, 32, s));   // no run prefix: the walk starts at 0
     hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 0);
     LDB_HIP(hipGetLastError());
     return fence_ws(c, s);
@@ -1242,11 +1311,27 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
     LDB_HIP(hipEventRecord(ev->e0, s));
   }
   // the run prefix: K = ~0 until k_uniform lowers it to the first entry outside the run
-  LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0xFF, 16, s));
-  {
-    const uint64_t batches = len / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
-    const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2);
-    hipLaunchKernelGGL(k_uniform, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p);
+  LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, no_run ? 0 : 0xFF, 32, s));   // K = ~0, setup not published
+  if (!no_run) {
+    auto launch = [&](uint64_t lo, uint64_t hi) {
+      const uint64_t batches = (hi - lo) / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
+      const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2);
+      if (chunked)
+        hipLaunchKernelGGL(k_uniform<true>, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+      else
+        hipLaunchKernelGGL(k_uniform<false>, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+    };
+    if (chunked) {
+      uint64_t lo = 0;
+      for (int i = 0; i < plan->n; ++i) {
+        LDB_HIP(hipStreamWaitEvent(s, plan->ev[i], 0));
+        const uint64_t hi = i + 1 == plan->n ? len : std::min(plan->avail[i], len);
+        launch(lo, hi);
+        lo = hi;
+      }
+    } else {
+      launch(0, len);
+    }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
   // persistent waves: exactly the workgroups that are resident at once (LDS-limited), so no
@@ -1342,10 +1427,9 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->h_out) (void)hipFree(c->h_out);
   if (c->h_res) (void)hipFree(c->h_res);
   if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
-  for (int i = 0; i < c->n_cp; ++i) {
+  for (int i = 0; i < c->n_cp; ++i)
     if (c->cp[i]) (void)hipStreamDestroy(c->cp[i]);
-    if (c->cp_ev[i]) (void)hipEventDestroy(c->cp_ev[i]);
-  }
+  for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
   if (c->merge) ldb_merge_release_(c->merge);
   if (c->ws_ev) (void)hipEventDestroy(c->ws_ev);
   for (const ldb_ctx::EvTriple& t : c->evs) {
@@ -1416,17 +1500,33 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
   const size_t tsz = tuple_kind == LDB_TUPLE_ENTRY ? sizeof(ldb_entry) : sizeof(ldb_index_tuple);
   // context-owned staging (grow-only): image, tuples, result; one stream per context
   if (!c->h_stream && hipStreamCreateWithFlags(&c->h_stream, hipStreamNonBlocking) != hipSuccess) return LDB_ERR_HIP;
-  const uint64_t img_need = (len + 15) & ~15ull, out_need = cap * tsz;
-  if ((img_need > c->h_img_cap || !c->h_img || out_need > c->h_out_cap || !c->h_out) && (c->h_img || c->h_out))
+  // A page-locked image (ldb_host_register, or a pinned allocation) is scanned in place, below
+  // (opt-in, LDB_DIRECT_IMAGE=1: measured slower than the staged copy, 23.7 vs 21.0 ms at config 2 --
+  // the CUs' PCIe reads reach 52 GB/s against the DMA engines' 57.6)
+  void* mapped = nullptr;
+  if (len && getenv("LDB_DIRECT_IMAGE") != nullptr &&
+      (hipHostGetDevicePointer(&mapped, const_cast<uint8_t*>(h_image), 0) != hipSuccess || ((uintptr_t)mapped & 15))) {
+    mapped = nullptr;   // pageable (the error is expected) or not 16-B aligned: the staged copy
+    (void)hipGetLastError();
+  }
+  // a page-locked output array is written in place too (the tuple writes cross PCIe while the scan
+  // runs, in the other direction), else the tuples are staged on the device and copied back
+  void* out_mapped = nullptr;
+  if (cap && getenv("LDB_NO_DIRECT_OUT") == nullptr && hipHostGetDevicePointer(&out_mapped, h_out, 0) != hipSuccess) {
+    out_mapped = nullptr;
+    (void)hipGetLastError();
+  }
+  const uint64_t img_need = mapped ? 0 : (len + 15) & ~15ull, out_need = out_mapped ? 0 : cap * tsz;
+  if ((img_need > c->h_img_cap || out_need > c->h_out_cap) && (c->h_img || c->h_out))
     (void)hipDeviceSynchronize();   // staging buffers are freed below: nothing may still use them
-  if (img_need > c->h_img_cap || !c->h_img) {
+  if (img_need > c->h_img_cap || (!c->h_img && !mapped)) {
     if (c->h_img) (void)hipFree(c->h_img);
     c->h_img = nullptr;
     c->h_img_cap = 0;
     if (hipMalloc(&c->h_img, img_need ? img_need : 16) != hipSuccess) return LDB_ERR_NOMEM;
     c->h_img_cap = img_need;
   }
-  if (out_need > c->h_out_cap || !c->h_out) {
+  if (out_need > c->h_out_cap || (!c->h_out && !out_mapped)) {
     if (c->h_out) (void)hipFree(c->h_out);
     c->h_out = nullptr;
     c->h_out_cap = 0;
@@ -1439,27 +1539,50 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
     const char* e = getenv("LDB_H2D_STREAMS");
     const int want = std::min(std::max(e ? atoi(e) : 2, 1), (int)ldb_ctx::kMaxCp);
     for (int i = 0; i < want; ++i) {
-      if (hipStreamCreateWithFlags(&c->cp[i], hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&c->cp_ev[i], hipEventDisableTiming) != hipSuccess)
+      if (hipStreamCreateWithFlags(&c->cp[i], hipStreamNonBlocking) != hipSuccess)
         return LDB_ERR_HIP;
       c->n_cp = i + 1;
     }
   }
-  // The image goes up in 64 MiB chunks dealt over the copy streams; the scan stream waits for all
-  // of them. Every stream is drained before the call returns, so no copy outlives the caller's
-  // buffer (a Go slice or an mmap'd file).
-  constexpr uint64_t kChunk = 64ull << 20;
+  // The image goes up in 64 MiB chunks dealt over the copy streams (SDMA; at PCIe rate from a
+  // page-locked mapping), and the run prefix verifies each chunk's entries as soon as it lands, so
+  // the decode overlaps the transfer; the region pipeline runs after the last
+  // chunk. Opt-in alternative: the image scanned in place through its device mapping (run prefix
+  // skipped, enqueue_scan no_run). Every stream is drained before the call returns, so no copy or
+  // read outlives the caller's buffer (a Go slice or an mmap'd file).
   int rc = LDB_OK;
-  uint64_t i = 0;
-  for (uint64_t off = 0; off < len && rc == LDB_OK; off += kChunk, ++i) {
-    const uint64_t nb = std::min(kChunk, len - off);
-    if (hipMemcpyAsync(c->h_img + off, h_image + off, nb, hipMemcpyHostToDevice, c->cp[i % c->n_cp]) != hipSuccess)
-      rc = LDB_ERR_HIP;
+  if (mapped) {
+    rc = enqueue_scan(c, static_cast<const uint8_t*>(mapped), len, fid, io_type, tuple_kind,
+                      out_mapped ? out_mapped : c->h_out, cap, c->h_res, s, false, true);
+    if (rc != LDB_OK) {
+      (void)hipStreamSynchronize(s);
+      return rc;
+    }
   }
-  for (int j = 0; j < c->n_cp && rc == LDB_OK; ++j)
-    if (hipEventRecord(c->cp_ev[j], c->cp[j]) != hipSuccess || hipStreamWaitEvent(s, c->cp_ev[j], 0) != hipSuccess)
+  constexpr uint64_t kChunk = 64ull << 20;
+  const int nch = mapped ? 0 : (int)((len + kChunk - 1) / kChunk);
+  while ((int)c->chunk_ev.size() < nch && rc == LDB_OK) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = LDB_ERR_HIP;
+    else c->chunk_ev.push_back(e);
+  }
+  std::vector<uint64_t> avail(nch);
+  for (int i = 0; i < nch && rc == LDB_OK; ++i) {
+    const uint64_t off = (uint64_t)i * kChunk, nb = std::min(kChunk, len - off);
+    hipStream_t cs = c->cp[i % c->n_cp];
+    // chunk i lands after chunk i - n_cp on the same copy stream: the prefix [0, off + nb) is in
+    // place once every stream's latest chunk up to i has landed, which the scan stream's waits on
+    // ev[0..i] in order give
+    if (hipMemcpyAsync(c->h_img + off, h_image + off, nb, hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipEventRecord(c->chunk_ev[i], cs) != hipSuccess)
       rc = LDB_ERR_HIP;
-  if (rc == LDB_OK) rc = enqueue_scan(c, c->h_img, len, fid, io_type, tuple_kind, c->h_out, cap, c->h_res, s, false);
+    avail[i] = off + nb;
+  }
+  if (rc == LDB_OK && !mapped) {
+    const ChunkPlan plan{nch, avail.data(), c->chunk_ev.data()};
+    rc = enqueue_scan(c, c->h_img, len, fid, io_type, tuple_kind, out_mapped ? out_mapped : c->h_out, cap, c->h_res, s,
+                      false, false, &plan);
+  }
   for (int j = 0; j < c->n_cp; ++j) (void)hipStreamSynchronize(c->cp[j]);
   if (rc != LDB_OK) {
     (void)hipStreamSynchronize(s);
@@ -1469,7 +1592,7 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
   if (hipMemcpyAsync(&res, c->h_res, sizeof(res), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return LDB_ERR_HIP;
-  const uint64_t n = std::min<uint64_t>(res.n_entries, cap);
+  const uint64_t n = out_mapped ? 0 : std::min<uint64_t>(res.n_entries, cap);
   if (n && (hipMemcpyAsync(h_out, c->h_out, n * tsz, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess))
     return LDB_ERR_HIP;

@@ -93,12 +93,18 @@ class Engine:
 
     # ---------------------------------------------------------------- host memory
     def scan_host(self, img: np.ndarray, fid: int = 0, io_type: int = N.FILEIO, kind: int = N.TUPLE_INDEX,
-                  cap: int | None = None):
+                  cap: int | None = None, out: np.ndarray | None = None):
+        """ldb_scan_file on a host image. `out`: the caller's tuple array (e.g. page-locked with
+        host_register, so the kernels write it in place); default a fresh one of `cap` tuples."""
         img = np.ascontiguousarray(img, dtype=np.uint8)
-        if cap is None:
-            cap = img.size // 10 + 16
         dt = N.INDEX_TUPLE if kind == N.TUPLE_INDEX else N.ENTRY_TUPLE
-        out = np.zeros(max(cap, 1), dtype=dt)
+        if out is not None:
+            assert out.dtype == dt and out.flags.c_contiguous
+            cap = out.size
+        else:
+            if cap is None:
+                cap = img.size // 10 + 16
+            out = np.zeros(max(cap, 1), dtype=dt)
         res = N.ScanResult()
         N.check(N.lib().ldb_scan_file(self.ctx, img.ctypes.data if img.size else None, img.size, fid, io_type, kind,
                                       out.ctypes.data, cap, C.byref(res)), "ldb_scan_file")

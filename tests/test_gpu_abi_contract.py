@@ -104,6 +104,37 @@ def test_bytes_past_len_ignored(gpu_engine):
                     same(res, tup, ref, rt)
 
 
+def test_scan_host_chunked_run_prefix(gpu_engine):
+    """ldb_scan_file stages the image in 64 MiB chunks and runs the run prefix chunk by chunk as they
+    land (ChunkPlan): runs that span chunks, a corrupt entry two chunks in, a run that ends mid-chunk
+    and is followed by other entries, and Zipf values (no run); pageable and page-locked images,
+    staged and in-place (LDB_DIRECT_IMAGE) reads."""
+    import os
+    eng = gpu_engine
+    run = coracle.gen_log(150 << 20, 61, ksize=64, vsize=256)[0]
+    bad = run.copy()
+    bad[(100 << 20) + 77] ^= 0x02
+    mixed = np.concatenate([run[: (90 << 20) // 332 * 332],
+                            coracle.gen_log(40 << 20, 62, ksize=16, vsize=40)[0]])
+    zipf = coracle.gen_log(130 << 20, 63, ksize=64, value_mode=1, zipf_max=2048)[0]
+    for img in (run, bad, mixed, zipf):
+        ref = coracle.scan(img, 0, fid=3)
+        res, tup = eng.scan_host(img, fid=3)
+        same(res, tup, *ref)
+        eng.host_register(img)
+        try:
+            for direct in (False, True):
+                if direct:
+                    os.environ["LDB_DIRECT_IMAGE"] = "1"
+                try:
+                    res, tup = eng.scan_host(img, fid=3)
+                finally:
+                    os.environ.pop("LDB_DIRECT_IMAGE", None)
+                same(res, tup, *ref)
+        finally:
+            eng.host_unregister(img)
+
+
 def test_five_contexts_five_threads():
     """index.go:103-108: one replay per value type, concurrently; each thread owns a context and a
     stream and scans its fids in ascending order (index.go:68)."""
@@ -178,17 +209,43 @@ def test_one_context_two_streams_no_host_sync(gpu_engine):
 
 
 def test_host_register_path(gpu_engine):
+    """ldb_scan_file on a page-locked image scans it in place over PCIe (no staging copy, region
+    pipeline only); on pageable memory it stages the image in chunks over the copy streams. Both
+    against the oracle: equal-sized entries, Zipf values, a corrupt entry, both IO rules and tuple
+    kinds; an unaligned-length image (its last 16-B granule lies partly past len)."""
     eng = gpu_engine
-    img = coracle.gen_log(32 << 20, 41, ksize=64, vsize=256)[0]
-    eng.host_register(img)
-    try:
-        for kind in (0, 1):
-            res, tup = eng.scan_host(img, fid=7, kind=kind)
-            same(res, tup, *coracle.scan(img, 0, fid=7, tuple_kind=kind))
-    finally:
-        eng.host_unregister(img)
-    res, tup = eng.scan_host(img, fid=7)
-    same(res, tup, *coracle.scan(img, 0, fid=7))
+    imgs = [coracle.gen_log(32 << 20, 41, ksize=64, vsize=256)[0],
+            coracle.gen_log(24 << 20, 42, ksize=64, value_mode=1, zipf_max=1024)[0]]
+    bad = imgs[1].copy()
+    bad[bad.size // 3] ^= 0x21
+    imgs += [bad, imgs[0][: (16 << 20) + 13].copy()]
+    for img in imgs:
+        eng.host_register(img)
+        try:
+            for kind in (0, 1):
+                for io in (0, 1):
+                    res, tup = eng.scan_host(img, fid=7, io_type=io, kind=kind)
+                    same(res, tup, *coracle.scan(img, io, fid=7, tuple_kind=kind))
+        finally:
+            eng.host_unregister(img)
+        res, tup = eng.scan_host(img, fid=7)
+        same(res, tup, *coracle.scan(img, 0, fid=7))
+        # a page-locked tuple array is written in place (with the image staged, then in place too)
+        from lazydb_amd import _native as N
+        hout = np.zeros(img.size // 10 + 16, dtype=N.INDEX_TUPLE)
+        eng.host_register(hout)
+        try:
+            res, tup = eng.scan_host(img, fid=7, out=hout)
+            same(res, tup, *coracle.scan(img, 0, fid=7))
+            eng.host_register(img)
+            try:
+                hout[:] = np.zeros(1, dtype=N.INDEX_TUPLE)
+                res, tup = eng.scan_host(img, fid=7, io_type=1, out=hout)
+                same(res, tup, *coracle.scan(img, 1, fid=7))
+            finally:
+                eng.host_unregister(img)
+        finally:
+            eng.host_unregister(hout)
 
 
 def test_fresh_context_first_merge_after_dirty_release():
