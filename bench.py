@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--xmerge", action="store_true",
                     help="config 5 as ONE 16-file set split over the ranks in fid blocks (cross-GPU merge)")
+    ap.add_argument("--xhash", action="store_true",
+                    help="with --xmerge/--xsim: the hash-partitioned liveness (route, owner resolve, apply)")
     ap.add_argument("--xsim", type=int, default=0,
                     help="config 5 --xmerge: play K ranks in this one process and time each rank's phases")
     ap.add_argument("--e2e", type=int, default=3, help="iterations of the PCIe-inclusive host-API leg (0: skip)")
@@ -412,6 +414,52 @@ def main_xmerge(args):
     def sync():
         torch.cuda.synchronize()
 
+    if sim and args.xhash:
+        engs = [eng] + [Engine(local) for _ in range(nr - 1)]
+        names = ["route", "resolve", "apply", "place"]
+        ph = np.zeros((nr, len(names)))
+        cur = {"on": False}
+
+        def timer(r, phase, fn):
+            sync()
+            t0 = time.perf_counter()
+            out = fn()
+            sync()
+            if cur["on"]:
+                ph[r, names.index(phase)] += time.perf_counter() - t0
+            return out
+
+        own = [[dfiles[i] for i in b] for b in blocks]
+        for step in range(args.warmup + args.steps):
+            cur["on"] = step >= args.warmup
+            parts, places = X.hashed_sim(engs, own, kw["active_fid"], kw["active_off"], kw["max_file_size"],
+                                         kw["now"], timer=timer)
+        ph /= args.steps
+        verified = None
+        if ref is not None:
+            verified = bool(b"".join(p["stream"].cpu().numpy().tobytes() for p in parts) == ref[1].tobytes()
+                            and places[-1]["end"] == (ref[0].end_fid, ref[0].end_off))
+        crit = float(ph.max(axis=0).sum())
+        # bytes that cross between ranks: route records + keys to other owners, one flag byte back each
+        xbytes = 0
+        for r in range(nr):
+            ro = X.route_phase(engs[r], own[r], nr)
+            for o in range(nr):
+                if o != r:
+                    xbytes += ro["rec_splits"][o] + ro["key_splits"][o] + int(ro["counts"][o])
+        print(json.dumps({
+            "metric": "merge/GC decode+CRC32+liveness+compaction: input GiB/s (BASELINE config 5), simulated ranks, "
+                      "hash-partitioned liveness",
+            "simulated_ranks": nr, "steps": args.steps, "warmup": args.warmup,
+            "per_rank_ms": {k: [round(x * 1e3, 3) for x in ph[:, i]] for i, k in enumerate(names)},
+            "critical_path_ms": round(crit * 1e3, 3),
+            "est_GiB_per_s_without_exchange": round(in_bytes / crit / 2**30, 3),
+            "exchange_bytes_between_ranks": xbytes,
+            "exchange_ms_at_xgmi_7x153GBps_per_gpu": round(xbytes / nr / (7 * 153e9) * 1e3, 3),
+            "verified_vs_oracle": verified}))
+        for e in engs:
+            e.close()
+        return
     if sim:
         ph = np.zeros((nr, 3))
         verified = None
@@ -452,6 +500,8 @@ def main_xmerge(args):
     files = [dfiles[i] for i in mine]
 
     def step_once():
+        if world > 1 and args.xhash:
+            return X.merge_hashed_distributed(eng, files, **kw, fetch_pos=False)
         return (X.merge_distributed(eng, files, 16, **kw, fetch_pos=False) if world > 1
                 else X.merge_distributed_single(eng, files, **kw, fetch_pos=False))
 
@@ -487,7 +537,9 @@ def main_xmerge(args):
             "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (writeLogEntry format, every key written twice)",
             "config": {"workload": "16 log files x 256 MiB, 64B key / 256B value, 50% stale, 15 targets",
-                       "parallelism": f"fid blocks over {world} GPU(s), summary all-gather + rollover chain"},
+                       "parallelism": f"fid blocks over {world} GPU(s), " + (
+                           "hash-partitioned liveness (2 all-to-alls)" if args.xhash else "summary all-gather") +
+                       " + rollover chain"},
             "verified_vs_oracle": verified}))
     eng.close()
     if world > 1:

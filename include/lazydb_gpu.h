@@ -284,6 +284,49 @@ int ldb_merge_repack_dev(ldb_ctx* ctx, uint64_t n, const uint32_t* d_sizes, ldb_
                          uint32_t active_fid, uint64_t active_off, uint64_t max_file_size,
                          ldb_merge_segment* h_segs, uint32_t seg_cap, ldb_merge_result* h_result, void* stream);
 
+/* ---- hash-partitioned cross-GPU merge -----------------------------------------
+ * Config 5 over N ranks, each holding a contiguous fid block (blocks ascending in rank order):
+ *   1. ldb_merge_route_dev on every rank: replay scans of its files, then every record is routed to
+ *      the owner of its key (owner = ((hash >> 32) * N) >> 32): route records and key bytes grouped
+ *      by owner, ready for one all-to-all (RCCL).
+ *   2. ldb_merge_resolve_dev on every owner, over what it received from all ranks: per record, is it
+ *      the last record of its key in the global order (source rank, seq)?  One flag byte per record,
+ *      returned to the sender by a second all-to-all.
+ *   3. ldb_merge_apply_dev on every rank: ldb_merge_files_dev with that liveness instead of its own
+ *      table (db.go:255 index[key] == (fid, offset) == last record of the key and not an SDelete).
+ *   4. ldb_merge_repack_dev: the rollover chain across ranks, as before. */
+typedef struct ldb_route_rec {
+  uint64_t hash;      /* 64-bit hash of the key bytes */
+  uint32_t seq;       /* the record's index in the sender's replay order (its files concatenated) */
+  uint32_t k_size;    /* key length */
+  uint64_t key_off;   /* offset of the key bytes in the sender's blob for this owner (16-B aligned) */
+} ldb_route_rec;
+
+/* Route the records of this rank's files (ascending fids) to n_owners owners (1..64). d_recs: device,
+ * rec_cap records; d_keys: device, key_cap bytes. On return h_counts[o] = records for owner o and
+ * h_counts[n_owners + o] = key bytes for owner o (16-B padded per key); owner o's records are
+ * d_recs[sum_{p<o} h_counts[p] ...] and its keys d_keys[sum_{p<o} h_counts[n_owners+p] ...], in no
+ * particular order inside an owner. h_result: n_records, or a file's fatal scan status (bad_file).
+ * LDB_ERR_CAPACITY: rec_cap or key_cap too small (h_counts holds the sizes). Synchronous. */
+int ldb_merge_route_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type, uint32_t n_owners,
+                        ldb_route_rec* d_recs, uint64_t rec_cap, uint8_t* d_keys, uint64_t key_cap,
+                        uint64_t* h_counts, ldb_merge_result* h_result, void* stream);
+
+/* Owner side: n received route records (device), their key bytes (device; each record's key_off
+ * already rebased into this concatenated blob) and their global order d_ord[i] = source rank << 32 |
+ * seq (device). d_last[i] = 1 iff record i is the last record of its key. Synchronous. */
+int ldb_merge_resolve_dev(ldb_ctx* ctx, uint64_t n, const ldb_route_rec* d_recs, const uint8_t* d_keys,
+                          const uint64_t* d_ord, uint8_t* d_last, void* stream);
+
+/* ldb_merge_files_dev with the liveness resolved elsewhere: d_last (device, one byte per replayed record
+ * of `files`, replay order) = "last record of its key" from the owners. Reuses the replay scan of the
+ * preceding ldb_merge_route_dev on this context when the file list is the same (images unchanged). */
+int ldb_merge_apply_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type, const uint8_t* d_last,
+                        uint32_t active_fid, uint64_t active_off, uint64_t max_file_size, int64_t now,
+                        uint8_t* d_stream, uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap,
+                        ldb_merge_segment* h_segs, uint32_t seg_cap, uint8_t* d_live, uint64_t live_cap,
+                        ldb_merge_file_stat* h_stats, ldb_merge_result* h_result, void* stream);
+
 /* Timing hook for bench.py: device time (ms) of the last ldb_merge_files_dev call, split into the
  * replay scans, the liveness resolution (hash + last-writer-wins) and the compaction (prefix sums,
  * rollover packing, stream copy), measured with HIP events on the merge stream. */

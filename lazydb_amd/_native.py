@@ -58,6 +58,8 @@ ENCODE_ITEM = np.dtype([("key_off", "<u8"), ("value_off", "<u8"), ("k_size", "<u
                         ("pad_", "u1", (5,))])
 assert C.sizeof(MergeFile) == 24 and C.sizeof(MergeResult) == 56 and ENCODE_ITEM.itemsize == 48
 assert MERGE_POS.itemsize == 32 and MERGE_SEGMENT.itemsize == 32 and MERGE_FILE_STAT.itemsize == 40
+ROUTE_REC = np.dtype([("hash", "<u8"), ("seq", "<u4"), ("k_size", "<u4"), ("key_off", "<u8")])   # ldb_route_rec
+assert ROUTE_REC.itemsize == 24
 
 RESULT_BYTES = C.sizeof(ScanResult)
 assert RESULT_BYTES == 48
@@ -112,6 +114,14 @@ def lib():
         if hasattr(L, "ldb_merge_repack_dev"):
             L.ldb_merge_repack_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u32, vp, vp]
             L.ldb_merge_repack_dev.restype = i32
+        if hasattr(L, "ldb_merge_route_dev"):
+            L.ldb_merge_route_dev.argtypes = [vp, i32, vp, i32, u32, vp, u64, vp, u64, vp, C.POINTER(MergeResult), vp]
+            L.ldb_merge_route_dev.restype = i32
+            L.ldb_merge_resolve_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+            L.ldb_merge_resolve_dev.restype = i32
+            L.ldb_merge_apply_dev.argtypes = [vp, i32, vp, i32, vp, u32, u64, u64, C.c_int64, vp, u64, vp, u64, vp,
+                                              u32, vp, u64, vp, C.POINTER(MergeResult), vp]
+            L.ldb_merge_apply_dev.restype = i32
         if hasattr(L, "ldb_encode_entries_dev"):
             L.ldb_encode_entries_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u64, vp, u64, vp, u32,
                                                  C.POINTER(MergeResult), vp]
@@ -125,7 +135,8 @@ def lib():
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
            "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_kernel_timing_split", "ldb_read_ceiling", "ldb_merge_files_dev",
-           "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_merge_repack_dev", "ldb_host_register", "ldb_host_unregister")
+           "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_merge_repack_dev", "ldb_host_register", "ldb_host_unregister",
+           "ldb_merge_route_dev", "ldb_merge_resolve_dev", "ldb_merge_apply_dev")
 
 
 def status_str(s: int) -> str:

@@ -47,6 +47,7 @@ constexpr uint8_t kSDelete = 1;  // logfile/log_entry.go:13-14
 constexpr int kScanItems = 8;    // items per thread in the prefix-sum kernels
 constexpr int kScanBlock = 256;
 constexpr uint64_t kScanTile = (uint64_t)kScanItems * kScanBlock;
+constexpr uint32_t kMaxOwners = 64;   // ranks of a hash-partitioned merge (ldb_merge_route_dev)
 
 struct FileDesc {       // one input file, in device memory
   const uint8_t* img;
@@ -77,6 +78,13 @@ struct MergeWs {
   ldb_ctx* aux = nullptr;
   hipStream_t aux_s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  // the last replay scan (ldb_merge_route_dev), reused by ldb_merge_apply_dev on the same files
+  bool cache_ok = false;
+  int cache_io = 0;
+  std::vector<ldb_merge_file> cache_files;
+  std::vector<FileDesc> cache_fdh;
+  std::vector<ldb_scan_result> cache_rh;
+  uint64_t cache_n = 0;
 };
 
 #define MHIP(x)                                    \
@@ -249,9 +257,11 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
 // live = last record of its key and not an SDelete (index.go:16-25); emit = live && target file &&
 // not expired (db.go:403-409, 255). Per-file live counts/bytes: a block whose records all lie in one
 // file writes one partial (k_file_stats sums them); a block that straddles files adds per record.
+// last_in (cross-GPU merge, ldb_merge_apply_dev): "last record of its key" per record, resolved at the
+// key's owner rank, instead of the local table.
 __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
                                               const unsigned long long* __restrict__ tab,
-                                              const uint32_t* __restrict__ slot,
+                                              const uint32_t* __restrict__ slot, const uint8_t* __restrict__ last_in,
                                               int64_t now, uint8_t* __restrict__ live_out,
                                               uint32_t* __restrict__ esz, unsigned long long* __restrict__ part,
                                               unsigned long long* __restrict__ fstat) {
@@ -266,8 +276,8 @@ __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __rest
   if (valid) {
     f = file_of(fd, n_files, seq);
     const Rec e = rec_of(fd, f, seq);
-    const uint32_t mx = (uint32_t)tab[slot[seq]];
-    live = mx == (uint32_t)(seq + 1) && e.stat != kSDelete;
+    const bool lastw = last_in ? last_in[seq] != 0 : (uint32_t)tab[slot[seq]] == (uint32_t)(seq + 1);
+    live = lastw && e.stat != kSDelete;
     size = e.enc_hdr_size + e.k_size + e.v_size;
     bool emit = live && fd[f].is_target;
     if (emit) {
@@ -301,6 +311,131 @@ __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __rest
     part[2 * blockIdx.x] = sc[0] + sc[1] + sc[2] + sc[3];
     part[2 * blockIdx.x + 1] = sb[0] + sb[1] + sb[2] + sb[3];
   }
+}
+
+// ------------------------------------------------------------------------------ hash-partitioned liveness
+// Cross-GPU merge: every rank routes its replayed records to the rank that owns
+// their key (a function of the key hash), the owner resolves last-writer-wins over the keys it owns,
+// and returns one "last record of its key" flag per record. A key's records all meet at its owner,
+// so the owner's maximum of the global record order (source rank, record index) per key is exactly
+// the key's last record over all files (index.go:68-95 replays fids in ascending order, the fid
+// blocks are ascending in rank order).
+__device__ __forceinline__ uint32_t owner_of(uint64_t h, uint32_t n_own) {
+  return (uint32_t)(((h >> 32) * (uint64_t)n_own) >> 32);   // the high half: the tables use the low bits
+}
+__device__ __forceinline__ uint64_t pad16(uint32_t k) { return ((uint64_t)k + 15) & ~15ull; }
+
+// pass 1: the key hash of every record, and per owner the record count and the key bytes (16-B
+// padded), aggregated per workgroup in LDS
+__global__ __launch_bounds__(256) void k_route_count(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
+                                                     uint32_t n_own, uint64_t* __restrict__ hsh,
+                                                     unsigned long long* __restrict__ tot) {
+  __shared__ FileDesc s_fd[kFdLds];
+  __shared__ unsigned long long sc[2 * kMaxOwners];
+  const FileDesc* fd = stage_fd(gfd, n_files, s_fd);
+  for (uint32_t i = threadIdx.x; i < 2 * n_own; i += blockDim.x) sc[i] = 0;
+  __syncthreads();
+  const uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seq < n) {
+    uint32_t kl;
+    const uint8_t* kp = key_of(fd, n_files, seq, &kl);
+    const uint64_t h = key_hash(kp, kl);
+    hsh[seq] = h;
+    const uint32_t o = owner_of(h, n_own);
+    atomicAdd(&sc[o], 1ull);
+    atomicAdd(&sc[n_own + o], (unsigned long long)pad16(kl));
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 2 * n_own; i += blockDim.x)
+    if (sc[i]) atomicAdd(&tot[i], sc[i]);
+}
+
+// pass 2: each record's route record and key bytes into its owner's bucket. A workgroup reserves one
+// range per owner (one global atomic per owner), then its records take slots inside it (LDS atomics):
+// the order inside a bucket is arbitrary, the owner orders by (source rank, seq).
+__global__ __launch_bounds__(256) void k_route_fill(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
+                                                    uint32_t n_own, const uint64_t* __restrict__ hsh,
+                                                    const unsigned long long* __restrict__ base,
+                                                    unsigned long long* __restrict__ cur,
+                                                    ldb_route_rec* __restrict__ recs, uint8_t* __restrict__ keys) {
+  __shared__ FileDesc s_fd[kFdLds];
+  __shared__ unsigned long long sc[2 * kMaxOwners], sb[2 * kMaxOwners];
+  const FileDesc* fd = stage_fd(gfd, n_files, s_fd);
+  for (uint32_t i = threadIdx.x; i < 2 * n_own; i += blockDim.x) sc[i] = 0;
+  __syncthreads();
+  const uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = seq < n;
+  uint32_t kl = 0, o = 0;
+  const uint8_t* kp = nullptr;
+  uint64_t h = 0, my_r = 0, my_k = 0;
+  if (valid) {
+    kp = key_of(fd, n_files, seq, &kl);
+    h = hsh[seq];
+    o = owner_of(h, n_own);
+    my_r = atomicAdd(&sc[o], 1ull);
+    my_k = atomicAdd(&sc[n_own + o], (unsigned long long)pad16(kl));
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 2 * n_own; i += blockDim.x) sb[i] = sc[i] ? atomicAdd(&cur[i], sc[i]) : 0;
+  __syncthreads();
+  if (!valid) return;
+  const uint64_t r = base[o] + sb[o] + my_r, koff = sb[n_own + o] + my_k;   // key offset inside the owner's blob
+  ldb_route_rec rec;
+  rec.hash = h;
+  rec.seq = (uint32_t)seq;
+  rec.k_size = kl;
+  rec.key_off = koff;
+  recs[r] = rec;
+  uint8_t* dst = keys + base[n_own + o] + koff;   // 16-B aligned
+  uint32_t i = 0;
+  for (; i + 16 <= kl; i += 16) {
+    uint4 x;
+    __builtin_memcpy(&x, kp + i, 16);
+    *reinterpret_cast<uint4*>(dst + i) = x;
+  }
+  if (i < kl) {
+    uint8_t t[16] = {};
+    for (uint32_t j = 0; i + j < kl; ++j) t[j] = kp[i + j];
+    uint4 x;
+    __builtin_memcpy(&x, t, 16);
+    *reinterpret_cast<uint4*>(dst + i) = x;
+  }
+}
+
+// owner: the full-key table over the received records (keys at key_off in the received blob), as
+// k_insert, plus the maximum of the global order per key (ord = source rank << 32 | seq)
+__global__ __launch_bounds__(256) void k_own_insert(uint64_t n, const ldb_route_rec* __restrict__ recs,
+                                                    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ ord,
+                                                    unsigned long long* tab, unsigned long long* otab, uint64_t mask,
+                                                    uint32_t* __restrict__ slot) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 >= n) return;
+  const ldb_route_rec me = recs[i0];
+  const uint8_t* kp = keys + me.key_off;
+  const unsigned long long mine = (me.hash & 0xFFFFFFFF00000000ull) | (i0 + 1);
+  uint64_t i = me.hash & mask;
+  for (;;) {
+    unsigned long long v = __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0) {
+      const unsigned long long prev = atomicCAS(&tab[i], 0ull, mine);
+      if (prev == 0) break;
+      v = prev;
+    }
+    if ((v >> 32) == (me.hash >> 32)) {
+      const ldb_route_rec rep = recs[(v & 0xFFFFFFFFull) - 1];
+      if (rep.k_size == me.k_size && key_equal(kp, keys + rep.key_off, me.k_size)) break;
+    }
+    i = (i + 1) & mask;
+  }
+  atomicMax(&otab[i], (unsigned long long)(ord[i0] + 1));
+  slot[i0] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_own_last(uint64_t n, const uint64_t* __restrict__ ord,
+                                                  const unsigned long long* __restrict__ otab,
+                                                  const uint32_t* __restrict__ slot, uint8_t* __restrict__ last) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) last[i] = otab[slot[i]] == ord[i] + 1 ? 1 : 0;
 }
 
 // one workgroup per file: sum the partials of the k_live blocks that lie wholly inside it
@@ -839,49 +974,36 @@ __attribute__((visibility("hidden"))) void ldb_merge_release_(void* p) {
   delete m;
 }
 
-extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type,
-                                   uint32_t active_fid, uint64_t active_off, uint64_t max_file_size, int64_t now,
-                                   uint8_t* d_stream, uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap,
-                                   ldb_merge_segment* h_segs, uint32_t seg_cap, uint8_t* d_live, uint64_t live_cap,
-                                   ldb_merge_file_stat* h_stats, ldb_merge_result* h_result, void* stream) {
-  if (!ctx || !h_result || n_files < 0 || (n_files && !files) || max_file_size == 0 ||
-      (io_type != LDB_IO_FILEIO && io_type != LDB_IO_MMAP))
-    return LDB_ERR_ARG;
-  std::memset(h_result, 0, sizeof(*h_result));
-  h_result->bad_file = -1;
-  h_result->end_fid = active_fid;
-  h_result->end_off = active_off;
-  for (int i = 0; i < n_files; ++i) {
-    if (i && files[i].fid <= files[i - 1].fid) return h_result->status = LDB_ERR_ARG;   // ascending fids
-    if (files[i].is_target && files[i].fid == active_fid) return h_result->status = LDB_ERR_ARG;
-    if (files[i].len && !files[i].d_image) return h_result->status = LDB_ERR_ARG;
-  }
-  if (hipSetDevice(ldb_ctx_device_(ctx)) != hipSuccess) return LDB_ERR_HIP;
-  MergeWs* m = get_ws(ctx);
-  if (!m) return LDB_ERR_NOMEM;
-  hipStream_t s = (hipStream_t)stream;
-  const uint32_t nf = (uint32_t)n_files;
+namespace {
 
-  // small device buffer: scan results | file descriptors (nf+1) | per-file stats (2 u64) | tail | segments
-  const uint64_t o_res = 0, o_fd = align256(o_res + sizeof(ldb_scan_result) * (nf + 1));
-  const uint64_t o_fst = align256(o_fd + sizeof(FileDesc) * (nf + 1));
-  const uint64_t o_tail = align256(o_fst + 16ull * (nf + 1));
-  const uint64_t o_seg = align256(o_tail + sizeof(Tail));
-  const uint64_t small_need = o_seg + sizeof(ldb_merge_segment) * ((uint64_t)seg_cap + 1);
-  int rc = grow(&m->small, &m->small_bytes, small_need);
-  if (rc != LDB_OK) return rc;
-  ldb_scan_result* d_res = reinterpret_cast<ldb_scan_result*>(m->small + o_res);
-  FileDesc* d_fd = reinterpret_cast<FileDesc*>(m->small + o_fd);
-  unsigned long long* d_fst = reinterpret_cast<unsigned long long*>(m->small + o_fst);
-  Tail* d_tail = reinterpret_cast<Tail*>(m->small + o_tail);
-  ldb_merge_segment* d_segs = reinterpret_cast<ldb_merge_segment*>(m->small + o_seg);
-
-  // ---- 1. replay scans (index.go:84-95 per file), 16-B index tuples. All files are enqueued back to back,
-  // each into its own slot of len/64 + 1024 records, and read back with one synchronisation; only
-  // if a file has more records than its slot are the files rescanned one by one into dense storage.
-  MHIP(hipEventRecord(m->ev[0], s));
-  std::vector<FileDesc> fdh(nf + 1);
+// Step 1 of every merge entry point: the replay scans (index.go:84-95 per file), 16-B index tuples.
+// All files are enqueued back to back, each into its own slot of len/64 + 1024 records, and read back
+// with one synchronisation; only if a file has more records than its slot are the files rescanned
+// one by one into dense storage. Fills fdh (nf + 1 descriptors; is_target from `files`) and n. A fatal
+// scan status of a file is returned with h_result's status / bad_file / n_records set. With
+// use_cache, the previous scan of the same files (ldb_merge_route_dev's) is reused.
+int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* files, int io_type,
+               ldb_scan_result* d_res, std::vector<FileDesc>& fdh, uint64_t& n, ldb_merge_file_stat* h_stats,
+               ldb_merge_result* h_result, hipStream_t s, bool use_cache) {
+  fdh.assign(nf + 1, FileDesc{});
   std::vector<ldb_scan_result> rh(nf);
+  bool hit = use_cache && m->cache_ok && m->cache_io == io_type && m->cache_files.size() == nf;
+  for (uint32_t i = 0; hit && i < nf; ++i)
+    hit = m->cache_files[i].d_image == files[i].d_image && m->cache_files[i].len == files[i].len &&
+          m->cache_files[i].fid == files[i].fid;
+  if (hit) {
+    fdh = m->cache_fdh;
+    rh = m->cache_rh;
+    n = m->cache_n;
+    for (uint32_t i = 0; i < nf; ++i) {
+      fdh[i].is_target = files[i].is_target;
+      if (h_stats) h_stats[i] = ldb_merge_file_stat{rh[i].status, files[i].fid, rh[i].n_entries, rh[i].end_off, 0, 0};
+    }
+    h_result->n_records = n;
+    return LDB_OK;
+  }
+  m->cache_ok = false;   // m->recs is rewritten below
+  int rc = LDB_OK;
   std::vector<uint64_t> sbase(nf + 1, 0);
   for (uint32_t i = 0; i < nf; ++i) sbase[i + 1] = sbase[i] + files[i].len / 64 + 1024;
   rc = grow_recs(m, std::max<uint64_t>(sbase[nf], 4096), 0, s);
@@ -947,10 +1069,67 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
     }
     base += rh[i].n_entries;
   }
-  const uint64_t n = base;
+  n = base;
   fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0};
   h_result->n_records = n;
   if (n >= 0xFFFFFFFFull) return h_result->status = LDB_ERR_ARG;   // record ids are 32-bit
+  m->cache_ok = true;
+  m->cache_io = io_type;
+  m->cache_files.assign(files, files + nf);
+  m->cache_fdh = fdh;
+  m->cache_rh = rh;
+  m->cache_n = n;
+  return LDB_OK;
+}
+
+}  // namespace
+
+
+namespace {
+
+int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type, bool ext_live,
+               const uint8_t* last_in, uint32_t active_fid, uint64_t active_off, uint64_t max_file_size, int64_t now, uint8_t* d_stream,
+               uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap, ldb_merge_segment* h_segs,
+               uint32_t seg_cap, uint8_t* d_live, uint64_t live_cap, ldb_merge_file_stat* h_stats,
+               ldb_merge_result* h_result, void* stream) {
+  if (!ctx || !h_result || n_files < 0 || (n_files && !files) || max_file_size == 0 ||
+      (io_type != LDB_IO_FILEIO && io_type != LDB_IO_MMAP))
+    return LDB_ERR_ARG;
+  std::memset(h_result, 0, sizeof(*h_result));
+  h_result->bad_file = -1;
+  h_result->end_fid = active_fid;
+  h_result->end_off = active_off;
+  for (int i = 0; i < n_files; ++i) {
+    if (i && files[i].fid <= files[i - 1].fid) return h_result->status = LDB_ERR_ARG;   // ascending fids
+    if (files[i].is_target && files[i].fid == active_fid) return h_result->status = LDB_ERR_ARG;
+    if (files[i].len && !files[i].d_image) return h_result->status = LDB_ERR_ARG;
+  }
+  if (hipSetDevice(ldb_ctx_device_(ctx)) != hipSuccess) return LDB_ERR_HIP;
+  MergeWs* m = get_ws(ctx);
+  if (!m) return LDB_ERR_NOMEM;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t nf = (uint32_t)n_files;
+
+  // small device buffer: scan results | file descriptors (nf+1) | per-file stats (2 u64) | tail | segments
+  const uint64_t o_res = 0, o_fd = align256(o_res + sizeof(ldb_scan_result) * (nf + 1));
+  const uint64_t o_fst = align256(o_fd + sizeof(FileDesc) * (nf + 1));
+  const uint64_t o_tail = align256(o_fst + 16ull * (nf + 1));
+  const uint64_t o_seg = align256(o_tail + sizeof(Tail));
+  const uint64_t small_need = o_seg + sizeof(ldb_merge_segment) * ((uint64_t)seg_cap + 1);
+  int rc = grow(&m->small, &m->small_bytes, small_need);
+  if (rc != LDB_OK) return rc;
+  ldb_scan_result* d_res = reinterpret_cast<ldb_scan_result*>(m->small + o_res);
+  FileDesc* d_fd = reinterpret_cast<FileDesc*>(m->small + o_fd);
+  unsigned long long* d_fst = reinterpret_cast<unsigned long long*>(m->small + o_fst);
+  Tail* d_tail = reinterpret_cast<Tail*>(m->small + o_tail);
+  ldb_merge_segment* d_segs = reinterpret_cast<ldb_merge_segment*>(m->small + o_seg);
+
+  MHIP(hipEventRecord(m->ev[0], s));
+  std::vector<FileDesc> fdh;
+  uint64_t n = 0;
+  rc = merge_scan(ctx, m, nf, files, io_type, d_res, fdh, n, h_stats, h_result, s, ext_live);
+  if (rc != LDB_OK) return rc;
+  if (ext_live && n && !last_in) return h_result->status = LDB_ERR_ARG;   // liveness flags for n records
   MHIP(hipEventRecord(m->ev[1], s));
 
   // ---- 2. liveness
@@ -978,11 +1157,11 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   const bool live_ok = !d_live || live_cap >= n;
   MHIP(hipMemcpyAsync(d_fd, fdh.data(), sizeof(FileDesc) * (nf + 1), hipMemcpyHostToDevice, s));
   MHIP(hipMemsetAsync(d_fst, 0, 16ull * (nf + 1), s));
-  MHIP(hipMemsetAsync(d_tk, 0, 8 * tcap, s));   // hash table slots
+  if (!ext_live) MHIP(hipMemsetAsync(d_tk, 0, 8 * tcap, s));   // hash table slots
   const uint32_t nbk = (uint32_t)((n + 255) / 256);
   if (n) {
-    k_insert<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot);
-    k_live<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, d_slot, now, live_ok ? d_live : nullptr, d_esz, d_part,
+    if (!ext_live) k_insert<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot);
+    k_live<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, d_slot, last_in, now, live_ok ? d_live : nullptr, d_esz, d_part,
                                d_fst);
     k_file_stats<<<nf, 256, 0, s>>>(d_fd, nf, n, d_part, d_fst);
     MHIP(hipGetLastError());
@@ -1040,6 +1219,122 @@ extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   MHIP(hipEventElapsedTime(&m->t_live, m->ev[1], m->ev[2]));
   MHIP(hipEventElapsedTime(&m->t_compact, m->ev[2], m->ev[3]));
   h_result->status = LDB_OK;
+  return LDB_OK;
+}
+
+}  // namespace
+
+extern "C" int ldb_merge_files_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type,
+                                   uint32_t active_fid, uint64_t active_off, uint64_t max_file_size, int64_t now,
+                                   uint8_t* d_stream, uint64_t stream_cap, ldb_merge_pos* d_pos, uint64_t pos_cap,
+                                   ldb_merge_segment* h_segs, uint32_t seg_cap, uint8_t* d_live, uint64_t live_cap,
+                                   ldb_merge_file_stat* h_stats, ldb_merge_result* h_result, void* stream) {
+  return merge_impl(ctx, n_files, files, io_type, false, nullptr, active_fid, active_off, max_file_size, now,
+                    d_stream, stream_cap, d_pos, pos_cap, h_segs, seg_cap, d_live, live_cap, h_stats, h_result, stream);
+}
+
+extern "C" int ldb_merge_apply_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type,
+                                   const uint8_t* d_last, uint32_t active_fid, uint64_t active_off,
+                                   uint64_t max_file_size, int64_t now, uint8_t* d_stream, uint64_t stream_cap,
+                                   ldb_merge_pos* d_pos, uint64_t pos_cap, ldb_merge_segment* h_segs, uint32_t seg_cap,
+                                   uint8_t* d_live, uint64_t live_cap, ldb_merge_file_stat* h_stats,
+                                   ldb_merge_result* h_result, void* stream) {
+  // d_last may be NULL only when the files hold no record (checked after the scan)
+  const int rc = merge_impl(ctx, n_files, files, io_type, true, d_last, active_fid, active_off, max_file_size, now,
+                            d_stream, stream_cap, d_pos, pos_cap, h_segs, seg_cap, d_live, live_cap, h_stats, h_result,
+                            stream);
+  if (rc != LDB_ERR_CAPACITY) {   // the route's scan is used once (a capacity retry may reuse it)
+    MergeWs* m = static_cast<MergeWs*>(*ldb_ctx_merge_slot_(ctx));
+    if (m) m->cache_ok = false;
+  }
+  return rc;
+}
+
+extern "C" int ldb_merge_route_dev(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_type,
+                                   uint32_t n_owners, ldb_route_rec* d_recs, uint64_t rec_cap, uint8_t* d_keys,
+                                   uint64_t key_cap, uint64_t* h_counts, ldb_merge_result* h_result, void* stream) {
+  if (!ctx || !h_result || !h_counts || n_files < 0 || (n_files && !files) || n_owners == 0 ||
+      n_owners > kMaxOwners || (io_type != LDB_IO_FILEIO && io_type != LDB_IO_MMAP))
+    return LDB_ERR_ARG;
+  std::memset(h_result, 0, sizeof(*h_result));
+  h_result->bad_file = -1;
+  std::memset(h_counts, 0, sizeof(uint64_t) * 2 * n_owners);
+  for (int i = 0; i < n_files; ++i) {
+    if (i && files[i].fid <= files[i - 1].fid) return h_result->status = LDB_ERR_ARG;
+    if (files[i].len && !files[i].d_image) return h_result->status = LDB_ERR_ARG;
+  }
+  if (hipSetDevice(ldb_ctx_device_(ctx)) != hipSuccess) return LDB_ERR_HIP;
+  MergeWs* m = get_ws(ctx);
+  if (!m) return LDB_ERR_NOMEM;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t nf = (uint32_t)n_files;
+  const uint64_t o_res = 0, o_fd = align256(sizeof(ldb_scan_result) * (nf + 1));
+  const uint64_t o_cnt = align256(o_fd + sizeof(FileDesc) * (nf + 1));
+  int rc = grow(&m->small, &m->small_bytes, o_cnt + 3 * 16ull * kMaxOwners);
+  if (rc != LDB_OK) return rc;
+  ldb_scan_result* d_res = reinterpret_cast<ldb_scan_result*>(m->small + o_res);
+  FileDesc* d_fd = reinterpret_cast<FileDesc*>(m->small + o_fd);
+  unsigned long long* d_tot = reinterpret_cast<unsigned long long*>(m->small + o_cnt);   // 2 n_own
+  unsigned long long* d_base = d_tot + 2 * kMaxOwners;
+  unsigned long long* d_cur = d_base + 2 * kMaxOwners;
+  std::vector<FileDesc> fdh;
+  uint64_t n = 0;
+  rc = merge_scan(ctx, m, nf, files, io_type, d_res, fdh, n, nullptr, h_result, s, false);
+  if (rc != LDB_OK) return rc;
+  rc = grow(&m->seqbuf, &m->seqbuf_bytes, align256(8 * (n + 1)));
+  if (rc != LDB_OK) return rc;
+  uint64_t* d_h = reinterpret_cast<uint64_t*>(m->seqbuf);
+  MHIP(hipMemcpyAsync(d_fd, fdh.data(), sizeof(FileDesc) * (nf + 1), hipMemcpyHostToDevice, s));
+  MHIP(hipMemsetAsync(d_tot, 0, 3 * 16ull * kMaxOwners, s));
+  const uint32_t nbk = (uint32_t)((n + 255) / 256);
+  if (n) k_route_count<<<nbk, 256, 0, s>>>(n, d_fd, nf, n_owners, d_h, d_tot);
+  MHIP(hipGetLastError());
+  std::vector<unsigned long long> tot(2 * n_owners);
+  MHIP(hipMemcpyAsync(tot.data(), d_tot, sizeof(unsigned long long) * 2 * n_owners, hipMemcpyDeviceToHost, s));
+  MHIP(hipStreamSynchronize(s));
+  std::vector<unsigned long long> base(2 * n_owners);
+  uint64_t nr = 0, nk = 0;
+  for (uint32_t o = 0; o < n_owners; ++o) {
+    h_counts[o] = tot[o];
+    h_counts[n_owners + o] = tot[n_owners + o];
+    base[o] = nr;
+    base[n_owners + o] = nk;
+    nr += tot[o];
+    nk += tot[n_owners + o];
+  }
+  h_result->n_records = n;
+  if (nr > rec_cap || nk > key_cap || (nr && (!d_recs || !d_keys))) return h_result->status = LDB_ERR_CAPACITY;
+  MHIP(hipMemcpyAsync(d_base, base.data(), sizeof(unsigned long long) * 2 * n_owners, hipMemcpyHostToDevice, s));
+  if (n) k_route_fill<<<nbk, 256, 0, s>>>(n, d_fd, nf, n_owners, d_h, d_base, d_cur, d_recs, d_keys);
+  MHIP(hipGetLastError());
+  MHIP(hipStreamSynchronize(s));
+  h_result->status = LDB_OK;
+  return LDB_OK;
+}
+
+extern "C" int ldb_merge_resolve_dev(ldb_ctx* ctx, uint64_t n, const ldb_route_rec* d_recs, const uint8_t* d_keys,
+                                     const uint64_t* d_ord, uint8_t* d_last, void* stream) {
+  if (!ctx || (n && (!d_recs || !d_keys || !d_ord || !d_last)) || n >= 0xFFFFFFFFull) return LDB_ERR_ARG;
+  if (hipSetDevice(ldb_ctx_device_(ctx)) != hipSuccess) return LDB_ERR_HIP;
+  MergeWs* m = get_ws(ctx);
+  if (!m) return LDB_ERR_NOMEM;
+  hipStream_t s = (hipStream_t)stream;
+  if (!n) return LDB_OK;
+  uint64_t tcap = 1024;
+  while (tcap < n + n / 4) tcap <<= 1;
+  const uint64_t o_tab = 0, o_otab = align256(8 * tcap), o_slot = align256(o_otab + 8 * tcap);
+  // (m->seqbuf only: the route's scan in m->recs stays valid for the rank's ldb_merge_apply_dev)
+  int rc = grow(&m->seqbuf, &m->seqbuf_bytes, align256(o_slot + 4 * n));
+  if (rc != LDB_OK) return rc;
+  unsigned long long* d_tab = reinterpret_cast<unsigned long long*>(m->seqbuf + o_tab);
+  unsigned long long* d_otab = reinterpret_cast<unsigned long long*>(m->seqbuf + o_otab);
+  uint32_t* d_slot = reinterpret_cast<uint32_t*>(m->seqbuf + o_slot);
+  MHIP(hipMemsetAsync(m->seqbuf, 0, o_slot, s));   // both tables
+  const uint32_t nbk = (uint32_t)((n + 255) / 256);
+  k_own_insert<<<nbk, 256, 0, s>>>(n, d_recs, d_keys, d_ord, d_tab, d_otab, tcap - 1, d_slot);
+  k_own_last<<<nbk, 256, 0, s>>>(n, d_ord, d_otab, d_slot, d_last);
+  MHIP(hipGetLastError());
+  MHIP(hipStreamSynchronize(s));
   return LDB_OK;
 }
 

@@ -114,27 +114,21 @@ class Engine:
     def merge_dev(self, files, active_fid: int, active_off: int, max_file_size: int, now: int,
                   io_type: int = N.FILEIO, stream_cap: int | None = None, pos_cap: int | None = None,
                   seg_cap: int = 256, live_cap: int | None = None, want_live: bool = True, stream=None,
-                  fetch_pos: bool = True):
+                  fetch_pos: bool = True, last=None):
         """Merge the target files of one value type (db.go:383-427 Merge + mergeStr + writeLogEntry).
 
         files: list of (device uint8 tensor, fid, is_target), ascending fid. Returns a dict with
         'result' (MergeResult), 'stream' (device tensor, the compacted bytes), 'pos' (ldb_merge_pos
         records, numpy), 'segments' (numpy), 'live' (device uint8 tensor, one flag per replayed record)
         and 'stats' (per-file numpy). Outputs that turn out too small are re-sized and the call repeated
-        (LDB_ERR_CAPACITY reports the sizes needed)."""
+        (LDB_ERR_CAPACITY reports the sizes needed). last: a device uint8 tensor, one "last record of
+        its key" flag per replayed record resolved by the key owners (cross-GPU merge): then
+        ldb_merge_apply_dev."""
         t = self.torch
         dev = f"cuda:{self.device}"
-        arr = (N.MergeFile * max(len(files), 1))()
-        tgt_len = 0
-        tot_len = 0
-        for i, (img, fid, tg) in enumerate(files):
-            assert img.dtype == t.uint8 and img.is_cuda and img.is_contiguous()
-            arr[i].d_image = img.data_ptr() if img.numel() else None
-            arr[i].len = img.numel()
-            arr[i].fid = fid
-            arr[i].is_target = 1 if tg else 0
-            tot_len += img.numel()
-            tgt_len += img.numel() if tg else 0
+        arr = self._merge_files(files)
+        tot_len = sum(img.numel() for img, _, _ in files)
+        tgt_len = sum(img.numel() for img, _, tg in files if tg)
         stream_cap = tgt_len if stream_cap is None else stream_cap
         pos_cap = tgt_len // 64 + 1024 if pos_cap is None else pos_cap
         live_cap = tot_len // 64 + 1024 if live_cap is None else live_cap
@@ -147,11 +141,16 @@ class Engine:
             segs = np.zeros(max(seg_cap, 1), dtype=N.MERGE_SEGMENT)
             stats = np.zeros(max(len(files), 1), dtype=N.MERGE_FILE_STAT)
             res = N.MergeResult()
-            rc = N.lib().ldb_merge_files_dev(
-                self.ctx, len(files), C.addressof(arr), io_type, active_fid, active_off, max_file_size, now,
-                d_stream.data_ptr(), stream_cap, d_pos.data_ptr(), pos_cap, segs.ctypes.data, seg_cap,
-                d_live.data_ptr() if want_live else None, live_cap if want_live else 0, stats.ctypes.data,
-                C.byref(res), C.c_void_p(stream.cuda_stream))
+            res.bad_file = -1   # an argument error returns before the library fills the result
+            tail = (active_fid, active_off, max_file_size, now, d_stream.data_ptr(), stream_cap, d_pos.data_ptr(),
+                    pos_cap, segs.ctypes.data, seg_cap, d_live.data_ptr() if want_live else None,
+                    live_cap if want_live else 0, stats.ctypes.data, C.byref(res), C.c_void_p(stream.cuda_stream))
+            if last is None:
+                rc = N.lib().ldb_merge_files_dev(self.ctx, len(files), C.addressof(arr), io_type, *tail)
+            else:
+                assert last.dtype == t.uint8 and last.is_cuda
+                rc = N.lib().ldb_merge_apply_dev(self.ctx, len(files), C.addressof(arr), io_type,
+                                                 C.c_void_p(last.data_ptr()) if last.numel() else None, *tail)
             if rc != N.ERR_CAPACITY or res.bad_file >= 0:
                 break
             stream_cap = max(stream_cap, res.emit_bytes)
@@ -169,6 +168,62 @@ class Engine:
         return {"rc": rc, "result": res, "stream": d_stream[: res.emit_bytes],
                 "pos": pos, "segments": segs[: min(res.n_segments, seg_cap)],
                 "live": d_live[: res.n_records] if want_live else None, "stats": stats[: len(files)]}
+
+    def _merge_files(self, files):
+        t = self.torch
+        arr = (N.MergeFile * max(len(files), 1))()
+        for i, (img, fid, tg) in enumerate(files):
+            assert img.dtype == t.uint8 and img.is_cuda and img.is_contiguous()
+            arr[i].d_image = img.data_ptr() if img.numel() else None
+            arr[i].len = img.numel()
+            arr[i].fid = fid
+            arr[i].is_target = 1 if tg else 0
+        return arr
+
+    def merge_route(self, files, n_owners: int, io_type: int = N.FILEIO, stream=None):
+        """ldb_merge_route_dev: this rank's records routed to n_owners key owners. Returns dict(result,
+        recs (device uint8, 24-B ldb_route_rec, grouped by owner), keys (device uint8, grouped by owner),
+        counts (numpy: records per owner), key_bytes (numpy: key bytes per owner))."""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        arr = self._merge_files(files)
+        if stream is None:
+            stream = t.cuda.current_stream(dev)
+        rec_cap = sum(img.numel() for img, _, _ in files) // 16 + 1024
+        key_cap = sum(img.numel() for img, _, _ in files) + 16 * rec_cap
+        for _attempt in range(2):
+            recs = t.empty(max(rec_cap, 1) * N.ROUTE_REC.itemsize, dtype=t.uint8, device=dev)
+            keys = t.empty(max(key_cap, 16), dtype=t.uint8, device=dev)
+            counts = np.zeros(2 * n_owners, dtype=np.uint64)
+            res = N.MergeResult()
+            res.bad_file = -1
+            rc = N.lib().ldb_merge_route_dev(self.ctx, len(files), C.addressof(arr), io_type, n_owners,
+                                             recs.data_ptr(), rec_cap, keys.data_ptr(), key_cap, counts.ctypes.data,
+                                             C.byref(res), C.c_void_p(stream.cuda_stream))
+            if rc != N.ERR_CAPACITY or res.bad_file >= 0:
+                break
+            rec_cap, key_cap = int(counts[:n_owners].sum()), int(counts[n_owners:].sum())
+        if rc != N.LDB_OK and res.bad_file < 0:
+            N.check(rc, "ldb_merge_route_dev")
+        nr, nk = int(counts[:n_owners].sum()), int(counts[n_owners:].sum())
+        return {"rc": rc, "result": res, "recs": recs[: nr * N.ROUTE_REC.itemsize], "keys": keys[:nk],
+                "counts": counts[:n_owners].astype(np.int64), "key_bytes": counts[n_owners:].astype(np.int64)}
+
+    def merge_resolve(self, recs, keys, ord_, stream=None):
+        """ldb_merge_resolve_dev at a key owner: recs (device uint8, 24-B route records, key_off rebased
+        into `keys`), keys (device uint8), ord_ (device int64: source rank << 32 | seq). Returns the
+        device uint8 "last record of its key" flags."""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        n = recs.numel() // N.ROUTE_REC.itemsize
+        last = t.empty(max(n, 1), dtype=t.uint8, device=dev)
+        if stream is None:
+            stream = t.cuda.current_stream(dev)
+        N.check(N.lib().ldb_merge_resolve_dev(self.ctx, n, recs.data_ptr() if n else None,
+                                              keys.data_ptr() if keys.numel() else None,
+                                              ord_.data_ptr() if n else None, last.data_ptr(),
+                                              C.c_void_p(stream.cuda_stream)), "ldb_merge_resolve_dev")
+        return last[:n]
 
     def encode_entries(self, items, blob, active_fid: int, active_off: int, max_file_size: int, seg_cap: int = 256,
                        stream=None):

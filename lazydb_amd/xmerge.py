@@ -155,6 +155,109 @@ def rank_place(eng, part, earlier_sizes, active_fid: int, active_off: int, max_f
     return {"start": (f0, o0), "end": (res.end_fid, res.end_off), "segments": segs, "pos": pos}
 
 
+# --------------------------------------------------------------------------- hash-partitioned liveness
+# The balanced form of coupling 1: instead of replaying the later ranks' summaries,
+# every rank routes each of its records to the owner of its key (ldb_merge_route_dev: 24-B route
+# record + key bytes, grouped by owner), one all-to-all delivers them, each owner resolves
+# last-writer-wins over ~1/N of the keys by the global order (source rank, seq)
+# (ldb_merge_resolve_dev), a second all-to-all returns one flag byte per record, and each rank merges
+# its own files with those flags (ldb_merge_apply_dev). Per rank the device work is its own 1/N of the
+# scans, of the hashing and of the table, whatever N.
+ROUTE_REC_BYTES = N.ROUTE_REC.itemsize
+
+
+def route_phase(eng, files, world: int, io_type: int = N.FILEIO):
+    """Phase H1 on one rank: its records and keys grouped by owner. Returns the route dict of
+    Engine.merge_route plus the per-owner byte splits of both buffers."""
+    out = eng.merge_route(files, world, io_type)
+    r = out["result"]
+    if r.bad_file >= 0:
+        raise N.LdbError(f"replay of file {files[r.bad_file][1]} failed: {N.status_str(r.status)}")
+    out["rec_splits"] = [int(c) * ROUTE_REC_BYTES for c in out["counts"]]
+    out["key_splits"] = [int(k) for k in out["key_bytes"]]
+    return out
+
+
+def owner_inputs(t, recv_recs, recv_keys, src_counts):
+    """Owner side of the exchange: the route records and key blobs received from every source rank
+    (rank order) joined into one array each; key offsets rebased into the joined blob; the global order
+    ord = source rank << 32 | seq."""
+    recs = t.cat(recv_recs) if recv_recs else None
+    keys = t.cat(recv_keys) if recv_keys else None
+    n = int(recs.numel()) // ROUTE_REC_BYTES if recs is not None else 0
+    if n == 0:
+        dev = recv_recs[0].device
+        return t.zeros(0, dtype=t.uint8, device=dev), t.zeros(16, dtype=t.uint8, device=dev), \
+            t.zeros(0, dtype=t.int64, device=dev)
+    q = recs.view(t.int64).view(n, 3).clone()
+    kb = t.tensor([0] + [int(k.numel()) for k in recv_keys[:-1]], dtype=t.int64, device=recs.device).cumsum(0)
+    src = t.repeat_interleave(t.arange(len(src_counts), device=recs.device),
+                              t.tensor(src_counts, dtype=t.int64, device=recs.device))
+    q[:, 2] += kb[src]
+    ord_ = (src.to(t.int64) << 32) | (q[:, 1] & 0xFFFFFFFF)
+    return q.view(t.uint8).view(-1), keys, ord_
+
+
+def last_by_seq(t, route, flags_from_owner, n_records: int):
+    """Sender side of the return exchange: the owners' flags (owner order, each in the order the
+    records were sent) scattered back to replay order."""
+    dev = route["recs"].device
+    last = t.zeros(max(n_records, 1), dtype=t.uint8, device=dev)
+    n = int(route["recs"].numel()) // ROUTE_REC_BYTES
+    if n:
+        seq = route["recs"].view(t.int64).view(n, 3)[:, 1] & 0xFFFFFFFF
+        last[seq] = t.cat(flags_from_owner)
+    return last[:n_records]
+
+
+def apply_phase(eng, files, last, active_fid: int, active_off: int, max_file_size: int, now: int,
+                io_type: int = N.FILEIO):
+    """Phase H3 on one rank: its own merge with the owners' liveness. Same output as rank_merge."""
+    out = eng.merge_dev(files, active_fid, active_off, max_file_size, now, io_type=io_type, fetch_pos=False,
+                        last=last)
+    r = out["result"]
+    if r.bad_file >= 0:
+        raise N.LdbError(f"merge input {r.bad_file} failed: {N.status_str(r.status)}")
+    return {"result": r, "stream": out["stream"], "pos": out["pos"], "n_emit": r.n_emit,
+            "live": out["live"][: r.n_records], "stats": out["stats"][: len(files)]}
+
+
+def hashed_sim(engs, blocks, active_fid: int, active_off: int, max_file_size: int, now: int,
+               io_type: int = N.FILEIO, timer=None):
+    """Every rank of the hash-partitioned merge in one process (tests, bench --xsim): engs[r] plays
+    rank r (its own context), blocks[r] its files. The exchanges are slices. `timer(rank, phase, fn)`
+    may wrap each rank's device phases. Returns the per-rank parts and places as merge_distributed."""
+    t = engs[0].torch
+    world = len(blocks)
+    tm = timer or (lambda r, ph, fn: fn())
+    routes = [tm(r, "route", lambda r=r: route_phase(engs[r], blocks[r], world, io_type)) for r in range(world)]
+    flags = [[None] * world for _ in range(world)]   # flags[src][owner]
+    for o in range(world):
+        rr, kk, cnt = [], [], []
+        for src in range(world):
+            ro = routes[src]
+            a = sum(ro["rec_splits"][:o])
+            rr.append(ro["recs"][a: a + ro["rec_splits"][o]])
+            ka = sum(ro["key_splits"][:o])
+            kk.append(ro["keys"][ka: ka + ro["key_splits"][o]])
+            cnt.append(int(ro["counts"][o]))
+        recs, keys, ord_ = owner_inputs(t, rr, kk, cnt)
+        last = tm(o, "resolve", lambda o=o, recs=recs, keys=keys, ord_=ord_: engs[o].merge_resolve(recs, keys, ord_))
+        b = 0
+        for src in range(world):
+            flags[src][o] = last[b: b + cnt[src]]
+            b += cnt[src]
+    parts = []
+    for r in range(world):
+        lr = last_by_seq(t, routes[r], flags[r], int(routes[r]["result"].n_records))
+        parts.append(tm(r, "apply", lambda r=r, lr=lr: apply_phase(engs[r], blocks[r], lr, active_fid, active_off,
+                                                                    max_file_size, now, io_type)))
+    sizes = [entry_sizes(engs[r], p) for r, p in enumerate(parts)]
+    places = [tm(r, "place", lambda r=r: rank_place(engs[r], parts[r], t.cat(sizes[:r]) if r else None, active_fid,
+                                                    active_off, max_file_size)) for r in range(world)]
+    return parts, places
+
+
 # ---------------------------------------------------------------------------------- distributed
 def _all_gather_varlen(x, dist):
     """All-gather 1-D tensors of different lengths (rank order). RCCL moves device tensors; gloo
@@ -192,6 +295,68 @@ def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int
         allsum = _all_gather_varlen(summ, dist)
     part = rank_merge(eng, files, allsum[rank + 1:], summary_fid_base(max_fid) + rank + 1, active_fid, active_off,
                       max_file_size, now, io_type)
+    sizes = _all_gather_varlen(entry_sizes(eng, part), dist) if world > 1 else []
+    earlier = torch.cat(sizes[:rank]) if rank else None
+    pl = rank_place(eng, part, earlier, active_fid, active_off, max_file_size, fetch_pos)
+    pl.update(stream=part["stream"], live=part["live"], stats=part["stats"], n_emit=part["n_emit"])
+    return pl
+
+
+def _all_to_all_varlen(chunks, dist):
+    """chunks[o] (1-D uint8 device tensors) to rank o; returns what every rank sent here, rank order.
+    RCCL: all_to_all_single with the splits; gloo (CPU tests): an all-gather of everything, host copies."""
+    import torch
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    dev = chunks[0].device
+    sizes = torch.tensor([int(c.numel()) for c in chunks], dtype=torch.int64)
+    if dist.get_backend() == "gloo":
+        flat = torch.cat(chunks).cpu() if chunks else torch.zeros(0, dtype=torch.uint8)
+        allsz = [torch.zeros_like(sizes) for _ in range(world)]
+        dist.all_gather(allsz, sizes)
+        got = _all_gather_varlen(flat, dist)
+        out = []
+        for src in range(world):
+            off = int(allsz[src][:rank].sum())
+            out.append(got[src][off: off + int(allsz[src][rank])].to(dev))
+        return out
+    sizes_d = sizes.to(dev)
+    recv_sz = torch.empty_like(sizes_d)
+    dist.all_to_all_single(recv_sz, sizes_d)
+    recv_sz = [int(x) for x in recv_sz.cpu()]
+    send = torch.cat(chunks) if chunks else torch.zeros(0, dtype=torch.uint8, device=dev)
+    recv = torch.empty(sum(recv_sz), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(recv, send, output_split_sizes=recv_sz, input_split_sizes=[int(x) for x in sizes])
+    out, b = [], 0
+    for n in recv_sz:
+        out.append(recv[b: b + n])
+        b += n
+    return out
+
+
+def merge_hashed_distributed(eng, files, active_fid: int, active_off: int, max_file_size: int, now: int,
+                             io_type: int = N.FILEIO, fetch_pos: bool = True):
+    """The hash-partitioned cross-GPU merge over torch.distributed: route, one
+    all-to-all of route records and keys, resolve at the owners, one all-to-all of flags back, apply,
+    then the rollover chain as merge_distributed. Same return value."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(), dist.get_world_size()
+    ro = route_phase(eng, files, world, io_type)
+    rc = [ro["recs"][sum(ro["rec_splits"][:o]): sum(ro["rec_splits"][:o + 1])] for o in range(world)]
+    kc = [ro["keys"][sum(ro["key_splits"][:o]): sum(ro["key_splits"][:o + 1])] for o in range(world)]
+    got_r = _all_to_all_varlen(rc, dist)
+    got_k = _all_to_all_varlen(kc, dist)
+    recs, keys, ord_ = owner_inputs(torch, got_r, got_k, [int(x.numel()) // ROUTE_REC_BYTES for x in got_r])
+    last = eng.merge_resolve(recs, keys, ord_)
+    back, b = [], 0
+    for x in got_r:
+        n = int(x.numel()) // ROUTE_REC_BYTES
+        back.append(last[b: b + n])
+        b += n
+    mine = _all_to_all_varlen(back, dist)
+    lr = last_by_seq(torch, ro, mine, int(ro["result"].n_records))
+    part = apply_phase(eng, files, lr, active_fid, active_off, max_file_size, now, io_type)
     sizes = _all_gather_varlen(entry_sizes(eng, part), dist) if world > 1 else []
     earlier = torch.cat(sizes[:rank]) if rank else None
     pl = rank_place(eng, part, earlier, active_fid, active_off, max_file_size, fetch_pos)

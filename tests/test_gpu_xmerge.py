@@ -69,17 +69,38 @@ def join(blocks, parts, places):
     return stream, pos, segs, live, stats
 
 
-def check(eng, files, kw, world):
+def run_ranks_hashed(engs, dfiles, world, kw):
+    """The hash-partitioned merge (xmerge.hashed_sim): route, resolve at the key owners, apply."""
+    from lazydb_amd import xmerge as X
+    blocks = blocks_of(len(dfiles), world)
+    own = [[dfiles[i] for i in b] for b in blocks]
+    parts, places = X.hashed_sim(engs[:world], own, kw["active_fid"], kw["active_off"], kw["max_file_size"],
+                                 kw["now"], kw.get("io_type", 0))
+    return blocks, parts, places
+
+
+@pytest.fixture(scope="module")
+def engs():
+    from lazydb_amd import Engine
+    es = [Engine(0) for _ in range(8)]
+    yield es
+    for e in es:
+        e.close()
+
+
+def check(eng, files, kw, world, hashed_engs=None):
     io = kw.get("io_type", 0)
     ref, stream, pos, segs, live, stats = coracle.merge(files, kw["active_fid"], kw["active_off"],
                                                         kw["max_file_size"], kw["now"], io)
     dfiles = [(to_dev(f[0]), f[1], f[2]) for f in files]
+    run = (lambda: run_ranks_hashed(hashed_engs, dfiles, world, kw)) if hashed_engs else \
+        (lambda: run_ranks(eng, dfiles, world, kw))
     if ref.status != 0:   # a file's replay fails (index.go:90 Fatalf): the rank holding it reports it
         from lazydb_amd import _native as N
         with pytest.raises(N.LdbError):
-            run_ranks(eng, dfiles, world, kw)
+            run()
         return ref
-    blocks, parts, places = run_ranks(eng, dfiles, world, kw)
+    blocks, parts, places = run()
     g_stream, g_pos, g_segs, g_live, g_stats = join(blocks, parts, places)
     assert places[-1]["end"] == (ref.end_fid, ref.end_off)
     for r in range(1, world):
@@ -117,4 +138,30 @@ def test_xmerge_config5_8_ranks(eng):
     imgs, n, ends = coracle.gen_merge(16, 256 << 20, 16 * 808_540, 3, ksize=64, vsize=256)
     files = [(imgs[i], i + 1, i < 15) for i in range(16)]
     ref = check(eng, files, dict(active_fid=16, active_off=ends[15], max_file_size=256 << 20, now=MC.NOW), 8)
+    assert ref.n_live == n // 2
+
+
+# ---- the hash-partitioned form: ldb_merge_route_dev / resolve / apply
+
+
+@pytest.mark.parametrize("name", sorted(MC.small_cases()))
+def test_xmerge_hashed_small_cases(eng, engs, name):
+    files, kw = MC.small_cases()[name]
+    for world in sorted({1, 2, min(len(files), 8)}):
+        check(eng, files, kw, world, hashed_engs=engs)
+
+
+@pytest.mark.parametrize("seed,world", [(21, 2), (22, 3), (23, 5), (24, 8)])
+def test_xmerge_hashed_medium_mixed(eng, engs, seed, world):
+    files, kw = MC.case_generated(seed, n_files=8, cap=16 << 20, n_records=8 * 50_000, max_file_size=8 << 20,
+                                  p_delete=20_000, p_expire=50_000, ksize=64, vsize=256)
+    ref = check(eng, files, kw, world, hashed_engs=engs)
+    assert ref.n_emit > 50_000
+
+
+def test_xmerge_hashed_config5_8_ranks(eng, engs):
+    imgs, n, ends = coracle.gen_merge(16, 256 << 20, 16 * 808_540, 3, ksize=64, vsize=256)
+    files = [(imgs[i], i + 1, i < 15) for i in range(16)]
+    ref = check(eng, files, dict(active_fid=16, active_off=ends[15], max_file_size=256 << 20, now=MC.NOW), 8,
+                hashed_engs=engs)
     assert ref.n_live == n // 2

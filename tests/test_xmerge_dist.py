@@ -58,11 +58,43 @@ def test_all_gather_varlen_gloo(world):
         assert gb == [[-r - 7] * (r + 1) for r in range(world)]
 
 
+def _a2a_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        from lazydb_amd.xmerge import _all_to_all_varlen
+        # rank r sends (r + 1) * o + 1 bytes of value 10 r + o to rank o (rank 0 sends nothing to rank 0)
+        chunks = [torch.full(((rank + 1) * o + (0 if rank == 0 and o == 0 else 1),), 10 * rank + o, dtype=torch.uint8)
+                  for o in range(world)]
+        got = _all_to_all_varlen(chunks, dist)
+        q.put((rank, [x.tolist() for x in got]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_to_all_varlen_gloo(world):
+    """The hash-partitioned merge's exchange (xmerge._all_to_all_varlen) on the gloo path."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_a2a_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, rows in got:
+        for src, row in enumerate(rows):
+            n = (src + 1) * rank + (0 if src == 0 and rank == 0 else 1)
+            assert row == [10 * src + rank] * n
+
+
 CASE = dict(seed=11, n_files=4, cap=32 << 20, n_records=4 * 101_000, max_file_size=8 << 20,
             p_delete=20_000, p_expire=50_000, ksize=64, vsize=256)
 
 
-def _merge_worker(rank, world, port, q):
+def _merge_worker(rank, world, port, q, hashed=False):
     _init(rank, world, port)
     try:
         from lazydb_amd import Engine
@@ -73,8 +105,12 @@ def _merge_worker(rank, world, port, q):
         eng = Engine(0)
         mine = [(torch.from_numpy(np.ascontiguousarray(files[i][0])).to("cuda:0"), files[i][1], files[i][2])
                 for i in blk]
-        out = X.merge_distributed(eng, mine, max(f[1] for f in files), kw["active_fid"], kw["active_off"],
-                                  kw["max_file_size"], kw["now"])
+        if hashed:
+            out = X.merge_hashed_distributed(eng, mine, kw["active_fid"], kw["active_off"], kw["max_file_size"],
+                                             kw["now"])
+        else:
+            out = X.merge_distributed(eng, mine, max(f[1] for f in files), kw["active_fid"], kw["active_off"],
+                                      kw["max_file_size"], kw["now"])
         q.put((rank, int(blk[0]), out["stream"].cpu().numpy().tobytes(), out["pos"].tobytes(),
                out["segments"].tobytes(), out["live"].cpu().numpy().tobytes(), out["start"], out["end"]))
         eng.close()
@@ -83,14 +119,17 @@ def _merge_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_merge_distributed_two_ranks():
+@pytest.mark.parametrize("hashed", [False, True])
+def test_merge_distributed_two_ranks(hashed):
+    """Summary exchange (hashed=False) and hash-partitioned liveness (hashed=True: route records and
+    keys to the key owners, flags back, two all-to-alls) over two real ranks."""
     from oracle import coracle
     from tests import merge_cases as MC
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_merge_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_merge_worker, args=(r, world, port, q, hashed)) for r in range(world)]
     for p in ps:
         p.start()
     got = sorted([q.get(timeout=240) for _ in range(world)])
