@@ -433,7 +433,7 @@ def main_xmerge(args):
         for step in range(args.warmup + args.steps):
             cur["on"] = step >= args.warmup
             parts, places = X.hashed_sim(engs, own, kw["active_fid"], kw["active_off"], kw["max_file_size"],
-                                         kw["now"], timer=timer)
+                                         kw["now"], timer=timer, fetch_pos=False)
         ph /= args.steps
         verified = None
         if ref is not None:

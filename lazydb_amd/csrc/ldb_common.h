@@ -192,6 +192,41 @@ LDB_HD uint32_t x8n_modp(uint64_t n) {
 }
 
 // Byte-at-a-time register step (8-bit table T0).
+// ---------------------------------------------------------------- key hash (merge liveness)
+// 64-bit hash of a record's key bytes: the merge's table (ldb_merge.hip k_insert / k_route_*) and the
+// scan's optional hash output (k_uniform, merge mode) must agree bit for bit, so both use this.
+// word16(i) = the 16 key bytes from key offset i as two little-endian u64 (bytes past n: any value,
+// they are masked), n = key length.
+LDB_HD uint64_t key_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+template <class Word16>
+LDB_HD uint64_t key_hash_w(Word16 word16, uint32_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xFF51AFD7ED558CCDull);
+  uint32_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    uint64_t w[2];
+    word16(i, w);
+    h = key_mix64(h ^ w[0]) + 0x632BE59BD9B4E019ull;
+    h = key_mix64(h ^ w[1]) + 0x632BE59BD9B4E019ull;
+  }
+  uint64_t t = 0;
+  if (i < n) {
+    uint64_t w[2];
+    word16(i, w);
+    if (i + 8 <= n) {
+      h = key_mix64(h ^ w[0]) + 0x632BE59BD9B4E019ull;
+      i += 8;
+      w[0] = w[1];
+    }
+    const uint32_t r = n - i;   // 0..7 tail bytes
+    t = r ? (w[0] & (~0ull >> (64 - 8 * r))) : 0;
+  }
+  return key_mix64(h ^ t ^ ((uint64_t)(n & 7) << 59));
+}
+
 LDB_HD uint32_t crc_byte(const uint32_t* t0, uint32_t reg, uint32_t byte) {
   return t0[(reg ^ byte) & 0xFFu] ^ (reg >> 8);
 }

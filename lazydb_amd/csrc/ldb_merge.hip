@@ -39,6 +39,10 @@
 #include "ldb_common.h"
 
 __attribute__((visibility("hidden"))) int ldb_ctx_device_(ldb_ctx* c);
+extern "C" __attribute__((visibility("hidden"))) int ldb_scan_file_dev_hashed(ldb_ctx* c, const uint8_t* d_image, uint64_t len,
+                                                                   uint32_t fid, int io_type, void* d_out,
+                                                                   uint64_t cap, ldb_scan_result* d_result,
+                                                                   void* stream, uint64_t* d_hash);
 __attribute__((visibility("hidden"))) void** ldb_ctx_merge_slot_(ldb_ctx* c);
 
 namespace {
@@ -55,6 +59,8 @@ struct FileDesc {       // one input file, in device memory
   uint64_t seq_base;    // first record index of the file; desc[n_files].seq_base = total records
   uint32_t is_target;
   uint32_t fid;
+  const uint64_t* hashes;   // key hashes of the file's first n_hashed records (the scan's run prefix)
+  uint64_t n_hashed;
 };
 
 struct Tail {           // k_pack output
@@ -66,6 +72,7 @@ struct Tail {           // k_pack output
 struct MergeWs {
   int device = 0;
   ldb_index_tuple* recs = nullptr;   // replayed records: one slot per file (or dense, after a capacity miss)
+  uint64_t* hashes = nullptr;        // key hashes, same slots as recs (the scans' run prefixes fill them)
   uint64_t rec_cap = 0;
   uint8_t* seqbuf = nullptr;     // per-record arrays + hash table + scan sums
   uint64_t seqbuf_bytes = 0;
@@ -99,25 +106,20 @@ __device__ __forceinline__ uint64_t load8u(const uint8_t* p) {
   return v;
 }
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
+// ldb::key_hash_w over key bytes in memory: whole 16-B (unaligned) loads, the tail byte by byte (it
+// never reads past the key)
 __device__ uint64_t key_hash(const uint8_t* p, uint32_t n) {
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xFF51AFD7ED558CCDull);
-  uint32_t i = 0;
-  for (; i + 16 <= n; i += 16) {   // 16-B (unaligned) loads: half the memory instructions
-    uint64_t w[2];
-    __builtin_memcpy(w, p + i, 16);
-    h = mix64(h ^ w[0]) + 0x632BE59BD9B4E019ull;
-    h = mix64(h ^ w[1]) + 0x632BE59BD9B4E019ull;
-  }
-  for (; i + 8 <= n; i += 8) h = mix64(h ^ load8u(p + i)) + 0x632BE59BD9B4E019ull;
-  uint64_t t = 0;
-  for (uint32_t j = 0; i + j < n; ++j) t |= (uint64_t)p[i + j] << (8 * j);
-  return mix64(h ^ t ^ ((uint64_t)(n & 7) << 59));
+  return ldb::key_hash_w(
+      [&](uint32_t i, uint64_t* w) {
+        if (i + 16 <= n) {
+          __builtin_memcpy(w, p + i, 16);
+        } else {
+          uint8_t t[16] = {};
+          for (uint32_t j = 0; i + j < n; ++j) t[j] = p[i + j];
+          __builtin_memcpy(w, t, 16);
+        }
+      },
+      n);
 }
 
 __device__ bool key_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
@@ -219,6 +221,14 @@ __device__ __forceinline__ const uint8_t* key_of(const FileDesc* fd, uint32_t n_
   return fd[f].img + e.offset + e.hdr_size;
 }
 
+// the record's key hash: from the scan (its file's run prefix) or computed here from the key bytes
+__device__ __forceinline__ uint64_t record_hash(const FileDesc* fd, uint32_t n_files, uint64_t seq, const uint8_t* kp,
+                                                uint32_t kl) {
+  const uint32_t f = file_of(fd, n_files, seq);
+  const uint64_t i = seq - fd[f].seq_base;
+  return i < fd[f].n_hashed ? fd[f].hashes[i] : key_hash(kp, kl);
+}
+
 // A slot is one 64-bit word (hash tag << 32 | max record id + 1), claimed by CAS and then raised by a
 // 64-bit atomicMax: every record that reaches a slot has the slot's key (it claimed it, or compared its
 // key bytes equal with the slot's current record), so the tag half never changes and the low half ends
@@ -231,7 +241,7 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
   if (seq >= n) return;
   uint32_t kl;
   const uint8_t* kp = key_of(fd, n_files, seq, &kl);
-  const uint64_t h = key_hash(kp, kl);
+  const uint64_t h = record_hash(fd, n_files, seq, kp, kl);
   const unsigned long long mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
   uint64_t i = h & mask;
   for (;;) {
@@ -339,7 +349,7 @@ __global__ __launch_bounds__(256) void k_route_count(uint64_t n, const FileDesc*
   if (seq < n) {
     uint32_t kl;
     const uint8_t* kp = key_of(fd, n_files, seq, &kl);
-    const uint64_t h = key_hash(kp, kl);
+    const uint64_t h = record_hash(fd, n_files, seq, kp, kl);
     hsh[seq] = h;
     const uint32_t o = owner_of(h, n_own);
     atomicAdd(&sc[o], 1ull);
@@ -928,14 +938,21 @@ int grow_recs(MergeWs* m, uint64_t need, uint64_t keep, hipStream_t s) {
   if (m->rec_cap >= need) return LDB_OK;
   uint64_t cap = std::max(need, m->rec_cap + m->rec_cap / 2);
   ldb_index_tuple* nr = nullptr;
+  uint64_t* nh = nullptr;
   if (hipMalloc(&nr, cap * sizeof(ldb_index_tuple)) != hipSuccess) return LDB_ERR_NOMEM;
+  if (hipMalloc(&nh, cap * sizeof(uint64_t)) != hipSuccess) {
+    (void)hipFree(nr);
+    return LDB_ERR_NOMEM;
+  }
   if (keep) MHIP(hipMemcpyAsync(nr, m->recs, keep * sizeof(ldb_index_tuple), hipMemcpyDeviceToDevice, s));
   MHIP(hipStreamSynchronize(s));
   if (m->recs) {   // and the aux stream's scans, which write into the record slots
     (void)hipDeviceSynchronize();
     (void)hipFree(m->recs);
+    (void)hipFree(m->hashes);
   }
   m->recs = nr;
+  m->hashes = nh;
   m->rec_cap = cap;
   return LDB_OK;
 }
@@ -963,6 +980,7 @@ __attribute__((visibility("hidden"))) void ldb_merge_release_(void* p) {
   MergeWs* m = static_cast<MergeWs*>(p);
   if (!m) return;
   if (m->recs) (void)hipFree(m->recs);
+  if (m->hashes) (void)hipFree(m->hashes);
   if (m->seqbuf) (void)hipFree(m->seqbuf);
   if (m->small) (void)hipFree(m->small);
   for (auto& e : m->ev)
@@ -1020,9 +1038,9 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
   }
   for (uint32_t i = 0; i < nf; ++i) {
     const bool odd = (i & 1) && nf > 1;
-    rc = ldb_scan_file_dev(odd ? m->aux : ctx, files[i].d_image, files[i].len, files[i].fid, io_type,
-                           LDB_TUPLE_INDEX, m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i,
-                           odd ? m->aux_s : s);
+    rc = ldb_scan_file_dev_hashed(odd ? m->aux : ctx, files[i].d_image, files[i].len, files[i].fid, io_type,
+                                  m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i, odd ? m->aux_s : s,
+                                  m->hashes + sbase[i]);
     if (rc != LDB_OK) {
       // scans already queued on either stream read the caller's images and write m->recs: drain
       // them before the caller can free or reuse anything
@@ -1056,8 +1074,12 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
         if (rc != LDB_OK) return rc;
       }
     }
+    // the run prefix's key hashes (slotted scans only; a dense rescan hashes in the merge kernels)
+    const uint64_t nh = slotted ? std::min<uint64_t>(rh[i].n_run, std::min<uint64_t>(rh[i].n_entries,
+                                                                                      sbase[i + 1] - sbase[i]))
+                                : 0;
     fdh[i] = FileDesc{files[i].d_image, slotted ? m->recs + sbase[i] : m->recs + base, base, files[i].is_target,
-                      files[i].fid};
+                      files[i].fid, slotted ? m->hashes + sbase[i] : nullptr, nh};
     if (h_stats) {
       h_stats[i] = ldb_merge_file_stat{rh[i].status, files[i].fid, rh[i].n_entries, rh[i].end_off, 0, 0};
     }
@@ -1070,7 +1092,7 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
     base += rh[i].n_entries;
   }
   n = base;
-  fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0};
+  fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0, nullptr, 0};
   h_result->n_records = n;
   if (n >= 0xFFFFFFFFull) return h_result->status = LDB_ERR_ARG;   // record ids are 32-bit
   m->cache_ok = true;

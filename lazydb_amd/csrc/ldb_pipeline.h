@@ -35,6 +35,7 @@ struct Pipe {
   uint64_t* dyn;              // [0] K: entries of the equal-sized run k_uniform verified, [1] their size,
                               // [2] kUniReady once a k_uniform launch published its setup to `uni`
   uint8_t* uni;               // the run prefix's published setup (memo, slicing, combine tables)
+  uint64_t* hash_out;         // merge mode (nullable): ldb::key_hash_w of the key of run entry k at [k]
   void* out;
   uint64_t cap;
   int kind;

@@ -401,7 +401,7 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 
 // One wave's share of the run prefix, S steps per lane (a compile-time count: the rows stay in
 // registers with static indices and the step loop has no per-step branch).
-template <int S, bool kChunk>
+template <int S, bool kChunk, bool kHash>
 __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint32_t* stab, int lane, int wave,
                                           uint64_t a_lo, uint64_t a_hi) {
   if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
@@ -500,6 +500,10 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     bool mine = x <= p.len;
     if (kChunk) {
       uint64_t lo_ = a_lo, hi_ = all_hi ? ~0ull : a_hi;   // opaque per batch: not held across the loop
+      lo_ = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_ >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)lo_);
+      hi_ = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(hi_ >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)hi_);
       asm volatile("" : "+s"(lo_), "+s"(hi_));
       mine = mine && (lo_ == 0 || x + need > lo_) && x + need <= hi_;
     }
@@ -542,13 +546,25 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
       } else {
         store_tuple(reinterpret_cast<ldb_index_tuple*>(p.out) + e, uni_pos(m, x), m.k, m.v);
       }
+      if (kHash) {   // merge mode: the key's hash, from the lines this wave just loaded
+        const uint32_t kx = hx + m.hs;
+        p.hash_out[e] = key_hash_w(
+            [&](uint32_t i, uint64_t* w) {
+              const uint32_t a0 = kx + i, al = a0 & ~3u, s0 = a0 & 3u;
+              const uint4 q = ld16(rs, al);
+              const uint32_t q4 = ld4(rs, al + 16);
+              w[0] = (uint64_t)funnel(q.y, q.x, s0) | ((uint64_t)funnel(q.z, q.y, s0) << 32);
+              w[1] = (uint64_t)funnel(q.w, q.z, s0) | ((uint64_t)funnel(q4, q.w, s0) << 32);
+            },
+            m.k);
+      }
     }
   }
 }
 
 // kChunk: a_lo, a_hi: image bytes [0, a_hi) are in place; candidates not already taken by a launch
 // with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
-template <bool kChunk>
+template <bool kChunk, bool kHash>
 __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_lo, uint64_t a_hi) {
   __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + kUniTabWords];   // S table, combine tables
   __shared__ UniSetup su;
@@ -562,7 +578,7 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n) case n: uni_waves<n, kChunk>(p, su, stab, lane, wave, a_lo, a_hi); break;
+#define LDB_UNI_CASE(n) case n: uni_waves<n, kChunk, kHash>(p, su, stab, lane, wave, a_lo, a_hi); break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
 #undef LDB_UNI_CASE
@@ -1236,6 +1252,7 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.blk = reinterpret_cast<uint64_t*>(w + L.o_blk);
   p.dyn = reinterpret_cast<uint64_t*>(w + L.o_dyn);
   p.uni = w + L.o_uni;
+  p.hash_out = nullptr;
   p.out = out;
   p.cap = cap;
   p.kind = kind;
@@ -1266,7 +1283,7 @@ struct ChunkPlan {
 // reads every byte once in 1 KiB pieces.
 int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, int io, int kind, void* d_out,
                  uint64_t cap, ldb_scan_result* d_res, hipStream_t s, bool serial, bool no_run = false,
-                 const ChunkPlan* plan = nullptr) {
+                 const ChunkPlan* plan = nullptr, uint64_t* hash_out = nullptr) {
   if (!c || !d_res || (io != LDB_IO_FILEIO && io != LDB_IO_MMAP) ||
       (kind != LDB_TUPLE_INDEX && kind != LDB_TUPLE_ENTRY) || (cap && !d_out))
     return LDB_ERR_ARG;
@@ -1276,7 +1293,8 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   const WsLayout L = layout(len);
   int rc = ensure_ws(c, L.total);
   if (rc != LDB_OK) return rc;
-  const Pipe p = make_pipe(c, L, d_img, len, fid, io, kind, d_out, cap, d_res);
+  Pipe p = make_pipe(c, L, d_img, len, fid, io, kind, d_out, cap, d_res);
+  p.hash_out = hash_out;
   // the workspace is free once the last pipeline enqueued on another stream has finished
   if (c->ws_ev_live && c->ws_stream != s) LDB_HIP(hipStreamWaitEvent(s, c->ws_ev, 0));
   // every pipeline starts from zeroed control words, in stream order: nothing depends on how the
@@ -1317,9 +1335,11 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
       const uint64_t batches = (hi - lo) / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
       const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2);
       if (chunked)
-        hipLaunchKernelGGL(k_uniform<true>, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+        hipLaunchKernelGGL((k_uniform<true, false>), dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+      else if (p.hash_out)
+        hipLaunchKernelGGL((k_uniform<false, true>), dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
       else
-        hipLaunchKernelGGL(k_uniform<false>, dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+        hipLaunchKernelGGL((k_uniform<false, false>), dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
     };
     if (chunked) {
       uint64_t lo = 0;
@@ -1358,6 +1378,18 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
 extern "C" {
 
 int ldb_abi_version(void) { return LDB_ABI_VERSION; }
+
+// internal (merge engine): ldb_scan_file_dev that also writes the key hash of every run-prefix entry
+// k < min(n_run, cap) to d_hash[k] (ldb::key_hash_w, the merge table's hash)
+__attribute__((visibility("hidden"))) int ldb_scan_file_dev_hashed(ldb_ctx* c, const uint8_t* d_image, uint64_t len,
+                                                                   uint32_t fid, int io_type, void* d_out,
+                                                                   uint64_t cap, ldb_scan_result* d_result,
+                                                                   void* stream, uint64_t* d_hash) {
+  if (!c) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  return enqueue_scan(c, d_image, len, fid, io_type, LDB_TUPLE_INDEX, d_out, cap, d_result, (hipStream_t)stream,
+                      false, false, nullptr, d_hash);
+}
 
 const char* ldb_status_str(int s) {
   switch (s) {

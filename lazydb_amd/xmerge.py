@@ -223,7 +223,7 @@ def apply_phase(eng, files, last, active_fid: int, active_off: int, max_file_siz
 
 
 def hashed_sim(engs, blocks, active_fid: int, active_off: int, max_file_size: int, now: int,
-               io_type: int = N.FILEIO, timer=None):
+               io_type: int = N.FILEIO, timer=None, fetch_pos: bool = True):
     """Every rank of the hash-partitioned merge in one process (tests, bench --xsim): engs[r] plays
     rank r (its own context), blocks[r] its files. The exchanges are slices. `timer(rank, phase, fn)`
     may wrap each rank's device phases. Returns the per-rank parts and places as merge_distributed."""
@@ -254,7 +254,7 @@ def hashed_sim(engs, blocks, active_fid: int, active_off: int, max_file_size: in
                                                                     max_file_size, now, io_type)))
     sizes = [entry_sizes(engs[r], p) for r, p in enumerate(parts)]
     places = [tm(r, "place", lambda r=r: rank_place(engs[r], parts[r], t.cat(sizes[:r]) if r else None, active_fid,
-                                                    active_off, max_file_size)) for r in range(world)]
+                                                    active_off, max_file_size, fetch_pos)) for r in range(world)]
     return parts, places
 
 
