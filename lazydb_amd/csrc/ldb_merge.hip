@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -80,11 +81,14 @@ struct MergeWs {
   uint64_t small_bytes = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float t_scan = 0, t_live = 0, t_compact = 0;
-  // a second scan context on its own stream: files alternate between the two, so one file's small
-  // pipeline kernels (k_link .. k_compact) overlap the next file's k_scan_main
-  ldb_ctx* aux = nullptr;
-  hipStream_t aux_s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  // more scan contexts, each on its own stream: files are dealt round-robin over the caller's
+  // context and these (LDB_MERGE_SCAN_LANES, default 4), so one file's small pipeline kernels
+  // (k_link .. k_compact, launch-bound) overlap the other files' scans
+  static constexpr int kMaxAux = 7;
+  int n_aux = 0;
+  ldb_ctx* aux[kMaxAux] = {};
+  hipStream_t aux_s[kMaxAux] = {};
+  hipEvent_t fork = nullptr, join[kMaxAux] = {};
   // the last replay scan (ldb_merge_route_dev), reused by ldb_merge_apply_dev on the same files
   bool cache_ok = false;
   int cache_io = 0;
@@ -736,10 +740,14 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
     const uint32_t len = (head && j == 0) ? head : min(16u, nbr - at);
     const uint8_t* s = s_src[w][lo] + at;
     uint8_t* d = d0 + at;
-    if (len == 16) {   // d is 16-B aligned here
+    if (len == 16) {   // d is 16-B aligned here; both sides are touched once: global, non-temporal
+      typedef unsigned int v4g __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(1))) const uint8_t* gsrc_t;
+      typedef __attribute__((address_space(1))) v4g* gdst_t;
       uint4 v;
-      __builtin_memcpy(&v, s, 16);
-      *reinterpret_cast<uint4*>(d) = v;
+      __builtin_memcpy(&v, (gsrc_t)s, 16);
+      const v4g x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, (gdst_t)d);
     } else {
       uint32_t b = 0;
       if (len & 8) {
@@ -985,10 +993,12 @@ __attribute__((visibility("hidden"))) void ldb_merge_release_(void* p) {
   if (m->small) (void)hipFree(m->small);
   for (auto& e : m->ev)
     if (e) (void)hipEventDestroy(e);
-  if (m->aux) (void)ldb_ctx_destroy(m->aux);
-  if (m->aux_s) (void)hipStreamDestroy(m->aux_s);
+  for (int i = 0; i < m->n_aux; ++i) {
+    if (m->aux[i]) (void)ldb_ctx_destroy(m->aux[i]);
+    if (m->aux_s[i]) (void)hipStreamDestroy(m->aux_s[i]);
+    if (m->join[i]) (void)hipEventDestroy(m->join[i]);
+  }
   if (m->fork) (void)hipEventDestroy(m->fork);
-  if (m->join) (void)hipEventDestroy(m->join);
   delete m;
 }
 
@@ -1026,32 +1036,39 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
   for (uint32_t i = 0; i < nf; ++i) sbase[i + 1] = sbase[i] + files[i].len / 64 + 1024;
   rc = grow_recs(m, std::max<uint64_t>(sbase[nf], 4096), 0, s);
   if (rc != LDB_OK) return rc;
-  if (nf > 1 && !m->aux) {
-    if (ldb_ctx_create(m->device, &m->aux) != LDB_OK) return LDB_ERR_HIP;
-    MHIP(hipStreamCreateWithFlags(&m->aux_s, hipStreamNonBlocking));
+  if (!m->fork) {
+    const char* e = getenv("LDB_MERGE_SCAN_LANES");
+    const int want = std::min(std::max(e ? atoi(e) : 4, 1), MergeWs::kMaxAux + 1) - 1;
     MHIP(hipEventCreateWithFlags(&m->fork, hipEventDisableTiming));
-    MHIP(hipEventCreateWithFlags(&m->join, hipEventDisableTiming));
+    for (int i = 0; i < want; ++i) {
+      if (ldb_ctx_create(m->device, &m->aux[i]) != LDB_OK) return LDB_ERR_HIP;
+      MHIP(hipStreamCreateWithFlags(&m->aux_s[i], hipStreamNonBlocking));
+      MHIP(hipEventCreateWithFlags(&m->join[i], hipEventDisableTiming));
+      m->n_aux = i + 1;
+    }
   }
-  if (nf > 1) {
+  const int lanes = std::min<int>(1 + m->n_aux, (int)nf);   // the caller's context is lane 0
+  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") == nullptr || atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
+  if (lanes > 1) {
     MHIP(hipEventRecord(m->fork, s));
-    MHIP(hipStreamWaitEvent(m->aux_s, m->fork, 0));
+    for (int a = 0; a + 1 < lanes; ++a) MHIP(hipStreamWaitEvent(m->aux_s[a], m->fork, 0));
   }
   for (uint32_t i = 0; i < nf; ++i) {
-    const bool odd = (i & 1) && nf > 1;
-    rc = ldb_scan_file_dev_hashed(odd ? m->aux : ctx, files[i].d_image, files[i].len, files[i].fid, io_type,
-                                  m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i, odd ? m->aux_s : s,
-                                  m->hashes + sbase[i]);
+    const int lane = (int)(i % (uint32_t)lanes);
+    rc = ldb_scan_file_dev_hashed(lane ? m->aux[lane - 1] : ctx, files[i].d_image, files[i].len, files[i].fid,
+                                  io_type, m->recs + sbase[i], sbase[i + 1] - sbase[i], d_res + i,
+                                  lane ? m->aux_s[lane - 1] : s, scan_hash ? m->hashes + sbase[i] : nullptr);
     if (rc != LDB_OK) {
-      // scans already queued on either stream read the caller's images and write m->recs: drain
+      // scans already queued on any stream read the caller's images and write m->recs: drain
       // them before the caller can free or reuse anything
-      if (nf > 1) (void)hipStreamSynchronize(m->aux_s);
+      for (int a = 0; a + 1 < lanes; ++a) (void)hipStreamSynchronize(m->aux_s[a]);
       (void)hipStreamSynchronize(s);
       return rc;
     }
   }
-  if (nf > 1) {
-    MHIP(hipEventRecord(m->join, m->aux_s));
-    MHIP(hipStreamWaitEvent(s, m->join, 0));
+  for (int a = 0; a + 1 < lanes; ++a) {
+    MHIP(hipEventRecord(m->join[a], m->aux_s[a]));
+    MHIP(hipStreamWaitEvent(s, m->join[a], 0));
   }
   if (nf) MHIP(hipMemcpyAsync(rh.data(), d_res, sizeof(ldb_scan_result) * nf, hipMemcpyDeviceToHost, s));
   MHIP(hipStreamSynchronize(s));
@@ -1075,7 +1092,7 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
       }
     }
     // the run prefix's key hashes (slotted scans only; a dense rescan hashes in the merge kernels)
-    const uint64_t nh = slotted ? std::min<uint64_t>(rh[i].n_run, std::min<uint64_t>(rh[i].n_entries,
+    const uint64_t nh = slotted && scan_hash ? std::min<uint64_t>(rh[i].n_run, std::min<uint64_t>(rh[i].n_entries,
                                                                                       sbase[i + 1] - sbase[i]))
                                 : 0;
     fdh[i] = FileDesc{files[i].d_image, slotted ? m->recs + sbase[i] : m->recs + base, base, files[i].is_target,
