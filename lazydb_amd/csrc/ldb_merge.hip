@@ -1048,7 +1048,10 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
     }
   }
   const int lanes = std::min<int>(1 + m->n_aux, (int)nf);   // the caller's context is lane 0
-  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") == nullptr || atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
+  // LDB_MERGE_SCAN_HASH=1: the scans' run prefixes also emit the key hashes k_insert / k_route_count
+  // then skip. Off by default: measured even (config 5: 4.894 ms with, 4.864 without,
+  // gpurun_out/r2_merge_H*.json) -- the key bytes are read once either way, in the scan or in k_insert.
+  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") != nullptr && atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
   if (lanes > 1) {
     MHIP(hipEventRecord(m->fork, s));
     for (int a = 0; a + 1 < lanes; ++a) MHIP(hipStreamWaitEvent(m->aux_s[a], m->fork, 0));
