@@ -23,7 +23,7 @@
 //   k_live          per record: live = (slot max == seq) && !SDelete; emit flag, sizes; per-block partials
 //   k_file_stats    per file: live counts and bytes
 //   k_scan_*        exclusive prefix sums of emitted bytes and counts (3-kernel reduce-then-scan)
-//   k_pack          one lane: greedy rollover packing by binary search over the byte prefix
+//   k_pack          one wave: greedy rollover packing by 64-ary search over the byte prefix
 //   k_emit_copy     one wave per 64 records: new ValuePos, unaligned 16-B copies of the emitted bytes,
 //                   re-encoded header + CRC-32 for the (rare) non-canonical records
 // and the batch writeLogEntry of a transaction commit (ldb_encode_entries_dev: k_enc_size, the same
@@ -40,6 +40,9 @@
 #include "ldb_common.h"
 
 __attribute__((visibility("hidden"))) int ldb_ctx_device_(ldb_ctx* c);
+extern "C" __attribute__((visibility("hidden"))) int ldb_scan_files_dev_batched(
+    ldb_ctx* c, int n_files, const uint8_t* const* d_images, const uint64_t* lens, const uint32_t* fids, int io_type,
+    void* const* d_outs, const uint64_t* caps, ldb_scan_result* d_results, void* stream, uint64_t* const* d_hash);
 extern "C" __attribute__((visibility("hidden"))) int ldb_scan_file_dev_hashed(ldb_ctx* c, const uint8_t* d_image, uint64_t len,
                                                                    uint32_t fid, int io_type, void* d_out,
                                                                    uint64_t cap, ldb_scan_result* d_result,
@@ -68,6 +71,9 @@ struct Tail {           // k_pack output
   uint32_t end_fid;
   uint32_t n_segments;
   uint64_t end_off;
+  uint64_t tot_b;        // emitted bytes P[n] and records C[n] (C may be null: tot_c = 0)
+  uint32_t tot_c;
+  uint32_t pad_;
 };
 
 struct MergeWs {
@@ -237,23 +243,38 @@ __device__ __forceinline__ uint64_t record_hash(const FileDesc* fd, uint32_t n_f
 // 64-bit atomicMax: every record that reaches a slot has the slot's key (it claimed it, or compared its
 // key bytes equal with the slot's current record), so the tag half never changes and the low half ends
 // as the key's last record. 8-B slots keep the table within the Infinity Cache at config-5 sizes.
+// kCasFirst: claim by CAS straight away (the CAS returns the slot's word when it is taken) instead
+// of a load first. The slot id goes to slot[seq] with bit 31 = "expired" (db.go:255, ExpiredAt <=
+// now): the header sits next to the key this kernel reads, so k_live needs no image access for it.
+template <bool kCasFirst>
 __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
-                                                unsigned long long* tab, uint64_t mask, uint32_t* __restrict__ slot) {
+                                                unsigned long long* tab, uint64_t mask, uint32_t* __restrict__ slot,
+                                                int64_t now) {
   __shared__ FileDesc s_fd[kFdLds];
   const FileDesc* fd = stage_fd(gfd, n_files, s_fd);
   uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (seq >= n) return;
-  uint32_t kl;
-  const uint8_t* kp = key_of(fd, n_files, seq, &kl);
+  const uint32_t f = file_of(fd, n_files, seq);
+  const Rec e = rec_of(fd, f, seq);
+  const uint32_t kl = e.k_size;
+  const uint8_t* kp = fd[f].img + e.offset + e.hdr_size;
+  const int64_t ea = expired_at_of(fd[f].img, e.offset);
+  const bool expired = ea != 0 && ea <= now;
   const uint64_t h = record_hash(fd, n_files, seq, kp, kl);
   const unsigned long long mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
   uint64_t i = h & mask;
   for (;;) {
-    unsigned long long v = __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (v == 0) {
-      const unsigned long long prev = atomicCAS(&tab[i], 0ull, mine);
-      if (prev == 0) break;
-      v = prev;
+    unsigned long long v;
+    if (kCasFirst) {
+      v = atomicCAS(&tab[i], 0ull, mine);
+      if (v == 0) break;
+    } else {
+      v = __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == 0) {
+        const unsigned long long prev = atomicCAS(&tab[i], 0ull, mine);
+        if (prev == 0) break;
+        v = prev;
+      }
     }
     if ((v >> 32) == (h >> 32)) {
       uint32_t rl;
@@ -265,7 +286,7 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
     }
     i = (i + 1) & mask;
   }
-  slot[seq] = (uint32_t)i;
+  slot[seq] = (uint32_t)i | (expired ? 0x80000000u : 0u);
 }
 
 // live = last record of its key and not an SDelete (index.go:16-25); emit = live && target file &&
@@ -290,13 +311,18 @@ __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __rest
   if (valid) {
     f = file_of(fd, n_files, seq);
     const Rec e = rec_of(fd, f, seq);
-    const bool lastw = last_in ? last_in[seq] != 0 : (uint32_t)tab[slot[seq]] == (uint32_t)(seq + 1);
+    const uint32_t sl = last_in ? 0u : slot[seq];   // k_insert's slot, bit 31 = expired
+    const bool lastw = last_in ? last_in[seq] != 0 : (uint32_t)tab[sl & 0x7FFFFFFFu] == (uint32_t)(seq + 1);
     live = lastw && e.stat != kSDelete;
     size = e.enc_hdr_size + e.k_size + e.v_size;
     bool emit = live && fd[f].is_target;
     if (emit) {
-      const int64_t ea = expired_at_of(fd[f].img, e.offset);
-      emit = !(ea != 0 && ea <= now);
+      if (last_in) {   // no k_insert ran (ldb_merge_apply_dev): the header from the image
+        const int64_t ea = expired_at_of(fd[f].img, e.offset);
+        emit = !(ea != 0 && ea <= now);
+      } else {
+        emit = !(sl >> 31);
+      }
     }
     esz[seq] = emit ? size : 0u;
     if (live_out) live_out[seq] = live ? 1 : 0;
@@ -526,12 +552,13 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint32_t* __re
                                                             uint64_t* __restrict__ bsum, uint32_t* __restrict__ bcnt) {
   __shared__ uint64_t sb[kScanBlock / 64];
   __shared__ uint32_t sc[kScanBlock / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  // the tile's totals only: coalesced loads, order does not matter
+  const uint64_t t0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
   uint64_t b = 0;
   uint32_t c = 0;
   for (int k = 0; k < kScanItems; ++k)
-    if (base + k < n) {
-      uint32_t s = esz[base + k];
+    if (t0 + (uint64_t)k * kScanBlock < n) {
+      const uint32_t s = esz[t0 + (uint64_t)k * kScanBlock];
       b += s;
       c += s ? 1u : 0u;
     }
@@ -577,12 +604,21 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_write(const uint32_t* __res
                                                            uint64_t* __restrict__ P, uint32_t* __restrict__ C) {
   __shared__ uint64_t sb[kScanBlock / 64];
   __shared__ uint32_t sc[kScanBlock / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  // the tile staged through LDS so that global loads and stores are coalesced; thread t scans the
+  // tile's items [t kScanItems, (t + 1) kScanItems)
+  __shared__ uint32_t s_e[kScanTile];   // sizes in, then the counts C out
+  __shared__ uint64_t s_p[kScanTile];   // byte offsets P out
+  const uint64_t t0 = (uint64_t)blockIdx.x * kScanTile;
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint32_t j = k * kScanBlock + threadIdx.x;
+    s_e[j] = t0 + j < n ? esz[t0 + j] : 0u;
+  }
+  __syncthreads();
   uint32_t s[kScanItems];
   uint64_t b = 0;
   uint32_t c = 0;
   for (int k = 0; k < kScanItems; ++k) {
-    s[k] = base + k < n ? esz[base + k] : 0u;
+    s[k] = s_e[threadIdx.x * kScanItems + k];
     b += s[k];
     c += s[k] ? 1u : 0u;
   }
@@ -591,21 +627,34 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_write(const uint32_t* __res
   block_exscan(b, c, sb, sc, tb, tc);
   b += bsum[blockIdx.x];
   c += bcnt[blockIdx.x];
-  for (int k = 0; k < kScanItems; ++k)
-    if (base + k < n) {
-      P[base + k] = b;
-      C[base + k] = c;
-      b += s[k];
-      c += s[k] ? 1u : 0u;
+  for (int k = 0; k < kScanItems; ++k) {   // each thread rewrites only the items it read
+    s_p[threadIdx.x * kScanItems + k] = b;
+    s_e[threadIdx.x * kScanItems + k] = c;
+    b += s[k];
+    c += s[k] ? 1u : 0u;
+  }
+  __syncthreads();
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint32_t j = k * kScanBlock + threadIdx.x;
+    if (t0 + j < n) {
+      P[t0 + j] = s_p[j];
+      C[t0 + j] = s_e[j];
     }
+  }
 }
 
 // ------------------------------------------------------------------------------ rollover packing
-__device__ uint64_t last_le(const uint64_t* P, uint64_t n, uint64_t x) {   // largest i in [0,n] with P[i] <= x
+// largest i in [0, n] with P[i] <= x (P non-decreasing, P[0] = 0): a 64-ary search, one probe per lane
+// per round (about 4 dependent rounds over 10^7 records instead of 24), wave-uniform result
+__device__ uint64_t last_le(const uint64_t* P, uint64_t n, uint64_t x, int lane) {
   uint64_t lo = 0, hi = n;
   while (lo < hi) {
-    uint64_t mid = (lo + hi + 1) >> 1;
-    if (P[mid] <= x) lo = mid; else hi = mid - 1;
+    const uint64_t step = (hi - lo + 62) / 63;   // lanes 0..63 probe lo .. lo + 63 step >= hi
+    const uint64_t idx = lo + (uint64_t)lane * step;
+    const uint64_t m = __ballot(idx <= hi && P[idx] <= x);   // a prefix of the lanes; lane 0 always
+    const uint64_t nlo = lo + (uint64_t)(63 - __builtin_clzll(m)) * step;
+    hi = min(hi, nlo + step - 1);
+    lo = nlo;
   }
   return lo;
 }
@@ -613,15 +662,17 @@ __device__ uint64_t last_le(const uint64_t* P, uint64_t n, uint64_t x) {   // la
 // writeLogEntry's greedy rollover (db.go:485-510) over the emitted records in stream order: a record
 // goes to the current file if Offset + size <= MaxLogFileSize, otherwise the file rolls over to fid+1
 // and the record is written there at 0 whatever its size. Runs of records that fit are found by binary
-// search over the byte prefix, so the loop runs once per output segment.
-__global__ void k_pack(const uint64_t* __restrict__ P, uint64_t n, uint32_t active_fid, uint64_t active_off,
-                       uint64_t max_size, ldb_merge_segment* segs, uint32_t seg_cap, Tail* tail) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// search over the byte prefix, so the loop runs once per output segment. One wave (the searches are
+// wave-wide; every lane holds the same state, lane 0 writes).
+__global__ __launch_bounds__(64) void k_pack(const uint64_t* __restrict__ P, const uint32_t* __restrict__ C, uint64_t n,
+                                             uint32_t active_fid, uint64_t active_off, uint64_t max_size,
+                                             ldb_merge_segment* segs, uint32_t seg_cap, Tail* tail) {
+  const int lane = threadIdx.x;
   const uint64_t total = P[n];
   uint32_t fid = active_fid, nseg = 0;
   uint64_t off = active_off, x = 0;
   while (x < total) {
-    const uint64_t r = last_le(P, n, x);        // the emitted record that starts at stream position x
+    const uint64_t r = last_le(P, n, x, lane);  // the emitted record that starts at stream position x
     const uint64_t size = P[r + 1] - P[r];
     ldb_merge_segment sg;
     sg.reserved_ = 0;
@@ -639,18 +690,25 @@ __global__ void k_pack(const uint64_t* __restrict__ P, uint64_t n, uint32_t acti
     }
     if (off < max_size) {                       // extend with every following record that fits
       const uint64_t lim = x + (max_size - off);
-      const uint64_t e = last_le(P, n, lim < total ? lim : total);
+      const uint64_t e = last_le(P, n, lim < total ? lim : total, lane);
       const uint64_t x2 = P[e] > x ? P[e] : x;
       off += x2 - x;
       x = x2;
     }
     sg.n_bytes = x - sg.stream_off;
-    if (nseg < seg_cap) segs[nseg] = sg;
+    if (nseg < seg_cap && lane == 0) segs[nseg] = sg;
     ++nseg;
   }
-  tail->end_fid = fid;
-  tail->end_off = off;
-  tail->n_segments = nseg;
+  if (lane == 0) {
+    Tail t;
+    t.end_fid = fid;
+    t.end_off = off;
+    t.n_segments = nseg;
+    t.tot_b = total;
+    t.tot_c = C ? C[n] : 0u;
+    t.pad_ = 0;
+    *tail = t;
+  }
 }
 
 // ------------------------------------------------------------------------------ emit + copy
@@ -670,10 +728,23 @@ constexpr int kCopyWaves = 4;
 // wave's pieces are dealt out over its lanes. Canonical records (hdr_size == enc_hdr_size) are copied
 // verbatim: EncodeEntry re-produces their bytes. A non-canonical record gets its key/value copied and
 // its header re-encoded by its lane, CRC-32 over the new header and the key/value (log_entry.go:48-78).
+// The capacities are checked here, against k_pack's tail, exactly as the host reports them
+// (merge_impl): over any of them nothing is written, and no host round trip separates the packing
+// from the copy. flags: bit 0 the live-flag output fits, bit 1 the caller takes segments.
+__host__ __device__ __forceinline__ bool emit_fits(const Tail& t, uint64_t pos_cap, uint64_t stream_cap, uint32_t seg_cap,
+                                          uint32_t flags, bool have_out) {
+  return (flags & 1u) && t.tot_c <= pos_cap && t.tot_b <= stream_cap && t.n_segments <= seg_cap &&
+         !(t.tot_c && !have_out) && !(t.n_segments && !(flags & 2u));
+}
+
 __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
     uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
     const uint64_t* __restrict__ P, const uint32_t* __restrict__ C, const ldb_merge_segment* __restrict__ segs,
-    uint32_t n_segs, uint8_t* __restrict__ stream, ldb_merge_pos* __restrict__ pos) {
+    const Tail* __restrict__ tail, uint64_t pos_cap, uint64_t stream_cap, uint32_t seg_cap, uint32_t flags,
+    uint8_t* __restrict__ stream, ldb_merge_pos* __restrict__ pos) {
+  const Tail tl = *tail;
+  if (!emit_fits(tl, pos_cap, stream_cap, seg_cap, flags, pos && stream) || tl.tot_c == 0) return;
+  const uint32_t n_segs = tl.n_segments;
   __shared__ const uint8_t* s_src[kCopyWaves][64];
   __shared__ uint8_t* s_dst[kCopyWaves][64];
   __shared__ uint32_t s_nb[kCopyWaves][64];
@@ -1010,6 +1081,13 @@ namespace {
 // one by one into dense storage. Fills fdh (nf + 1 descriptors; is_target from `files`) and n. A fatal
 // scan status of a file is returned with h_result's status / bad_file / n_records set. With
 // use_cache, the previous scan of the same files (ldb_merge_route_dev's) is reused.
+int merge_scan_lanes(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* files, int io_type,
+                     ldb_scan_result* d_res, const std::vector<uint64_t>& sbase, hipStream_t s, bool scan_hash);
+int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* files, int io_type,
+                      ldb_scan_result* d_res, std::vector<FileDesc>& fdh, uint64_t& n, ldb_merge_file_stat* h_stats,
+                      ldb_merge_result* h_result, hipStream_t s, const std::vector<uint64_t>& sbase,
+                      std::vector<ldb_scan_result>& rh, bool scan_hash);
+
 int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* files, int io_type,
                ldb_scan_result* d_res, std::vector<FileDesc>& fdh, uint64_t& n, ldb_merge_file_stat* h_stats,
                ldb_merge_result* h_result, hipStream_t s, bool use_cache) {
@@ -1036,6 +1114,42 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
   for (uint32_t i = 0; i < nf; ++i) sbase[i + 1] = sbase[i] + files[i].len / 64 + 1024;
   rc = grow_recs(m, std::max<uint64_t>(sbase[nf], 4096), 0, s);
   if (rc != LDB_OK) return rc;
+  // LDB_MERGE_SCAN_HASH=1: the scans' run prefixes also emit the key hashes k_insert / k_route_count
+  // then skip. Off by default: measured even (config 5: 4.894 ms with, 4.864 without,
+  // gpurun_out/r2_merge_H*.json) -- the key bytes are read once either way, in the scan or in k_insert.
+  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") != nullptr && atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
+  // every file's replay scan in ONE batched pipeline (ldb_scan.hip enqueue_scan_batch) on the
+  // caller's context and stream; a set the batch does not take (a tiny image) goes file by file
+  {
+    std::vector<const uint8_t*> im(nf);
+    std::vector<uint64_t> ln(nf), cp(nf);
+    std::vector<uint32_t> fi(nf);
+    std::vector<void*> ou(nf);
+    std::vector<uint64_t*> hs(nf);
+    for (uint32_t i = 0; i < nf; ++i) {
+      im[i] = files[i].d_image;
+      ln[i] = files[i].len;
+      fi[i] = files[i].fid;
+      ou[i] = m->recs + sbase[i];
+      cp[i] = sbase[i + 1] - sbase[i];
+      hs[i] = m->hashes + sbase[i];
+    }
+    rc = nf ? ldb_scan_files_dev_batched(ctx, (int)nf, im.data(), ln.data(), fi.data(), io_type, ou.data(), cp.data(),
+                                         d_res, s, scan_hash ? hs.data() : nullptr)
+            : LDB_ERR_ARG;
+    if (rc != LDB_OK && rc != LDB_ERR_ARG) return rc;
+  }
+  if (rc != LDB_OK) rc = merge_scan_lanes(ctx, m, nf, files, io_type, d_res, sbase, s, scan_hash);
+  if (rc != LDB_OK) return rc;
+  if (nf) MHIP(hipMemcpyAsync(rh.data(), d_res, sizeof(ldb_scan_result) * nf, hipMemcpyDeviceToHost, s));
+  MHIP(hipStreamSynchronize(s));
+  return merge_scan_finish(ctx, m, nf, files, io_type, d_res, fdh, n, h_stats, h_result, s, sbase, rh, scan_hash);
+}
+
+// the replay scans file by file, dealt round-robin over the caller's context and the aux contexts
+int merge_scan_lanes(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* files, int io_type,
+                     ldb_scan_result* d_res, const std::vector<uint64_t>& sbase, hipStream_t s, bool scan_hash) {
+  int rc = LDB_OK;
   if (!m->fork) {
     const char* e = getenv("LDB_MERGE_SCAN_LANES");
     const int want = std::min(std::max(e ? atoi(e) : 4, 1), MergeWs::kMaxAux + 1) - 1;
@@ -1048,10 +1162,6 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
     }
   }
   const int lanes = std::min<int>(1 + m->n_aux, (int)nf);   // the caller's context is lane 0
-  // LDB_MERGE_SCAN_HASH=1: the scans' run prefixes also emit the key hashes k_insert / k_route_count
-  // then skip. Off by default: measured even (config 5: 4.894 ms with, 4.864 without,
-  // gpurun_out/r2_merge_H*.json) -- the key bytes are read once either way, in the scan or in k_insert.
-  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") != nullptr && atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
   if (lanes > 1) {
     MHIP(hipEventRecord(m->fork, s));
     for (int a = 0; a + 1 < lanes; ++a) MHIP(hipStreamWaitEvent(m->aux_s[a], m->fork, 0));
@@ -1073,8 +1183,15 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
     MHIP(hipEventRecord(m->join[a], m->aux_s[a]));
     MHIP(hipStreamWaitEvent(s, m->join[a], 0));
   }
-  if (nf) MHIP(hipMemcpyAsync(rh.data(), d_res, sizeof(ldb_scan_result) * nf, hipMemcpyDeviceToHost, s));
-  MHIP(hipStreamSynchronize(s));
+  return LDB_OK;
+}
+
+// after the replay scans: a dense rescan on a capacity miss, then the file descriptors
+int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* files, int io_type,
+                      ldb_scan_result* d_res, std::vector<FileDesc>& fdh, uint64_t& n, ldb_merge_file_stat* h_stats,
+                      ldb_merge_result* h_result, hipStream_t s, const std::vector<uint64_t>& sbase,
+                      std::vector<ldb_scan_result>& rh, bool scan_hash) {
+  int rc = LDB_OK;
   bool slotted = true;
   for (uint32_t i = 0; i < nf && slotted; ++i) {
     if (rh[i].status == LDB_ERR_CAPACITY) slotted = false;
@@ -1177,6 +1294,7 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   // ---- 2. liveness
   uint64_t tcap = 1024;   // >= 1.25 slots per record (load <= 0.8 when every key is distinct)
   while (tcap < n + n / 4) tcap <<= 1;
+  if (!ext_live && tcap > (1ull << 31)) return h_result->status = LDB_ERR_ARG;   // slot ids are 31-bit (k_insert)
   const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
   const uint64_t nlb = (n + 255) / 256;
   const uint64_t o_part = 0, o_slot = align256(o_part + 16 * (nlb + 1));
@@ -1202,7 +1320,13 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   if (!ext_live) MHIP(hipMemsetAsync(d_tk, 0, 8 * tcap, s));   // hash table slots
   const uint32_t nbk = (uint32_t)((n + 255) / 256);
   if (n) {
-    if (!ext_live) k_insert<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot);
+    // LDB_INSERT_CAS=1: claim by CAS without the load first. Off: slower (config 5 k_insert 1.96 ms
+    // against 1.72 ms, gpurun_out/ktm_b3) -- a failed CAS costs more than the load it replaces.
+    static const bool cas_first = getenv("LDB_INSERT_CAS") != nullptr && atoi(getenv("LDB_INSERT_CAS")) != 0;
+    if (!ext_live) {
+      if (cas_first) k_insert<true><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now);
+      else k_insert<false><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now);
+    }
     k_live<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, d_slot, last_in, now, live_ok ? d_live : nullptr, d_esz, d_part,
                                d_fst);
     k_file_stats<<<nf, 256, 0, s>>>(d_fd, nf, n, d_part, d_fst);
@@ -1219,17 +1343,28 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
     MHIP(hipMemsetAsync(d_P, 0, 8, s));
     MHIP(hipMemsetAsync(d_C, 0, 4, s));
   }
-  k_pack<<<1, 64, 0, s>>>(d_P, n, active_fid, active_off, max_file_size, d_segs, seg_cap + 1, d_tail);
+  k_pack<<<1, 64, 0, s>>>(d_P, d_C, n, active_fid, active_off, max_file_size, d_segs, seg_cap + 1, d_tail);
+  const uint32_t gate = (live_ok ? 1u : 0u) | (h_segs ? 2u : 0u);
+  if (n) {   // gated on the device by the capacities (emit_fits): no host round trip in between
+    const uint32_t ngrp = (uint32_t)((n + 64 * kCopyWaves - 1) / (64 * kCopyWaves));
+    k_emit_copy<<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, d_tail, pos_cap, stream_cap, seg_cap,
+                                                 gate, d_stream, d_pos);
+  }
   MHIP(hipGetLastError());
-  uint64_t tot_b = 0;
-  uint32_t tot_c = 0;
-  Tail tail;
-  std::vector<unsigned long long> fst(2 * (nf + 1));
-  MHIP(hipMemcpyAsync(&tot_b, d_P + n, 8, hipMemcpyDeviceToHost, s));
-  MHIP(hipMemcpyAsync(&tot_c, d_C + n, 4, hipMemcpyDeviceToHost, s));
-  MHIP(hipMemcpyAsync(&tail, d_tail, sizeof(Tail), hipMemcpyDeviceToHost, s));
-  MHIP(hipMemcpyAsync(fst.data(), d_fst, 16ull * (nf + 1), hipMemcpyDeviceToHost, s));
+  MHIP(hipEventRecord(m->ev[3], s));
+  // one copy back: the per-file stats and the tail (adjacent in `small`)
+  std::vector<uint8_t> sm(o_tail + sizeof(Tail) - o_fst);
+  MHIP(hipMemcpyAsync(sm.data(), m->small + o_fst, sm.size(), hipMemcpyDeviceToHost, s));
   MHIP(hipStreamSynchronize(s));
+  Tail tail;
+  std::memcpy(&tail, sm.data() + (o_tail - o_fst), sizeof(Tail));
+  std::vector<unsigned long long> fst(2 * (nf + 1));
+  std::memcpy(fst.data(), sm.data(), 16ull * (nf + 1));
+  MHIP(hipEventElapsedTime(&m->t_scan, m->ev[0], m->ev[1]));
+  MHIP(hipEventElapsedTime(&m->t_live, m->ev[1], m->ev[2]));
+  MHIP(hipEventElapsedTime(&m->t_compact, m->ev[2], m->ev[3]));
+  const uint64_t tot_b = tail.tot_b;
+  const uint32_t tot_c = tail.tot_c;
   h_result->n_emit = tot_c;
   h_result->emit_bytes = tot_b;
   h_result->end_fid = tail.end_fid;
@@ -1242,24 +1377,12 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
       h_stats[i].live_bytes = fst[2 * i + 1];
     }
   }
-  if (!live_ok || tot_c > pos_cap || tot_b > stream_cap || tail.n_segments > seg_cap ||
-      (tot_c && (!d_pos || !d_stream)) || (tail.n_segments && !h_segs)) {
-    MHIP(hipEventRecord(m->ev[3], s));
-    return h_result->status = LDB_ERR_CAPACITY;
-  }
-  if (tot_c) {
-    const uint32_t ngrp = (uint32_t)((n + 64 * kCopyWaves - 1) / (64 * kCopyWaves));
-    k_emit_copy<<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, tail.n_segments,
-                                                 d_stream, d_pos);
-    MHIP(hipGetLastError());
-  }
-  MHIP(hipEventRecord(m->ev[3], s));
-  if (tail.n_segments)
+  if (!emit_fits(tail, pos_cap, stream_cap, seg_cap, gate, d_pos && d_stream))
+    return h_result->status = LDB_ERR_CAPACITY;   // k_emit_copy wrote nothing
+  if (tail.n_segments) {
     MHIP(hipMemcpyAsync(h_segs, d_segs, sizeof(ldb_merge_segment) * tail.n_segments, hipMemcpyDeviceToHost, s));
-  MHIP(hipStreamSynchronize(s));
-  MHIP(hipEventElapsedTime(&m->t_scan, m->ev[0], m->ev[1]));
-  MHIP(hipEventElapsedTime(&m->t_live, m->ev[1], m->ev[2]));
-  MHIP(hipEventElapsedTime(&m->t_compact, m->ev[2], m->ev[3]));
+    MHIP(hipStreamSynchronize(s));
+  }
   h_result->status = LDB_OK;
   return LDB_OK;
 }
@@ -1421,7 +1544,7 @@ extern "C" int ldb_encode_entries_dev(ldb_ctx* ctx, uint64_t n, const ldb_encode
   } else {
     MHIP(hipMemsetAsync(d_P, 0, 8, s));
   }
-  k_pack<<<1, 64, 0, s>>>(d_P, n, active_fid, active_off, max_file_size, d_segs, seg_cap + 1, d_tail);
+  k_pack<<<1, 64, 0, s>>>(d_P, nullptr, n, active_fid, active_off, max_file_size, d_segs, seg_cap + 1, d_tail);
   MHIP(hipGetLastError());
   uint64_t tot = 0;
   uint32_t bad = 0;
@@ -1520,7 +1643,7 @@ extern "C" int ldb_merge_repack_dev(ldb_ctx* ctx, uint64_t n, const uint32_t* d_
     if (rc != LDB_OK) return rc;
     Tail* d_tail = reinterpret_cast<Tail*>(m->small + o_tail);
     ldb_merge_segment* d_segs = reinterpret_cast<ldb_merge_segment*>(m->small + o_seg);
-    k_pack<<<1, 64, 0, s>>>(d_P, n, active_fid, active_off, max_file_size, d_segs, dev_cap + 1, d_tail);
+    k_pack<<<1, 64, 0, s>>>(d_P, nullptr, n, active_fid, active_off, max_file_size, d_segs, dev_cap + 1, d_tail);
     MHIP(hipGetLastError());
     MHIP(hipMemcpyAsync(&tot, d_P + n, 8, hipMemcpyDeviceToHost, s));
     MHIP(hipMemcpyAsync(&tail, d_tail, sizeof(Tail), hipMemcpyDeviceToHost, s));

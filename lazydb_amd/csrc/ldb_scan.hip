@@ -322,6 +322,10 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // When entry 1 is not a run member the prefix is skipped outright (K = 0: the region pipeline from
 // offset 0 -- the same scan, without a run of one). Shifts come from the x^(8n) table (n <= kW).
 // Workgroup 0 publishes K = 0 or the entry size for the pipeline. Returns false when there is no run.
+// Every pipeline kernel serves one scan (its Pipe by value, p0) or, with kB, one file of a batched
+// scan: grid.y = file, its Pipe from the device array pb (enqueue_scan_batch).
+#define LDB_PIPE_SELECT const Pipe p = kB ? pb[blockIdx.y] : p0
+
 __device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
   __shared__ uint32_t xn[kUniLevels];
   __shared__ uint32_t win[2][16];   // bytes [0, 64) and [sz, sz + 64) of the image, zero past len
@@ -586,8 +590,41 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   }
 }
 static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
+
+
+// a batched scan's run prefixes: grid.y = file. The Pipes travel as kernel arguments (not through
+// a device pointer like the other batched stages): kernarg loads stay re-loadable constants, so the
+// hot loop keeps k_uniform's register budget (8 waves per SIMD).
+constexpr int kUniBatch = 16;
+struct UniBatch {
+  Pipe p[kUniBatch];
+};
+template <bool kHash>
+__global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
+  const Pipe p = b.p[blockIdx.y];
+  __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + kUniTabWords];   // S table, combine tables
+  __shared__ UniSetup su;
+  if (!uni_prepare(p, su, stab + 5120)) return;
+  {
+    const uint4* g = reinterpret_cast<const uint4*>(p.gtab);
+    uint4* t = reinterpret_cast<uint4*>(stab);
+    for (int i = threadIdx.x; i < 5120 / 4; i += blockDim.x) t[i] = g[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
+#define LDB_UNI_CASE(n) case n: uni_waves<n, false, kHash>(p, su, stab, lane, wave, 0, p.len); break;
+    LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
+    LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
+#undef LDB_UNI_CASE
+    default: break;
+  }
+}
 // ---------------------------------------------------------------- k_scan_main
-__global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
+template <bool kB>
+__global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
   // CRC tables in a static LDS array: its address is a link-time constant, so every table read
   // folds the table base into the ds_read offset field
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
@@ -742,7 +779,9 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p) {
 // the pre-chain pipeline did every region); k_link / k_repair / k_combine then verify them like
 // any other region. Staging is synchronous (rare regions).
 constexpr int kFbWaves = 4;
-__global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p) {
+template <bool kB>
+__global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p0, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
   const uint32_t n = (uint32_t)min((uint64_t)p.ctr[4], p.nreg);
   if ((uint64_t)blockIdx.x * kFbWaves >= n) return;   // no deferred region for this block
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
@@ -785,7 +824,9 @@ __global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p) {
 }
 
 // ---------------------------------------------------------------- k_link
-__global__ void k_link(Pipe p) {
+template <bool kB>
+__global__ void k_link(Pipe p0, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t rf = first_region(p);
   if (r >= p.nreg || r < rf) return;
@@ -816,7 +857,9 @@ struct CohRd {
   }
 };
 
-__global__ __launch_bounds__(64) void k_repair(Pipe p) {
+template <bool kB>
+__global__ __launch_bounds__(64) void k_repair(Pipe p0, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
   const uint32_t nfail = (uint32_t)min((uint64_t)p.ctr[0], p.nreg + 1);
   if (nfail == 0) return;
   // CRC tables in a static LDS array: its address is a link-time constant, so every table read
@@ -883,7 +926,10 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p) {
 }
 
 // ---------------------------------------------------------------- k_combine
-__global__ __launch_bounds__(256) void k_combine(Pipe p) {
+template <bool kB>
+__global__ __launch_bounds__(256) void k_combine(Pipe p0, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
+  if ((uint64_t)blockIdx.x * blockDim.x >= p.nreg) return;   // a batched grid sized for a longer file
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ uint64_t s_sum[256];
   uint64_t cnt = 0;
@@ -942,7 +988,9 @@ __device__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out)
 // counts (k_combine), its regions are scanned in LDS, and tuples are copied flat (thread j of
 // the block's output range finds its region by binary search). The block holding the terminal
 // region writes the ldb_scan_result.
-__global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
+template <bool kB>
+__global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
   __shared__ uint32_t s_off[kBlkRegions + 1];
   __shared__ uint32_t s_wsum[kBlkRegions / 64];
   __shared__ uint64_t s_part[kBlkRegions / 64];
@@ -1042,7 +1090,9 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p) {
 
 // ---------------------------------------------------------------- k_serial
 // One lane walks the chain exactly like index.go:84-95 (global memory, byte-wise CRC).
-__global__ __launch_bounds__(64) void k_serial(Pipe p, int only_on_overflow) {
+template <bool kB>
+__global__ __launch_bounds__(64) void k_serial(Pipe p0, int only_on_overflow, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
   if (threadIdx.x != 0) return;
   if (only_on_overflow && !p.ctr[1]) return;
   struct G {
@@ -1156,6 +1206,12 @@ struct ldb_ctx {
   std::vector<hipEvent_t> chunk_ev;
   double t_run = 0, t_main = 0, t_total = 0;
   uint64_t t_n = 0;
+  // batched scans (enqueue_scan_batch): page-locked staging of the per-file Pipes, reused once the
+  // copy of the previous batch has completed (pipes_ev)
+  Pipe* h_pipes = nullptr;
+  int h_pipes_cap = 0;
+  hipEvent_t pipes_ev = nullptr;
+  bool pipes_ev_live = false;
   void* merge = nullptr;       // merge/GC workspace (ldb_merge.hip), created on first use
 };
 
@@ -1232,9 +1288,9 @@ int ensure_ws(ldb_ctx* c, uint64_t bytes) {
 }
 
 Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, uint32_t fid, int io, int kind,
-               void* out, uint64_t cap, ldb_scan_result* res) {
+               void* out, uint64_t cap, ldb_scan_result* res, uint8_t* w = nullptr) {
   Pipe p;
-  uint8_t* w = c->ws;
+  if (!w) w = c->ws;
   p.img = img;
   p.len = len;
   p.io = io;
@@ -1267,6 +1323,43 @@ int fence_ws(ldb_ctx* c, hipStream_t s) {
   c->ws_stream = s;
   c->ws_ev_live = true;
   return LDB_OK;
+}
+
+// kernel timing (ldb_kernel_timing): the event triple of the pipeline about to be enqueued, its start
+// recorded; null when timing is off
+int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
+  *out = nullptr;
+  if (!c->timing) return LDB_OK;
+  if (c->ev_used == c->evs.size()) {
+    if (c->evs.size() < 4096) {
+      ldb_ctx::EvTriple t{};
+      LDB_HIP(hipEventCreate(&t.e0));
+      LDB_HIP(hipEventCreate(&t.eu));
+      LDB_HIP(hipEventCreate(&t.e1));
+      LDB_HIP(hipEventCreate(&t.e2));
+      c->evs.push_back(t);
+    } else {
+      const int rc = resolve_timing(c);
+      if (rc != LDB_OK) return rc;
+    }
+  }
+  const ldb_ctx::EvTriple* ev = &c->evs[c->ev_used++];
+  LDB_HIP(hipEventRecord(ev->e0, s));
+  *out = ev;
+  return LDB_OK;
+}
+
+// persistent k_scan_main workgroups: exactly those resident at once (LDS-limited), so no second
+// dispatch round leaves a tail
+int scan_main_grid(const ldb_ctx* c, uint64_t nreg) {
+  const int per_cu = LDB_BLOCKS_PER_CU > 0 ? LDB_BLOCKS_PER_CU
+                                           : std::max(1, (int)(163840 / (main_lds_bytes() + kTabBytes)));
+  return (int)std::min<uint64_t>((nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * per_cu);
+}
+
+int uniform_grid(const ldb_ctx* c, uint64_t bytes) {
+  const uint64_t batches = bytes / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
+  return std::max(1, (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2));
 }
 
 // An image that is still being copied in: bytes [0, avail[i]) are in place once ev[i] has fired
@@ -1306,40 +1399,24 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   if (serial || len < (uint64_t)kMaxHeader) {
     LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
     LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0, 32, s));   // no run prefix: the walk starts at 0
-    hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 0);
+    hipLaunchKernelGGL(k_serial<false>, dim3(1), dim3(64), 0, s, p, 0, nullptr);
     LDB_HIP(hipGetLastError());
     return fence_ws(c, s);
   }
   const ldb_ctx::EvTriple* ev = nullptr;
-  if (c->timing) {
-    if (c->ev_used == c->evs.size()) {
-      if (c->evs.size() < 4096) {
-        ldb_ctx::EvTriple t{};
-        LDB_HIP(hipEventCreate(&t.e0));
-        LDB_HIP(hipEventCreate(&t.eu));
-        LDB_HIP(hipEventCreate(&t.e1));
-        LDB_HIP(hipEventCreate(&t.e2));
-        c->evs.push_back(t);
-      } else {
-        const int rc = resolve_timing(c);
-        if (rc != LDB_OK) return rc;
-      }
-    }
-    ev = &c->evs[c->ev_used++];
-    LDB_HIP(hipEventRecord(ev->e0, s));
-  }
+  rc = timing_begin(c, s, &ev);
+  if (rc != LDB_OK) return rc;
   // the run prefix: K = ~0 until k_uniform lowers it to the first entry outside the run
   LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, no_run ? 0 : 0xFF, 32, s));   // K = ~0, setup not published
   if (!no_run) {
     auto launch = [&](uint64_t lo, uint64_t hi) {
-      const uint64_t batches = (hi - lo) / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
-      const int ug = (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2);
+      const int ug = uniform_grid(c, hi - lo);
       if (chunked)
-        hipLaunchKernelGGL((k_uniform<true, false>), dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+        hipLaunchKernelGGL((k_uniform<true, false>), dim3(ug), dim3(64 * kUniWaves), 0, s, p, lo, hi);
       else if (p.hash_out)
-        hipLaunchKernelGGL((k_uniform<false, true>), dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+        hipLaunchKernelGGL((k_uniform<false, true>), dim3(ug), dim3(64 * kUniWaves), 0, s, p, lo, hi);
       else
-        hipLaunchKernelGGL((k_uniform<false, false>), dim3(std::max(ug, 1)), dim3(64 * kUniWaves), 0, s, p, lo, hi);
+        hipLaunchKernelGGL((k_uniform<false, false>), dim3(ug), dim3(64 * kUniWaves), 0, s, p, lo, hi);
     };
     if (chunked) {
       uint64_t lo = 0;
@@ -1354,23 +1431,130 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
     }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-  // persistent waves: exactly the workgroups that are resident at once (LDS-limited), so no
-  // second dispatch round leaves a tail
-  const int per_cu = LDB_BLOCKS_PER_CU > 0 ? LDB_BLOCKS_PER_CU
-                                           : std::max(1, (int)(163840 / (main_lds_bytes() + kTabBytes)));
-  const int grid = (int)std::min<uint64_t>((L.nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * per_cu);
-  hipLaunchKernelGGL(k_scan_main, dim3(grid), dim3(64 * kWPB), main_lds_bytes(), s, p);
+  hipLaunchKernelGGL(k_scan_main<false>, dim3(scan_main_grid(c, L.nreg)), dim3(64 * kWPB), main_lds_bytes(), s, p, nullptr);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   const int g256 = (int)((L.nreg + 255) / 256);
-  hipLaunchKernelGGL(k_fallback, dim3(c->n_cu), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p);
-  hipLaunchKernelGGL(k_link, dim3(g256), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(k_repair, dim3(1), dim3(64), repair_lds_bytes(), s, p);
-  hipLaunchKernelGGL(k_combine, dim3(g256), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(k_compact, dim3((unsigned)L.nblk), dim3(kBlkRegions), 0, s, p);
-  hipLaunchKernelGGL(k_serial, dim3(1), dim3(64), 0, s, p, 1);
+  hipLaunchKernelGGL(k_fallback<false>, dim3(c->n_cu), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p, nullptr);
+  hipLaunchKernelGGL(k_link<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
+  hipLaunchKernelGGL(k_repair<false>, dim3(1), dim3(64), repair_lds_bytes(), s, p, nullptr);
+  hipLaunchKernelGGL(k_combine<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
+  hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)L.nblk), dim3(kBlkRegions), 0, s, p, nullptr);
+  hipLaunchKernelGGL(k_serial<false>, dim3(1), dim3(64), 0, s, p, 1, nullptr);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
+}
+
+// ---------------------------------------------------------------- batched scans
+// Several device-resident images scanned as ONE pipeline: every stage is one launch whose grid.y
+// is the file (each file's Pipe in a device array at the head of the workspace, each file its own
+// workspace slice), so the per-file run prefixes share one dispatch with a single tail and the small
+// stitching kernels run once for all files instead of once per file. Every file must be a plain
+// device scan (len >= kMaxHeader, 16-B aligned); the caller falls back to enqueue_scan otherwise.
+struct BatchFile {
+  const uint8_t* img;
+  uint64_t len;
+  uint32_t fid;
+  void* out;
+  uint64_t cap;
+  ldb_scan_result* res;
+  uint64_t* hash_out;   // all files or none
+};
+
+bool batch_eligible(const uint8_t* img, uint64_t len) {
+  return img && len >= (uint64_t)kMaxHeader && ((uintptr_t)img & 15) == 0 && len < (1ull << 40);
+}
+
+// the control words every pipeline starts from (enqueue_scan's memsets): ctr zero, K = ~0, setup
+// not published
+__global__ __launch_bounds__(64) void k_batch_init(const Pipe* __restrict__ pb) {
+  const Pipe& p = pb[blockIdx.x];
+  if (threadIdx.x < 8) p.ctr[threadIdx.x] = 0u;
+  if (threadIdx.x < 4) p.dyn[threadIdx.x] = ~0ull;
+}
+
+int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s) {
+  if (!c || nf < 0 || (io != LDB_IO_FILEIO && io != LDB_IO_MMAP) ||
+      (kind != LDB_TUPLE_INDEX && kind != LDB_TUPLE_ENTRY))
+    return LDB_ERR_ARG;
+  if (nf == 0) return LDB_OK;
+  const bool hashed = f[0].hash_out != nullptr;
+  std::vector<WsLayout> Ls(nf);
+  std::vector<uint64_t> off(nf);
+  uint64_t o = (sizeof(Pipe) * (uint64_t)nf + 255) & ~255ull;
+  int ug = 1, mg = 1;
+  uint64_t nblk = 1;
+  for (int i = 0; i < nf; ++i) {
+    if (!batch_eligible(f[i].img, f[i].len) || !f[i].res || (f[i].cap && !f[i].out) ||
+        (f[i].hash_out != nullptr) != hashed)
+      return LDB_ERR_ARG;
+    Ls[i] = layout(f[i].len);
+    off[i] = o;
+    o += Ls[i].total;
+    ug = std::max(ug, uniform_grid(c, f[i].len));
+    mg = std::max(mg, scan_main_grid(c, Ls[i].nreg));
+    nblk = std::max(nblk, Ls[i].nblk);
+  }
+  int rc = ensure_ws(c, o);
+  if (rc != LDB_OK) return rc;
+  if (!c->pipes_ev) LDB_HIP(hipEventCreateWithFlags(&c->pipes_ev, hipEventDisableTiming));
+  if (c->pipes_ev_live) LDB_HIP(hipEventSynchronize(c->pipes_ev));   // the previous batch's copy is done
+  c->pipes_ev_live = false;
+  if (c->h_pipes_cap < nf) {
+    if (c->h_pipes) (void)hipHostFree(c->h_pipes);
+    c->h_pipes = nullptr;
+    c->h_pipes_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_pipes), sizeof(Pipe) * (size_t)nf) != hipSuccess)
+      return LDB_ERR_NOMEM;
+    c->h_pipes_cap = nf;
+  }
+  for (int i = 0; i < nf; ++i) {
+    c->h_pipes[i] = make_pipe(c, Ls[i], f[i].img, f[i].len, f[i].fid, io, kind, f[i].out, f[i].cap, f[i].res,
+                              c->ws + off[i]);
+    c->h_pipes[i].hash_out = f[i].hash_out;
+  }
+  const Pipe* d_pipes = reinterpret_cast<const Pipe*>(c->ws);
+  const Pipe p0{};   // unused by the kB instances
+  if (c->ws_ev_live && c->ws_stream != s) LDB_HIP(hipStreamWaitEvent(s, c->ws_ev, 0));
+  LDB_HIP(hipMemcpyAsync(const_cast<Pipe*>(d_pipes), c->h_pipes, sizeof(Pipe) * (size_t)nf, hipMemcpyHostToDevice, s));
+  LDB_HIP(hipEventRecord(c->pipes_ev, s));
+  c->pipes_ev_live = true;
+  const ldb_ctx::EvTriple* ev = nullptr;
+  rc = timing_begin(c, s, &ev);
+  if (rc != LDB_OK) return rc;
+  const unsigned n = (unsigned)nf;
+  hipLaunchKernelGGL(k_batch_init, dim3(n), dim3(64), 0, s, d_pipes);
+  // the run prefixes: the whole batch gets the workgroups one file's launch would (uniform_grid, 2
+  // per CU at most), dealt evenly over its files (LDB_UNI_BATCH_BPC: workgroups per CU, A/B)
+  static const int bpc = getenv("LDB_UNI_BATCH_BPC") ? std::max(1, atoi(getenv("LDB_UNI_BATCH_BPC"))) : 2;
+  for (int i0 = 0; i0 < nf; i0 += kUniBatch) {
+    UniBatch ub{};
+    const int m = std::min(kUniBatch, nf - i0);
+    const int ugb = std::min(ug, std::max(1, (c->n_cu * bpc + m - 1) / m));
+    for (int i = 0; i < m; ++i) ub.p[i] = c->h_pipes[i0 + i];
+    if (hashed)
+      hipLaunchKernelGGL(k_uniform_batch<true>, dim3(ugb, (unsigned)m), dim3(64 * kUniWaves), 0, s, ub);
+    else
+      hipLaunchKernelGGL(k_uniform_batch<false>, dim3(ugb, (unsigned)m), dim3(64 * kUniWaves), 0, s, ub);
+  }
+  if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+  hipLaunchKernelGGL(k_scan_main<true>, dim3(mg, n), dim3(64 * kWPB), main_lds_bytes(), s, p0, d_pipes);
+  if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
+  hipLaunchKernelGGL(k_fallback<true>, dim3(c->n_cu, n), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p0, d_pipes);
+  hipLaunchKernelGGL(k_link<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
+  hipLaunchKernelGGL(k_repair<true>, dim3(1, n), dim3(64), repair_lds_bytes(), s, p0, d_pipes);
+  hipLaunchKernelGGL(k_combine<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
+  hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)nblk, n), dim3(kBlkRegions), 0, s, p0, d_pipes);
+  hipLaunchKernelGGL(k_serial<true>, dim3(1, n), dim3(64), 0, s, p0, 1, d_pipes);
+  if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
+  LDB_HIP(hipGetLastError());
+  return fence_ws(c, s);
+}
+
+// LDB_SCAN_BATCH=0 turns the batched multi-file path off (A/B)
+bool batch_enabled() {
+  static const bool on = getenv("LDB_SCAN_BATCH") == nullptr || atoi(getenv("LDB_SCAN_BATCH")) != 0;
+  return on;
 }
 
 }  // namespace
@@ -1389,6 +1573,26 @@ __attribute__((visibility("hidden"))) int ldb_scan_file_dev_hashed(ldb_ctx* c, c
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
   return enqueue_scan(c, d_image, len, fid, io_type, LDB_TUPLE_INDEX, d_out, cap, d_result, (hipStream_t)stream,
                       false, false, nullptr, d_hash);
+}
+
+// internal (merge engine): the replay scans of several device images in one batched pipeline
+// (enqueue_scan_batch), index tuples; d_hash null or one array per file (ldb_scan_file_dev_hashed).
+// Returns LDB_ERR_ARG without enqueuing anything when the batch is off or a file is not eligible.
+__attribute__((visibility("hidden"))) int ldb_scan_files_dev_batched(ldb_ctx* c, int n_files,
+                                                                     const uint8_t* const* d_images,
+                                                                     const uint64_t* lens, const uint32_t* fids,
+                                                                     int io_type, void* const* d_outs,
+                                                                     const uint64_t* caps,
+                                                                     ldb_scan_result* d_results, void* stream,
+                                                                     uint64_t* const* d_hash) {
+  if (!c || n_files <= 0 || !batch_enabled()) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  std::vector<BatchFile> bf(n_files);
+  for (int i = 0; i < n_files; ++i) {
+    if (!batch_eligible(d_images[i], lens[i])) return LDB_ERR_ARG;
+    bf[i] = BatchFile{d_images[i], lens[i], fids[i], d_outs[i], caps[i], d_results + i, d_hash ? d_hash[i] : nullptr};
+  }
+  return enqueue_scan_batch(c, n_files, bf.data(), io_type, LDB_TUPLE_INDEX, (hipStream_t)stream);
 }
 
 const char* ldb_status_str(int s) {
@@ -1434,11 +1638,17 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }
-  if (hipFuncSetAttribute((const void*)k_scan_main, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if (hipFuncSetAttribute((const void*)k_scan_main<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)main_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_repair, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)k_scan_main<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)main_lds_bytes()) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_repair<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)repair_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_fallback, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)k_repair<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)repair_lds_bytes()) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_fallback<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)fallback_lds_bytes()) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_fallback<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)fallback_lds_bytes()) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
@@ -1459,6 +1669,8 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->h_out) (void)hipFree(c->h_out);
   if (c->h_res) (void)hipFree(c->h_res);
   if (c->h_stream) (void)hipStreamDestroy(c->h_stream);
+  if (c->h_pipes) (void)hipHostFree(c->h_pipes);
+  if (c->pipes_ev) (void)hipEventDestroy(c->pipes_ev);
   for (int i = 0; i < c->n_cp; ++i)
     if (c->cp[i]) (void)hipStreamDestroy(c->cp[i]);
   for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
@@ -1500,6 +1712,14 @@ int ldb_scan_files_dev(ldb_ctx* c, int n_files, const uint8_t* const* d_images, 
   if (!c || n_files < 0 || (n_files && (!d_images || !lens || !fids || !d_outs || !caps || !d_results)))
     return LDB_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  bool batch = batch_enabled() && n_files > 1;
+  for (int i = 0; batch && i < n_files; ++i) batch = batch_eligible(d_images[i], lens[i]);
+  if (batch) {
+    std::vector<BatchFile> bf(n_files);
+    for (int i = 0; i < n_files; ++i)
+      bf[i] = BatchFile{d_images[i], lens[i], fids[i], d_outs[i], caps[i], d_results + i, nullptr};
+    return enqueue_scan_batch(c, n_files, bf.data(), io_type, tuple_kind, (hipStream_t)stream);
+  }
   uint64_t mx = 0;
   for (int i = 0; i < n_files; ++i) mx = std::max(mx, lens[i]);
   int rc = ensure_ws(c, layout(mx).total);

@@ -78,6 +78,55 @@ def test_scan_files_dev_batch(gpu_engine):
         same(r, tup, *coracle.scan(im, 0))
 
 
+def _scan_files(eng, imgs, io, kind, caps, fid0=5):
+    """ldb_scan_files_dev over device copies of imgs; returns [(result, tuples)]"""
+    import torch
+    from lazydb_amd import _native as N
+    dt = N.INDEX_TUPLE if kind == N.TUPLE_INDEX else N.ENTRY_TUPLE
+    d = [to_dev(im) if im.size else to_dev(np.zeros(16, np.uint8)) for im in imgs]
+    outs = [eng.alloc_out(max(c, 1), kind) for c in caps]
+    res = torch.zeros(N.RESULT_BYTES * len(imgs), dtype=torch.uint8, device="cuda:0")
+    k = len(imgs)
+    s = torch.cuda.current_stream()
+    N.check(N.lib().ldb_scan_files_dev(
+        eng.ctx, k, (C.c_void_p * k)(*[x.data_ptr() for x in d]), (C.c_uint64 * k)(*[im.size for im in imgs]),
+        (C.c_uint32 * k)(*[fid0 + i for i in range(k)]), io, kind, (C.c_void_p * k)(*[o.data_ptr() for o in outs]),
+        (C.c_uint64 * k)(*caps), C.c_void_p(res.data_ptr()), C.c_void_p(s.cuda_stream)), "ldb_scan_files_dev")
+    rb = res.cpu().numpy().tobytes()
+    got = []
+    for i in range(k):
+        r = N.ScanResult.from_buffer_copy(rb[i * N.RESULT_BYTES:(i + 1) * N.RESULT_BYTES])
+        n = min(r.n_entries, caps[i])
+        got.append((r, np.frombuffer(outs[i].cpu().numpy().tobytes()[: n * dt.itemsize], dt)))
+    return got
+
+
+@pytest.mark.parametrize("io", [0, 1])
+@pytest.mark.parametrize("kind", [0, 1])
+def test_scan_files_dev_batched_pipeline(gpu_engine, golden, io, kind):
+    """The batched pipeline (every stage one launch, grid.y = file): every golden fixture that is at
+    least one header window long, plus run / Zipf / small-entry images of different lengths and one
+    undersized output, scanned as ONE batch; each file must match its own oracle scan. A set holding
+    a shorter image goes file by file (the same results)."""
+    meta, gimgs = golden
+    names = sorted({m["name"] for m in meta})
+    imgs = [np.frombuffer(gimgs[nm], np.uint8) for nm in names]
+    imgs = [im for im in imgs if im.size >= 38] + _files(7, 5)
+    caps = [im.size // 10 + 16 for im in imgs]
+    caps[-2] = 3   # LDB_ERR_CAPACITY for this file only
+    for i, (r, tup) in enumerate(_scan_files(gpu_engine, imgs, io, kind, caps)):
+        assert r.fid == 5 + i
+        ref, rt = coracle.scan(imgs[i], io, fid=5 + i, tuple_kind=kind, cap=caps[i])
+        assert (r.status, r.end_off, r.n_entries) == (ref.status, ref.end_off, ref.n_entries), (i, r.as_dict())
+        assert tup.tobytes() == rt.tobytes(), i
+    short = [np.frombuffer(gimgs[nm], np.uint8) for nm in names if len(gimgs[nm]) < 38][:3]
+    mixed = short + _files(8, 2)
+    for i, (r, tup) in enumerate(_scan_files(gpu_engine, mixed, io, kind, [im.size // 10 + 16 for im in mixed])):
+        ref, rt = coracle.scan(mixed[i], io, fid=5 + i, tuple_kind=kind)
+        assert (r.status, r.end_off, r.n_entries) == (ref.status, ref.end_off, ref.n_entries), (i, r.as_dict())
+        assert tup.tobytes() == rt.tobytes(), i
+
+
 def test_bytes_past_len_ignored(gpu_engine):
     """include/lazydb_gpu.h: the kernels may load up to 15 bytes past `len` (whole 16-B granules);
     those bytes must never change a result. Each image sits at the start of a larger device buffer
