@@ -56,6 +56,8 @@ constexpr int kScanItems = 8;    // items per thread in the prefix-sum kernels
 constexpr int kScanBlock = 256;
 constexpr uint64_t kScanTile = (uint64_t)kScanItems * kScanBlock;
 constexpr uint32_t kMaxOwners = 64;   // ranks of a hash-partitioned merge (ldb_merge_route_dev)
+constexpr uint64_t kGBits = 40;       // record positions in the liveness table: 1 TiB of input per merge
+constexpr uint64_t kGMask = (1ull << kGBits) - 1;
 
 struct FileDesc {       // one input file, in device memory
   const uint8_t* img;
@@ -65,6 +67,8 @@ struct FileDesc {       // one input file, in device memory
   uint32_t fid;
   const uint64_t* hashes;   // key hashes of the file's first n_hashed records (the scan's run prefix)
   uint64_t n_hashed;
+  uint64_t gbase;       // the file's first byte in the concatenation of all images (the table's
+                        // record positions g; desc[n_files].gbase = total bytes)
 };
 
 struct Tail {           // k_pack output
@@ -145,6 +149,16 @@ __device__ bool key_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
   for (; i < n; ++i)
     if (a[i] != b[i]) return false;
   return true;
+}
+
+// the file holding position g of the images' concatenation (last file with gbase <= g)
+__device__ __forceinline__ uint32_t file_of_g(const FileDesc* d, uint32_t n_files, uint64_t g) {
+  uint32_t lo = 0, hi = n_files - 1;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (d[mid].gbase <= g) lo = mid; else hi = mid - 1;
+  }
+  return lo;
 }
 
 __device__ __forceinline__ uint32_t file_of(const FileDesc* d, uint32_t n_files, uint64_t seq) {
@@ -239,17 +253,65 @@ __device__ __forceinline__ uint64_t record_hash(const FileDesc* fd, uint32_t n_f
   return i < fd[f].n_hashed ? fd[f].hashes[i] : key_hash(kp, kl);
 }
 
-// A slot is one 64-bit word (hash tag << 32 | max record id + 1), claimed by CAS and then raised by a
-// 64-bit atomicMax: every record that reaches a slot has the slot's key (it claimed it, or compared its
-// key bytes equal with the slot's current record), so the tag half never changes and the low half ends
-// as the key's last record. 8-B slots keep the table within the Infinity Cache at config-5 sizes.
+// The key length of the record whose key starts at byte ko of img, from the bytes before the key: the
+// header ends with the k_size and v_size varints (log_entry.go:66-67), and in a binary.Varint every
+// byte but the last carries the continuation bit, so walking back from the key, v_size's bytes end
+// at ko - 1 and k_size's bytes are those after the previous varint's last byte. The up to 32 bytes
+// before the key hold both (<= 10 bytes each) and the last byte of the varint before them; they are
+// the lines the key itself is read from.
+__device__ __forceinline__ uint32_t key_len_before(const uint8_t* img, uint64_t ko) {
+  const uint32_t K = ko < 32 ? (uint32_t)ko : 32u;
+  const uint8_t* w = img + ko - K;
+  uint32_t m = 0;   // bit i: window byte i carries the continuation bit
+  uint64_t W[4] = {0, 0, 0, 0};
+  if (K == 32) {
+    __builtin_memcpy(W, w, 32);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t c = (uint32_t)(W[j >> 1] >> (32 * (j & 1))) & 0x80808080u;
+      m |= (((c >> 7) | (c >> 14) | (c >> 21) | (c >> 28)) & 0xFu) << (4 * j);
+    }
+  } else {   // a file's first record: no bytes before the image
+    for (uint32_t i = 0; i < K; ++i) m |= (uint32_t)(w[i] >> 7) << i;
+  }
+  const uint32_t z = ~m & (K == 32 ? 0xFFFFFFFFu : ((1u << K) - 1u));   // last bytes of varints
+  const uint32_t bv = z & ((1u << (K - 1)) - 1u);   // below v_size's last byte (K - 1)
+  const int p = 31 - __builtin_clz(bv | 1u);        // k_size's last byte
+  const uint32_t bk = z & ((1u << p) - 1u);
+  const int q = bk ? 31 - __builtin_clz(bk) : -1;   // the previous varint's last byte
+  const int L = p - q;                              // k_size's bytes [q + 1, p]
+  uint64_t u = 0;
+  if (K == 32 && L <= 8) {   // from the registers: the 8 bytes from q + 1, 7-bit groups packed
+    const int b0 = q + 1, wi = b0 >> 3, sh = 8 * (b0 & 7);
+    const uint64_t lo = wi == 0 ? W[0] : wi == 1 ? W[1] : wi == 2 ? W[2] : W[3];
+    const uint64_t hi = wi == 0 ? W[1] : wi == 1 ? W[2] : wi == 2 ? W[3] : 0ull;
+    uint64_t x = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    x &= L == 8 ? ~0ull : ((1ull << (8 * L)) - 1ull);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u |= (x >> j) & (0x7Full << (7 * j));
+  } else {
+    for (int i = q + 1, sh = 0; i <= p && sh < 64; ++i, sh += 7) u |= (uint64_t)(w[i] & 0x7Fu) << sh;
+  }
+  return (uint32_t)(int64_t)((u >> 1) ^ (0ull - (u & 1ull)));   // zig-zag (binary.Varint)
+}
+
+// A slot is one 64-bit word (hash tag << 40 | g + 1), g = the position of the record's KEY in the
+// concatenation of the images (FileDesc::gbase + offset + hdr_size): g grows with the replay order,
+// so it names the record AND orders it. The slot is claimed by CAS and then raised by a 64-bit
+// atomicMax: every record that reaches a slot has the slot's key (it claimed it, or compared its key
+// bytes equal with the slot's current record), so the tag never changes and the low 40 bits end as
+// the key's last record. A probe that meets its tag reads the slot's key straight from g (its length
+// from the bytes before it, key_len_before), with no detour through the record's index tuple. 8-B
+// slots keep the table within the Infinity Cache at config-5 sizes.
 // kCasFirst: claim by CAS straight away (the CAS returns the slot's word when it is taken) instead
 // of a load first. The slot id goes to slot[seq] with bit 31 = "expired" (db.go:255, ExpiredAt <=
 // now): the header sits next to the key this kernel reads, so k_live needs no image access for it.
-template <bool kCasFirst>
+// kAbl (timing ablations, results invalid; LDB_INSERT_ABL): 1 no atomicMax, 2 no key compare, 3 both,
+// 4 no table at all (key read + hash only)
+template <bool kCasFirst, int kAbl = 0>
 __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
                                                 unsigned long long* tab, uint64_t mask, uint32_t* __restrict__ slot,
-                                                int64_t now) {
+                                                int64_t now, uint64_t tagmask) {
   __shared__ FileDesc s_fd[kFdLds];
   const FileDesc* fd = stage_fd(gfd, n_files, s_fd);
   uint64_t seq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -261,8 +323,12 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
   const int64_t ea = expired_at_of(fd[f].img, e.offset);
   const bool expired = ea != 0 && ea <= now;
   const uint64_t h = record_hash(fd, n_files, seq, kp, kl);
-  const unsigned long long mine = (h & 0xFFFFFFFF00000000ull) | (seq + 1);
+  const unsigned long long mine = (h & ~kGMask) | (fd[f].gbase + e.offset + e.hdr_size + 1);
   uint64_t i = h & mask;
+  if (kAbl == 4) {
+    slot[seq] = (uint32_t)(h & mask) | (expired ? 0x80000000u : 0u);
+    return;
+  }
   for (;;) {
     unsigned long long v;
     if (kCasFirst) {
@@ -276,11 +342,18 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
         v = prev;
       }
     }
-    if ((v >> 32) == (h >> 32)) {
-      uint32_t rl;
-      const uint8_t* rp = key_of(fd, n_files, (v & 0xFFFFFFFFull) - 1, &rl);
-      if (rl == kl && key_equal(kp, rp, kl)) {
-        atomicMax(&tab[i], mine);
+    if (((v ^ mine) & tagmask) == 0) {   // tagmask: ~kGMask (0 = every probe compares keys: a test mode)
+      uint32_t rl = kl;
+      const uint8_t* rp = kp;
+      if (!(kAbl & 2)) {
+        const uint64_t g = (v & kGMask) - 1;
+        const uint32_t fr = file_of_g(fd, n_files, g);
+        const uint64_t ko = g - fd[fr].gbase;
+        rl = key_len_before(fd[fr].img, ko);
+        rp = fd[fr].img + ko;
+      }
+      if ((kAbl & 2) || (rl == kl && key_equal(kp, rp, kl))) {
+        if (!(kAbl & 1)) atomicMax(&tab[i], mine);
         break;
       }
     }
@@ -312,7 +385,7 @@ __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __rest
     f = file_of(fd, n_files, seq);
     const Rec e = rec_of(fd, f, seq);
     const uint32_t sl = last_in ? 0u : slot[seq];   // k_insert's slot, bit 31 = expired
-    const bool lastw = last_in ? last_in[seq] != 0 : (uint32_t)tab[sl & 0x7FFFFFFFu] == (uint32_t)(seq + 1);
+    const bool lastw = last_in ? last_in[seq] != 0 : (tab[sl & 0x7FFFFFFFu] & kGMask) == fd[f].gbase + e.offset + e.hdr_size + 1;
     live = lastw && e.stat != kSDelete;
     size = e.enc_hdr_size + e.k_size + e.v_size;
     bool emit = live && fd[f].is_target;
@@ -1197,7 +1270,7 @@ int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_fil
     if (rh[i].status == LDB_ERR_CAPACITY) slotted = false;
     if (rh[i].status < 0) break;   // a fatal scan status: later files do not matter
   }
-  uint64_t base = 0;
+  uint64_t base = 0, gbase = 0;
   for (uint32_t i = 0; i < nf; ++i) {
     if (!slotted) {   // dense rescan, growing the record array as needed
       for (;;) {
@@ -1216,7 +1289,8 @@ int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_fil
                                                                                       sbase[i + 1] - sbase[i]))
                                 : 0;
     fdh[i] = FileDesc{files[i].d_image, slotted ? m->recs + sbase[i] : m->recs + base, base, files[i].is_target,
-                      files[i].fid, slotted ? m->hashes + sbase[i] : nullptr, nh};
+                      files[i].fid, slotted ? m->hashes + sbase[i] : nullptr, nh, gbase};
+    gbase += files[i].len;
     if (h_stats) {
       h_stats[i] = ldb_merge_file_stat{rh[i].status, files[i].fid, rh[i].n_entries, rh[i].end_off, 0, 0};
     }
@@ -1229,7 +1303,7 @@ int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_fil
     base += rh[i].n_entries;
   }
   n = base;
-  fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0, nullptr, 0};
+  fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0, nullptr, 0, gbase};
   h_result->n_records = n;
   if (n >= 0xFFFFFFFFull) return h_result->status = LDB_ERR_ARG;   // record ids are 32-bit
   m->cache_ok = true;
@@ -1295,6 +1369,7 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   uint64_t tcap = 1024;   // >= 1.25 slots per record (load <= 0.8 when every key is distinct)
   while (tcap < n + n / 4) tcap <<= 1;
   if (!ext_live && tcap > (1ull << 31)) return h_result->status = LDB_ERR_ARG;   // slot ids are 31-bit (k_insert)
+  if (!ext_live && fdh[nf].gbase >= kGMask) return h_result->status = LDB_ERR_ARG;   // table positions are 40-bit
   const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
   const uint64_t nlb = (n + 255) / 256;
   const uint64_t o_part = 0, o_slot = align256(o_part + 16 * (nlb + 1));
@@ -1322,10 +1397,18 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   if (n) {
     // LDB_INSERT_CAS=1: claim by CAS without the load first. Off: slower (config 5 k_insert 1.96 ms
     // against 1.72 ms, gpurun_out/ktm_b3) -- a failed CAS costs more than the load it replaces.
+    // LDB_MERGE_TAGLESS=1 (tests): no hash tag, every probe that meets a taken slot compares the keys
+    const char* tl = getenv("LDB_MERGE_TAGLESS");
+    const uint64_t tagmask = tl && atoi(tl) != 0 ? 0ull : ~kGMask;
     static const bool cas_first = getenv("LDB_INSERT_CAS") != nullptr && atoi(getenv("LDB_INSERT_CAS")) != 0;
     if (!ext_live) {
-      if (cas_first) k_insert<true><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now);
-      else k_insert<false><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now);
+      static const int abl = getenv("LDB_INSERT_ABL") ? atoi(getenv("LDB_INSERT_ABL")) : 0;
+      if (abl == 1) k_insert<false, 1><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
+      else if (abl == 2) k_insert<false, 2><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
+      else if (abl == 3) k_insert<false, 3><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
+      else if (abl == 4) k_insert<false, 4><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
+      else if (cas_first) k_insert<true><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
+      else k_insert<false><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
     }
     k_live<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, d_slot, last_in, now, live_ok ? d_live : nullptr, d_esz, d_part,
                                d_fst);

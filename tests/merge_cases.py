@@ -117,6 +117,25 @@ def case_tiny_entries():
                        now=NOW)
 
 
+def case_prefix_keys():
+    """Keys that are prefixes of one another, each followed by value bytes that continue the longer
+    keys ("a" + value "aaa..." reads like the key "aaaa"), rewritten across files, with headers of
+    every varint length (TTLs, tx ids): key identity must come from the key length, not the bytes."""
+    keys = [b"a" * n for n in range(0, 40)] + [b"ab" * n for n in range(1, 9)]
+    files = []
+    for f in range(4):
+        recs = []
+        for i, k in enumerate(keys):
+            if (i + f) % 3 == 0:
+                continue
+            recs.append(dict(key=k, value=b"a" * (5 + (i * 7 + f) % 50) + b"b" * f,
+                             expired_at=[0, NOW + 100, NOW - 100, 1 << 40][(i + f) % 4],
+                             tx_id=[0, 5, 1 << 30, (1 << 62) + 3][(i * 3 + f) % 4]))
+        files.append(_log(recs))
+    return [(img, 40 + f, f != 3) for f, img in enumerate(files)], \
+        dict(active_fid=43, active_off=int(files[3].size), max_file_size=1 << 16, now=NOW)
+
+
 def case_crc_corrupt():
     return [(golden_img("mixed_64k"), 1, True), (golden_img("crc_corrupt"), 2, True),
             (np.zeros(64, np.uint8), 3, False)], dict(active_fid=3, active_off=0, max_file_size=1 << 20, now=NOW)
@@ -133,4 +152,5 @@ def small_cases():
     for s in (1, 2, 3):
         out[f"hot_keys{s}"] = case_hot_keys(s)
     out["tiny_entries"] = case_tiny_entries()
+    out["prefix_keys"] = case_prefix_keys()
     return out

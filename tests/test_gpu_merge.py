@@ -55,6 +55,16 @@ def test_merge_small_cases(eng, name):
     check_case(eng, files, kw)
 
 
+@pytest.mark.parametrize("name", sorted(MC.small_cases()))
+def test_merge_small_cases_tagless(eng, name, monkeypatch):
+    """The same cases with the liveness table's hash tag off (LDB_MERGE_TAGLESS): every probe that
+    meets a taken slot compares the keys, so the key-length recovery from the bytes before a
+    slot's key (key_len_before) and the byte compare decide every duplicate."""
+    monkeypatch.setenv("LDB_MERGE_TAGLESS", "1")
+    files, kw = MC.small_cases()[name]
+    check_case(eng, files, kw)
+
+
 @pytest.mark.parametrize("seed", [11, 12])
 def test_merge_medium_mixed(eng, seed):
     # 4 files x 32 MiB, 64/256 entries, 2% deletes, 5% expiring records, rollover every 8 MiB
