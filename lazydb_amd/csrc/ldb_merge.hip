@@ -320,9 +320,12 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
   const Rec e = rec_of(fd, f, seq);
   const uint32_t kl = e.k_size;
   const uint8_t* kp = fd[f].img + e.offset + e.hdr_size;
-  const int64_t ea = expired_at_of(fd[f].img, e.offset);
+  // a record of its file's run prefix (the records the scan hashed) has entry 0's header bytes, so
+  // entry 0's ExpiredAt (one line every such record shares) instead of a line of its own
+  const bool in_run = seq - fd[f].seq_base < fd[f].n_hashed;
+  const int64_t ea = expired_at_of(fd[f].img, in_run ? 0 : e.offset);
   const bool expired = ea != 0 && ea <= now;
-  const uint64_t h = record_hash(fd, n_files, seq, kp, kl);
+  const uint64_t h = in_run ? fd[f].hashes[seq - fd[f].seq_base] : key_hash(kp, kl);
   const unsigned long long mine = (h & ~kGMask) | (fd[f].gbase + e.offset + e.hdr_size + 1);
   uint64_t i = h & mask;
   if (kAbl == 4) {
@@ -810,6 +813,29 @@ __host__ __device__ __forceinline__ bool emit_fits(const Tail& t, uint64_t pos_c
          !(t.tot_c && !have_out) && !(t.n_segments && !(flags & 2u));
 }
 
+// 16 bytes at any address from whole aligned 16-B granules: the granule holding p, and the next one
+// only when p is unaligned (it then holds byte p + 15 of the piece, so it lies inside the image's
+// granules, lazydb_gpu.h); the bytes are funnel-shifted into place. An unaligned 16-B load straddles
+// two granules per lane instead.
+__device__ __forceinline__ uint4 load16_aligned_pair(const uint8_t* p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) const v4u* g4_t;
+  const uintptr_t a = (uintptr_t)p & ~(uintptr_t)15;
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 15);
+  const v4u lo = *(g4_t)a;
+  if (sh == 0) return make_uint4(lo.x, lo.y, lo.z, lo.w);
+  const v4u hi = *(g4_t)(a + 16);
+  const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t q = sh >> 2, r = sh & 3u;
+  uint32_t o[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)   // dwords q .. q + 4 of d
+    o[k] = q == 0 ? d[k] : q == 1 ? d[k + 1] : q == 2 ? d[k + 2] : (k + 3 < 8 ? d[k + 3] : 0u);
+  return make_uint4(__builtin_amdgcn_alignbyte(o[1], o[0], r), __builtin_amdgcn_alignbyte(o[2], o[1], r),
+                    __builtin_amdgcn_alignbyte(o[3], o[2], r), __builtin_amdgcn_alignbyte(o[4], o[3], r));
+}
+
+template <int kCopyUnroll>   // pieces in flight per lane
 __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
     uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
     const uint64_t* __restrict__ P, const uint32_t* __restrict__ C, const ldb_merge_segment* __restrict__ segs,
@@ -870,49 +896,69 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
   s_nb[w][lane] = nb;
   s_ex[w][lane] = inc - pieces;
   __syncthreads();
-  for (uint32_t t = lane; t < total; t += 64) {
-    int lo = 0, hi = 63;   // last record with ex <= t and pieces > 0 (ties: the later record owns t)
-    while (lo < hi) {
-      int mid = (lo + hi + 1) >> 1;
-      if (s_ex[w][mid] <= t) lo = mid; else hi = mid - 1;
+  // kCopyUnroll pieces per lane per round: every full piece's load is issued before the round's first
+  // store, so a lane keeps that many 16-B reads in flight (one at a time left the copy latency-bound)
+  typedef unsigned int v4g __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) const uint8_t* gsrc_t;
+  typedef __attribute__((address_space(1))) v4g* gdst_t;
+  for (uint32_t t0 = 0; t0 < total; t0 += 64 * kCopyUnroll) {
+    const uint8_t* ss[kCopyUnroll];
+    uint8_t* dd[kCopyUnroll];
+    uint32_t ll[kCopyUnroll];
+    uint4 vv[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const uint32_t t = t0 + 64u * u + lane;
+      ll[u] = 0;
+      ss[u] = nullptr;
+      dd[u] = nullptr;
+      if (t < total) {
+        int lo = 0, hi = 63;   // last record with ex <= t and pieces > 0 (ties: the later record owns t)
+        while (lo < hi) {
+          int mid = (lo + hi + 1) >> 1;
+          if (s_ex[w][mid] <= t) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t j = t - s_ex[w][lo];
+        uint8_t* const d0 = s_dst[w][lo];
+        const uint32_t nbr = s_nb[w][lo];
+        const uint32_t head = min(nbr, (16u - (uint32_t)((uintptr_t)d0 & 15u)) & 15u);
+        const uint32_t at = head ? (j ? head + 16 * (j - 1) : 0u) : 16 * j;   // piece start within the record
+        ll[u] = (head && j == 0) ? head : min(16u, nbr - at);
+        ss[u] = s_src[w][lo] + at;
+        dd[u] = d0 + at;
+        if (ll[u] == 16) vv[u] = load16_aligned_pair(ss[u]);
+      }
     }
-    const uint32_t j = t - s_ex[w][lo];
-    uint8_t* const d0 = s_dst[w][lo];
-    const uint32_t nbr = s_nb[w][lo];
-    const uint32_t head = min(nbr, (16u - (uint32_t)((uintptr_t)d0 & 15u)) & 15u);
-    const uint32_t at = head ? (j ? head + 16 * (j - 1) : 0u) : 16 * j;   // piece start within the record
-    const uint32_t len = (head && j == 0) ? head : min(16u, nbr - at);
-    const uint8_t* s = s_src[w][lo] + at;
-    uint8_t* d = d0 + at;
-    if (len == 16) {   // d is 16-B aligned here; both sides are touched once: global, non-temporal
-      typedef unsigned int v4g __attribute__((ext_vector_type(4)));
-      typedef __attribute__((address_space(1))) const uint8_t* gsrc_t;
-      typedef __attribute__((address_space(1))) v4g* gdst_t;
-      uint4 v;
-      __builtin_memcpy(&v, (gsrc_t)s, 16);
-      const v4g x = {v.x, v.y, v.z, v.w};
-      __builtin_nontemporal_store(x, (gdst_t)d);
-    } else {
-      uint32_t b = 0;
-      if (len & 8) {
-        uint64_t v;
-        __builtin_memcpy(&v, s, 8);
-        __builtin_memcpy(d, &v, 8);
-        b = 8;
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const uint32_t len = ll[u];
+      const uint8_t* s = ss[u];
+      uint8_t* d = dd[u];
+      if (len == 16) {   // d is 16-B aligned here; both sides are touched once: global, non-temporal
+        const v4g x = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+        __builtin_nontemporal_store(x, (gdst_t)d);
+      } else if (len) {
+        uint32_t b = 0;
+        if (len & 8) {
+          uint64_t v;
+          __builtin_memcpy(&v, s, 8);
+          __builtin_memcpy(d, &v, 8);
+          b = 8;
+        }
+        if (len & 4) {
+          uint32_t v;
+          __builtin_memcpy(&v, s + b, 4);
+          __builtin_memcpy(d + b, &v, 4);
+          b += 4;
+        }
+        if (len & 2) {
+          uint16_t v;
+          __builtin_memcpy(&v, s + b, 2);
+          __builtin_memcpy(d + b, &v, 2);
+          b += 2;
+        }
+        if (len & 1) d[b] = s[b];
       }
-      if (len & 4) {
-        uint32_t v;
-        __builtin_memcpy(&v, s + b, 4);
-        __builtin_memcpy(d + b, &v, 4);
-        b += 4;
-      }
-      if (len & 2) {
-        uint16_t v;
-        __builtin_memcpy(&v, s + b, 2);
-        __builtin_memcpy(d + b, &v, 2);
-        b += 2;
-      }
-      if (len & 1) d[b] = s[b];
     }
   }
   if (pieces && !canon) {   // re-encode the header (EncodeEntry :52-66) and its CRC (:75-76)
@@ -1187,10 +1233,13 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
   for (uint32_t i = 0; i < nf; ++i) sbase[i + 1] = sbase[i] + files[i].len / 64 + 1024;
   rc = grow_recs(m, std::max<uint64_t>(sbase[nf], 4096), 0, s);
   if (rc != LDB_OK) return rc;
-  // LDB_MERGE_SCAN_HASH=1: the scans' run prefixes also emit the key hashes k_insert / k_route_count
-  // then skip. Off by default: measured even (config 5: 4.894 ms with, 4.864 without,
-  // gpurun_out/r2_merge_H*.json) -- the key bytes are read once either way, in the scan or in k_insert.
-  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") != nullptr && atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
+  // The scans' run prefixes also emit the key hashes, which k_insert / k_route_count then take instead
+  // of reading the key; k_insert reads a run record's ExpiredAt from the file's entry 0 (same header
+  // bytes), so such a record's own lines are read only when its hash tag meets a taken slot. Config 5:
+  // 4.482 ms against 4.602 without (replay 1.58 vs 1.23 ms, liveness 1.56 vs 2.03; gpurun_out/m3_h*).
+  // LDB_MERGE_SCAN_HASH=0 turns it off. Measured and rejected: the entry's G lanes hashing key chunks in
+  // parallel (shuffle-combined): replay 1.88-1.97 ms.
+  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") == nullptr || atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
   // every file's replay scan in ONE batched pipeline (ldb_scan.hip enqueue_scan_batch) on the
   // caller's context and stream; a set the batch does not take (a tiny image) goes file by file
   {
@@ -1366,8 +1415,10 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   MHIP(hipEventRecord(m->ev[1], s));
 
   // ---- 2. liveness
-  uint64_t tcap = 1024;   // >= 1.25 slots per record (load <= 0.8 when every key is distinct)
-  while (tcap < n + n / 4) tcap <<= 1;
+  // >= (1 + 1/tdiv) slots per record: load <= 0.8 at the default when every key is distinct
+  static const uint64_t tdiv = getenv("LDB_MERGE_TDIV") ? (uint64_t)std::max(1, atoi(getenv("LDB_MERGE_TDIV"))) : 4;
+  uint64_t tcap = 1024;
+  while (tcap < n + n / tdiv) tcap <<= 1;
   if (!ext_live && tcap > (1ull << 31)) return h_result->status = LDB_ERR_ARG;   // slot ids are 31-bit (k_insert)
   if (!ext_live && fdh[nf].gbase >= kGMask) return h_result->status = LDB_ERR_ARG;   // table positions are 40-bit
   const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
@@ -1430,8 +1481,16 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   const uint32_t gate = (live_ok ? 1u : 0u) | (h_segs ? 2u : 0u);
   if (n) {   // gated on the device by the capacities (emit_fits): no host round trip in between
     const uint32_t ngrp = (uint32_t)((n + 64 * kCopyWaves - 1) / (64 * kCopyWaves));
-    k_emit_copy<<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, d_tail, pos_cap, stream_cap, seg_cap,
-                                                 gate, d_stream, d_pos);
+    static const int unroll = getenv("LDB_COPY_UNROLL") ? atoi(getenv("LDB_COPY_UNROLL")) : 1;
+    if (unroll >= 4)
+      k_emit_copy<4><<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, d_tail, pos_cap, stream_cap,
+                                                      seg_cap, gate, d_stream, d_pos);
+    else if (unroll == 2)
+      k_emit_copy<2><<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, d_tail, pos_cap, stream_cap,
+                                                      seg_cap, gate, d_stream, d_pos);
+    else
+      k_emit_copy<1><<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, d_tail, pos_cap, stream_cap,
+                                                      seg_cap, gate, d_stream, d_pos);
   }
   MHIP(hipGetLastError());
   MHIP(hipEventRecord(m->ev[3], s));
