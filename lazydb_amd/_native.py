@@ -28,7 +28,7 @@ ENTRY_TUPLE = np.dtype([("offset", "<u8"), ("expired_at", "<i8"), ("tx_id", "<u8
 class ScanResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("fid", C.c_uint32), ("n_entries", C.c_uint64), ("end_off", C.c_uint64),
                 ("n_repairs", C.c_uint32), ("n_regions", C.c_uint32),
-                ("n_fast", C.c_uint32), ("reserved_", C.c_uint32), ("n_run", C.c_uint64)]
+                ("n_fast", C.c_uint32), ("n_broken", C.c_uint32), ("n_run", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -297,22 +297,31 @@ LDB_HD int32_t term_status(uint64_t t) { return (int32_t)(t & 15) - 2; }
 
 namespace ldb {
 
-// Repair walk (DESIGN.md §3.4). Wave-uniform control flow: every lane of the one repairing
-// wavefront evaluates the same loads. `rd` reads summaries coherently, `first_term(lo, hi)`
-// returns the first region in (lo, hi] whose (verified) walk stopped with a terminal status
-// or -1, and `run(r, enter)` re-processes region r with its entering position forced and
-// returns its new summary.  Returns the number of regions re-processed.
-template <class Rd, class FirstTerm, class Run>
-LDB_HD uint32_t repair(const Pipe& p, uint32_t nfail, Rd rd, FirstTerm first_term, Run run) {
+// Link failures and walker claims share the workspace block of p.fail_src (8 (nreg + 1) bytes):
+//   fail flags  uint8_t[nreg + 1]: flag i <-> source rf - 1 + i (source rf - 1: region rf does not
+//               start at the chain's entry point x0; source r >= rf: region r's outgoing link is broken).
+//               k_link writes every flag of the pipeline, so nothing is cleared between scans.
+//   claims      uint32_t[nreg] after them: a region one optimistic walker re-runs (k_link zeroes them).
+LDB_HD uint8_t* fail_flags(const Pipe& p) { return reinterpret_cast<uint8_t*>(p.fail_src); }
+LDB_HD uint32_t* repair_claims(const Pipe& p) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p.fail_src) + ((p.nreg + 1 + 15) & ~15ull));
+}
+LDB_HD uint64_t n_fail_flags(const Pipe& p) { return p.nreg - first_region(p) + 1; }
+
+// Repair walk (DESIGN.md §3.3). Wave-uniform control flow: every lane of the one repairing
+// wavefront evaluates the same loads. `next_fail(done)` returns the smallest flagged source > done
+// (INT64_MAX: none), `rd` reads summaries coherently, `first_term(lo, hi)` returns the first region
+// in (lo, hi] whose (verified) walk stopped with a terminal status or -1, and `run(r, enter)`
+// re-processes region r with its entering position forced and returns its new summary.
+// Correct for ANY set of region summaries, each a valid processing of its region from its own start,
+// provided the flags name every region whose outgoing link is broken. Returns the regions re-processed.
+template <class NextFail, class Rd, class FirstTerm, class Run>
+LDB_HD uint32_t repair(const Pipe& p, NextFail next_fail, Rd rd, FirstTerm first_term, Run run) {
   const int64_t rf = (int64_t)first_region(p);   // source rf - 1: the chain's entry point x0
   int64_t done = rf - 2;
   uint32_t repairs = 0;
   for (;;) {
-    int64_t src = INT64_MAX;
-    for (uint32_t i = 0; i < nfail; ++i) {
-      const int64_t s = p.fail_src[i];
-      if (s > done && s < src) src = s;
-    }
+    const int64_t src = next_fail(done);
     if (src == INT64_MAX) break;
     if (first_term(done, src) >= 0) break;  // a verified region before src already ends the scan
     uint64_t x = src < rf ? chain_x0(p) : rd.exitp((uint64_t)src);
@@ -341,6 +350,40 @@ LDB_HD uint32_t repair(const Pipe& p, uint32_t nfail, Rd rd, FirstTerm first_ter
     if (stop) break;
   }
   return repairs;
+}
+
+// One optimistic walker (k_repair, first phase): assume source src lies on the true chain and
+// re-run the regions its exit leads through, as repair() would, until the walk merges into a region
+// that already starts there, ends, meets a region another walker claimed, or has taken kWalkMax
+// steps. Every region it writes is claimed first (`claim(r)`: true for the one walker that gets r), so
+// walkers never write the same region; what they read may be stale or another walker's, which is
+// harmless: each region they write is a valid processing from its new start, and the links are
+// checked again over all regions before the serial repair() runs (its precondition above).
+constexpr int kWalkMax = 256;
+template <class Rd, class Claim, class Run>
+LDB_HD uint32_t walk_source(const Pipe& p, int64_t src, Rd rd, Claim claim, Run run) {
+  const int64_t rf = (int64_t)first_region(p);
+  uint64_t x = src < rf ? chain_x0(p) : rd.exitp((uint64_t)src);
+  int64_t cur = src;
+  uint32_t runs = 0;
+  for (int step = 0; step < kWalkMax; ++step) {
+    if (x >= p.len) break;
+    const uint64_t m = x / kW;
+    bool stop = false;
+    for (int64_t k = cur + 1; k < (int64_t)m && !stop; ++k) {
+      if (rd.start((uint64_t)k) != kNone64) {
+        if (!claim((uint64_t)k)) stop = true;
+        else { run((uint64_t)k, kForceNone); ++runs; }
+      }
+    }
+    if (stop || rd.start(m) == x || !claim(m)) break;   // merged: the serial pass sees to a kOwnerOk landing
+    const RegionSum s = run(m, (uint32_t)(x - m * (uint64_t)kW));
+    ++runs;
+    if (s.status != kCont) break;
+    cur = (int64_t)m;
+    x = s.exitp;
+  }
+  return runs;
 }
 
 }  // namespace ldb

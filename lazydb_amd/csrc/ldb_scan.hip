@@ -778,7 +778,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
 // The regions k_scan_main deferred, each through region_process (speculative entry, exactly as
 // the pre-chain pipeline did every region); k_link / k_repair / k_combine then verify them like
 // any other region. Staging is synchronous (rare regions).
-constexpr int kFbWaves = 4;
+constexpr int kFbWaves = 16;   // 16 waves per CU (118 VGPRs, 149 KB of LDS)
 template <bool kB>
 __global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
@@ -824,26 +824,29 @@ __global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p0, const Pipe*
 }
 
 // ---------------------------------------------------------------- k_link
+// One thread per region: its outgoing link's flag (ldb_pipeline.h fail_flags; every flag of the
+// pipeline is written, the first region's also for the virtual source rf - 1) and its walker claim
+// cleared. ctr[0] counts the broken links.
 template <bool kB>
 __global__ void k_link(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t rf = first_region(p);
   if (r >= p.nreg || r < rf) return;
-  // fail_src holds nreg + 1 entries: one per region plus the first region's "does not start at the
-  // chain's entry point x0" (virtual source rf - 1)
-  bool bad = link_broken(p, r);
-  if (bad) {
-    const uint32_t i = atomicAdd(&p.ctr[0], 1u);
-    if (i <= p.nreg) p.fail_src[i] = (int64_t)r; else atomicOr(&p.ctr[5], 1u);
+  uint8_t* fl = fail_flags(p);
+  const bool bad = link_broken(p, r);
+  fl[r - rf + 1] = bad ? 1 : 0;
+  repair_claims(p)[r] = 0;
+  uint32_t nb = bad ? 1u : 0u;
+  if (r == rf) {
+    const bool b0 = p.rs[rf].start != chain_x0(p);
+    fl[0] = b0 ? 1 : 0;
+    nb += b0 ? 1u : 0u;
   }
-  if (r == rf && p.rs[rf].start != chain_x0(p)) {
-    const uint32_t i = atomicAdd(&p.ctr[0], 1u);
-    if (i <= p.nreg) p.fail_src[i] = (int64_t)rf - 1; else atomicOr(&p.ctr[5], 1u);
-  }
+  if (nb) atomicAdd(&p.ctr[0], nb);
 }
 
-// ---------------------------------------------------------------- k_repair (one wavefront)
+// ---------------------------------------------------------------- k_repair
 struct CohRd {
   const Pipe* p;
   __device__ uint64_t start(uint64_t r) const {
@@ -857,36 +860,34 @@ struct CohRd {
   }
 };
 
+// Nothing to do unless k_link flagged a broken link (ctr[0]). Then, DESIGN.md §3.3:
+// 1. every wave of the grid takes flagged sources (64 flags per ballot) and walks each one
+//    optimistically (ldb_pipeline.h walk_source), claiming every region it re-runs;
+// 2. the last workgroup to finish (ctr[6]) re-checks every link over the summaries as they now are
+//    (the same flags, rewritten), and its first wave runs the serial repair() from those flags.
+// ctr[2] = regions re-run (both phases).
+constexpr int kRepWaves = 16;
 template <bool kB>
-__global__ __launch_bounds__(64) void k_repair(Pipe p0, const Pipe* __restrict__ pb) {
+__global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
-  const uint32_t nfail = (uint32_t)min((uint64_t)p.ctr[0], p.nreg + 1);
-  if (nfail == 0) return;
+  if (p.ctr[0] == 0) return;
   // CRC tables in a static LDS array: its address is a link-time constant, so every table read
   // folds the table base into the ds_read offset field
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
+  __shared__ int s_last;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   copy_tables(tab, p.gtab);
-  WaveLds* wl = reinterpret_cast<WaveLds*>(smem);
-  uint8_t* buf = smem + sizeof(WaveLds);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  WaveLds* wl = reinterpret_cast<WaveLds*>(smem + wave * (sizeof(WaveLds) + kBuf));
+  uint8_t* buf = smem + wave * (sizeof(WaveLds) + kBuf) + sizeof(WaveLds);
   __syncthreads();
-  const int lane = threadIdx.x;
   GpuWave wp{lane};
   CohRd rd{&p};
   const int64_t rf = (int64_t)first_region(p);
-  auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
-    for (int64_t b = lo + 1 > rf ? lo + 1 : rf; b <= hi; b += 64) {
-      const int64_t r = b + lane;
-      bool t = false;
-      if (r >= 0 && r <= hi && (uint64_t)r < p.nreg) {
-        const int32_t st = __hip_atomic_load(&p.rs[r].status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = st != kCont && rd.start((uint64_t)r) != kNone64;
-      }
-      const uint64_t m = __ballot(t ? 1 : 0);
-      if (m) return b + __builtin_ctzll(m);
-    }
-    return -1;
-  };
+  uint8_t* fl = fail_flags(p);
+  uint32_t* claims = repair_claims(p);
+  const uint64_t nflag = n_fail_flags(p);
   auto run = [&](uint64_t r, uint32_t enter) -> RegionSum {
     const uint64_t R0 = r * (uint64_t)kW;
     // synchronous staging through registers
@@ -921,8 +922,69 @@ __global__ __launch_bounds__(64) void k_repair(Pipe p0, const Pipe* __restrict__
     GpuWave::sync();
     return s;
   };
-  const uint32_t n = repair(p, nfail, rd, first_term, run);
-  if (lane == 0) p.ctr[2] = n;
+  // ---- 1. optimistic walkers
+  uint32_t runs = 0;
+  for (uint64_t b = ((uint64_t)blockIdx.x * kRepWaves + wave) * 64; b < nflag;
+       b += (uint64_t)gridDim.x * kRepWaves * 64) {
+    uint64_t m = __ballot(b + lane < nflag && fl[b + lane] != 0);
+    while (m) {
+      const int i = __builtin_ctzll(m);
+      m &= m - 1;
+      runs += walk_source(p, rf - 1 + (int64_t)(b + i), rd,
+                          [&](uint64_t r) {   // wave-uniform: lane 0 claims, the wave follows
+                            uint32_t won = 0;
+                            if (lane == 0) won = atomicCAS(&claims[r], 0u, 1u) == 0u ? 1u : 0u;
+                            return __shfl((int)won, 0) != 0;
+                          },
+                          run);
+    }
+  }
+  if (lane == 0 && runs) atomicAdd(&p.ctr[2], runs);
+  // ---- 2. the last workgroup: links again, then the serial repair
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&p.ctr[6], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  uint32_t nb = 0;
+  for (uint64_t r = (uint64_t)rf + threadIdx.x; r < p.nreg; r += blockDim.x) {
+    bool bad = link_broken(p, r);
+    if ((int64_t)r == rf) {
+      const bool b0 = rd.start(r) != chain_x0(p);
+      fl[0] = b0 ? 1 : 0;
+      nb += b0 ? 1u : 0u;
+    }
+    fl[r - rf + 1] = bad ? 1 : 0;
+    nb += bad ? 1u : 0u;
+  }
+  if (nb) atomicAdd(&p.ctr[7], nb);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (wave != 0 || __hip_atomic_load(&p.ctr[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  auto next_fail = [&](int64_t done) -> int64_t {   // smallest flagged source > done
+    for (uint64_t b = (uint64_t)(done - (rf - 1) + 1); b < nflag; b += 64) {
+      const uint64_t m = __ballot(b + lane < nflag && fl[b + lane] != 0);
+      if (m) return rf - 1 + (int64_t)(b + __builtin_ctzll(m));
+    }
+    return INT64_MAX;
+  };
+  auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
+    for (int64_t b = lo + 1 > rf ? lo + 1 : rf; b <= hi; b += 64) {
+      const int64_t r = b + lane;
+      bool t = false;
+      if (r >= 0 && r <= hi && (uint64_t)r < p.nreg) {
+        const int32_t st = __hip_atomic_load(&p.rs[r].status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = st != kCont && rd.start((uint64_t)r) != kNone64;
+      }
+      const uint64_t m = __ballot(t ? 1 : 0);
+      if (m) return b + __builtin_ctzll(m);
+    }
+    return -1;
+  };
+  const uint32_t n = repair(p, next_fail, rd, first_term, run);
+  if (lane == 0 && n) atomicAdd(&p.ctr[2], n);
 }
 
 // ---------------------------------------------------------------- k_combine
@@ -1011,7 +1073,7 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __
       res.n_repairs = 0;
       res.n_regions = 0;
       res.n_fast = 0;
-      res.reserved_ = 0;
+      res.n_broken = 0;
       res.n_run = K;
       if (K > p.cap) res.status = LDB_ERR_CAPACITY;
       *p.result = res;
@@ -1065,7 +1127,7 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __
     res.n_repairs = p.ctr[2];
     res.n_regions = (uint32_t)(p.nreg - rf);
     res.n_fast = p.ctr[3];
-    res.reserved_ = 0;
+    res.n_broken = p.ctr[7];
     res.n_run = K;
     if (n > p.cap) res.status = LDB_ERR_CAPACITY;
     if (p.ctr[5]) res.status = LDB_ERR_INTERNAL;   // a device-side index guard fired (never expected)
@@ -1134,7 +1196,7 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p0, int only_on_overflow, co
   res.n_repairs = 0;
   res.n_regions = (uint32_t)p.nreg;
   res.n_fast = 0;
-  res.reserved_ = 0;
+  res.n_broken = 0;
   res.n_run = run_k(p);
   *p.result = res;
 }
@@ -1163,8 +1225,10 @@ __global__ __launch_bounds__(256) void k_read_reduce(const uint4* __restrict__ p
 }
 
 size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
-size_t repair_lds_bytes() { return sizeof(WaveLds) + kBuf; }
+size_t repair_lds_bytes() { return kRepWaves * (sizeof(WaveLds) + kBuf); }
 size_t fallback_lds_bytes() { return kFbWaves * (sizeof(WaveLds) + kBuf); }
+static_assert(kFbWaves * (sizeof(WaveLds) + kBuf) + kTabBytes <= 160 * 1024, "k_fallback: LDS per workgroup");
+static_assert(kRepWaves * (sizeof(WaveLds) + kBuf) + kTabBytes + 64 <= 160 * 1024, "k_repair: LDS per workgroup");
 
 }  // namespace
 
@@ -1263,7 +1327,7 @@ WsLayout layout(uint64_t len) {
   L.o_uni = take(kUniSetupBytes + 4 * kUniTabWords);   // run prefix: the published setup
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
-  L.o_fail = take(8 * (L.nreg + 1));
+  L.o_fail = take(8 * (L.nreg + 1) + 64);   // fail flags + walker claims (ldb_pipeline.h fail_flags)
   L.o_defer = take(4 * L.nreg);
   L.o_scratch = take(sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg);
   L.total = o;
@@ -1357,6 +1421,12 @@ int scan_main_grid(const ldb_ctx* c, uint64_t nreg) {
   return (int)std::min<uint64_t>((nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * per_cu);
 }
 
+// k_repair's workgroups: one wave per 64 flags, at most one workgroup per CU (they exit at once when
+// k_link found no broken link)
+int repair_grid(const ldb_ctx* c, uint64_t nreg) {
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((nreg + 1 + 64 * kRepWaves - 1) / (64 * kRepWaves), (uint64_t)c->n_cu));
+}
+
 int uniform_grid(const ldb_ctx* c, uint64_t bytes) {
   const uint64_t batches = bytes / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
   return std::max(1, (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2));
@@ -1436,7 +1506,8 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   const int g256 = (int)((L.nreg + 255) / 256);
   hipLaunchKernelGGL(k_fallback<false>, dim3(c->n_cu), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p, nullptr);
   hipLaunchKernelGGL(k_link<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
-  hipLaunchKernelGGL(k_repair<false>, dim3(1), dim3(64), repair_lds_bytes(), s, p, nullptr);
+  hipLaunchKernelGGL(k_repair<false>, dim3(repair_grid(c, L.nreg)), dim3(64 * kRepWaves), repair_lds_bytes(), s, p,
+                     nullptr);
   hipLaunchKernelGGL(k_combine<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
   hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)L.nblk), dim3(kBlkRegions), 0, s, p, nullptr);
   hipLaunchKernelGGL(k_serial<false>, dim3(1), dim3(64), 0, s, p, 1, nullptr);
@@ -1483,7 +1554,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   std::vector<uint64_t> off(nf);
   uint64_t o = (sizeof(Pipe) * (uint64_t)nf + 255) & ~255ull;
   int ug = 1, mg = 1;
-  uint64_t nblk = 1;
+  uint64_t nblk = 1, max_nreg = 1;
   for (int i = 0; i < nf; ++i) {
     if (!batch_eligible(f[i].img, f[i].len) || !f[i].res || (f[i].cap && !f[i].out) ||
         (f[i].hash_out != nullptr) != hashed)
@@ -1494,6 +1565,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     ug = std::max(ug, uniform_grid(c, f[i].len));
     mg = std::max(mg, scan_main_grid(c, Ls[i].nreg));
     nblk = std::max(nblk, Ls[i].nblk);
+    max_nreg = std::max(max_nreg, Ls[i].nreg);
   }
   int rc = ensure_ws(c, o);
   if (rc != LDB_OK) return rc;
@@ -1542,7 +1614,8 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   hipLaunchKernelGGL(k_fallback<true>, dim3(c->n_cu, n), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p0, d_pipes);
   hipLaunchKernelGGL(k_link<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
-  hipLaunchKernelGGL(k_repair<true>, dim3(1, n), dim3(64), repair_lds_bytes(), s, p0, d_pipes);
+  hipLaunchKernelGGL(k_repair<true>, dim3(repair_grid(c, max_nreg), n), dim3(64 * kRepWaves), repair_lds_bytes(), s,
+                     p0, d_pipes);
   hipLaunchKernelGGL(k_combine<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
   hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)nblk, n), dim3(kBlkRegions), 0, s, p0, d_pipes);
   hipLaunchKernelGGL(k_serial<true>, dim3(1, n), dim3(64), 0, s, p0, 1, d_pipes);

@@ -253,9 +253,9 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
   const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
   std::vector<uint64_t> blk(nblk, 0), tpos(2, ~0ull), dyn(2, 0);
   std::vector<RegionSum> rs(nreg);
-  std::vector<uint32_t> ctr(4, 0);
+  std::vector<uint32_t> ctr(8, 0);
   std::vector<ldb_index_tuple> scratch(nreg * (uint64_t)kRegionCap);
-  std::vector<int64_t> fail(nreg + 1);
+  std::vector<int64_t> fail(nreg + 9);   // fail flags + walker claims (8 (nreg + 1) + 64 B, as the GPU)
   Pipe p;
   p.img = img; p.len = len; p.io = io; p.fid = fid; p.nreg = nreg;
   p.gtab = emu.tab.data(); p.xw = emu.xw.data(); p.gsh = emu.gsh.data();
@@ -295,29 +295,66 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
     }
     for (uint64_t r : deferred) emu.run(p, r, kForceSpec);   // k_fallback
   }
-  // k_link
-  for (uint64_t r = rf; r < nreg; ++r) {
-    if (link_broken(p, r)) {
-      fail[ctr[0]++] = (int64_t)r;
-      if (getenv("LDB_EMU_DEBUG")) {
+  // k_link: every flag of the pipeline (ldb_pipeline.h fail_flags), claims cleared
+  uint8_t* fl = fail_flags(p);
+  uint32_t* claims = repair_claims(p);
+  const uint64_t nflag = n_fail_flags(p);
+  auto relink = [&]() -> uint32_t {
+    uint32_t nb = 0;
+    for (uint64_t r = rf; r < nreg; ++r) {
+      const bool bad = link_broken(p, r);
+      if (bad && getenv("LDB_EMU_DEBUG")) {
         const uint64_t m = rs[r].exitp / kW;
         fprintf(stderr, "fail r=%llu start=%llu exit=%llu st=%d -> m=%llu rs[m].start=%llu (rel %lld) st[m]=%d\n",
                 (unsigned long long)r, (unsigned long long)rs[r].start, (unsigned long long)rs[r].exitp, rs[r].status,
                 (unsigned long long)m, (unsigned long long)rs[m].start, (long long)(rs[m].start - m * kW), rs[m].status);
       }
+      fl[r - rf + 1] = bad ? 1 : 0;
+      nb += bad ? 1u : 0u;
+      if (r == rf) {
+        fl[0] = rs[rf].start != x0 ? 1 : 0;
+        nb += fl[0];
+      }
     }
-    if (r == rf && rs[rf].start != x0) fail[ctr[0]++] = (int64_t)rf - 1;
-  }
-  const uint32_t nfail = ctr[0];
-  // k_repair
+    return nb;
+  };
+  for (uint64_t r = rf; r < nreg; ++r) claims[r] = 0;
+  const uint32_t nfail = relink();
+  ctr[0] = nfail;
+  // k_repair: the optimistic walkers (in flag order here; any order is correct), the links again,
+  // then the serial repair from the fresh flags
+  uint32_t walker_runs = 0, n2 = 0;
+  auto run = [&](uint64_t r, uint32_t enter) { return emu.run(p, r, enter); };
   if (nfail) {
+    // LDB_EMU_WALKERS: "0" none (the serial repair alone), "rev" in reverse flag order (each walker
+    // reads its source before an earlier walker rewrites it: stale starting points, lost claims)
+    const char* wm = getenv("LDB_EMU_WALKERS");
+    const bool walk = !(wm && wm[0] == '0'), rev = wm && wm[0] == 'r';
+    for (uint64_t j = 0; walk && j < nflag; ++j) {
+      const uint64_t i = rev ? nflag - 1 - j : j;
+      if (fl[i])
+        walker_runs += walk_source(p, (int64_t)rf - 1 + (int64_t)i, Rd{&p},
+                                   [&](uint64_t r) { return claims[r]++ == 0; }, run);
+    }
+    n2 = relink();
+  }
+  if (n2) {
+    auto next_fail = [&](int64_t done) -> int64_t {
+      for (uint64_t i = (uint64_t)(done - ((int64_t)rf - 1) + 1); i < nflag; ++i)
+        if (fl[i]) return (int64_t)rf - 1 + (int64_t)i;
+      return INT64_MAX;
+    };
     auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
       for (int64_t r = std::max<int64_t>(lo + 1, (int64_t)rf); r <= hi && (uint64_t)r < nreg; ++r)
         if (rs[r].status != kCont && rs[r].start != kNone64) return r;
       return -1;
     };
-    ctr[2] = repair(p, nfail, Rd{&p}, first_term, [&](uint64_t r, uint32_t enter) { return emu.run(p, r, enter); });
+    ctr[2] = repair(p, next_fail, Rd{&p}, first_term, run);
   }
+  ctr[2] += walker_runs;
+  if (getenv("LDB_EMU_REPAIR_STATS"))
+    fprintf(stderr, "repair: %u flagged, %u walker runs, %u flagged after, %u serial runs\n", nfail, walker_runs, n2,
+            ctr[2] - walker_runs);
   // k_combine
   for (uint64_t r = rf; r < nreg; ++r) {
     const int32_t st = rs[r].status;

@@ -105,6 +105,30 @@ def test_emulated_engine_random(seed, run_len):
             assert_same(res, tup, ref, rt)
 
 
+@pytest.mark.parametrize("walkers", ["0", "rev", "fwd"])
+def test_emulated_two_phase_repair(golden, walkers, monkeypatch):
+    """k_repair's two phases (ldb_pipeline.h walk_source, then the links again and the serial
+    repair): the result is the oracle's whatever the walkers did -- none ("0", the serial repair
+    alone), in flag order, or in reverse flag order, where every walker starts from a source an
+    earlier walker has yet to rewrite and loses claims to it. Adversarial logs (values holding valid
+    entries, every header field varied, random binary) break links in most regions."""
+    from tests.golden import make_golden as G
+    monkeypatch.setenv("LDB_EMU_WALKERS", walkers)
+    meta, imgs = golden
+    cases = [np.frombuffer(imgs[m["name"]], np.uint8) for m in meta]
+    for seed in range(2):
+        for gen in (G.embedded, G.mixed, G.binary_values):
+            b = np.frombuffer(gen(50 + seed, 150000), np.uint8)
+            ref, _ = coracle.scan(b)
+            cases.append(np.concatenate([np.tile(b[: ref.end_off], 3), np.zeros(64, np.uint8)]))
+    for img in cases:
+        for io in (0, 1):
+            for run_len in (0, 1, 3):
+                res, tup, st = emu_scan(img, io, run_len)
+                ref, rt = coracle.scan(img, io)
+                assert_same(res, tup, ref, rt)
+
+
 def _log_with_entry_at(target: int, big_value: int, seed: int) -> np.ndarray:
     """Entries of 16-B keys and 100-B values (128-B entries) up to `target`, one 12-B-header
     filler that makes the next entry start exactly at `target`, that entry with a `big_value`-byte
