@@ -194,34 +194,53 @@ LDB_HD uint32_t field_value(uint32_t b, uint32_t n, bool* canon) {
   return pext7(b);
 }
 
+// Header-window bytes [b, b+4), b in [4, 31], from the window dwords w[0..8] (bytes 0..35):
+// win_word's select chain, four words further.
+LDB_HD uint32_t win_word9(const uint32_t* w, uint32_t b) {
+  const uint32_t d = b >> 2;
+  uint32_t lo = w[1], hi = w[2];
+#pragma unroll
+  for (uint32_t i = 2; i <= 7; ++i) {
+    lo = d >= i ? w[i] : lo;
+    hi = d >= i ? w[i + 1] : hi;
+  }
+  return funnel(hi, lo, b & 3u);
+}
+
+// The lean decode takes Go's whole varint range for ExpiredAt and TxID (up to 10 bytes each: a
+// snowflake TxID, tx.go:47-56, is a 9-10 byte varint), so Tx.Commit's entries stay on the lean path.
 LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   const int a = p + kPre;
   const int q = a & ~3;
   const uint32_t sh = (uint32_t)(a & 3);
-  uint32_t d[7];
+  uint32_t d[10];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) d[i] = lds32(v, q + 4 * i);
-  uint32_t w[6];
+  for (int i = 0; i < 10; ++i) d[i] = lds32(v, q + 4 * i);
+  uint32_t w[9];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) w[i] = funnel(d[i + 1], d[i], sh);
-  // terminator bits of window bytes 5..19 (bit i <-> byte 4 + i)
-  const uint32_t M = msb4(w[1]) | (msb4(w[2]) << 4) | (msb4(w[3]) << 8) | (msb4(w[4]) << 12);
-  uint32_t T = (~M) & 0xFFFEu;
-  const uint32_t e0 = ctz_or(T, 16); T &= T - 1;
-  const uint32_t e1 = ctz_or(T, 16); T &= T - 1;
-  const uint32_t e2 = ctz_or(T, 16); T &= T - 1;
-  const uint32_t e3 = ctz_or(T, 16); T &= T - 1;
-  const uint32_t e4 = ctz_or(T, 16);
+  for (int i = 0; i < 9; ++i) w[i] = funnel(d[i + 1], d[i], sh);
+  // terminator bits of window bytes 5..35 (bit i <-> byte 4 + i)
+  const uint32_t M = msb4(w[1]) | (msb4(w[2]) << 4) | (msb4(w[3]) << 8) | (msb4(w[4]) << 12) | (msb4(w[5]) << 16) |
+                     (msb4(w[6]) << 20) | (msb4(w[7]) << 24) | (msb4(w[8]) << 28);
+  uint32_t T = (~M) & 0xFFFFFFFEu;
+  const uint32_t e0 = ctz_or(T, 32); T &= T - 1;
+  const uint32_t e1 = ctz_or(T, 32); T &= T - 1;
+  const uint32_t e2 = ctz_or(T, 32); T &= T - 1;
+  const uint32_t e3 = ctz_or(T, 32); T &= T - 1;
+  const uint32_t e4 = ctz_or(T, 32);
   // field lengths: expiredAt e0, txID e1-e0, txStat e2-e1 (== 1), kSize e3-e2, vSize e4-e3
-  bool ok = e4 < 16u && e0 <= 5u && e1 - e0 <= 5u && e2 - e1 == 1u && e3 - e2 <= 4u && e4 - e3 <= 4u;
+  bool ok = e4 < 32u && e0 <= 10u && e1 - e0 <= 10u && e2 - e1 == 1u && e3 - e2 <= 4u && e4 - e3 <= 4u;
   const uint32_t stat = w[1] & 0xFFu;
-  const uint32_t ts = win_word(w, 4 + e2) & 0xFFu;   // txStat byte: zz(0..2) = 0, 2, 4
+  const uint32_t ts = win_word9(w, (4 + e2) & 31u) & 0xFFu;   // txStat byte: zz(0..2) = 0, 2, 4
   ok = ok && stat <= 2u && (ts == 0u || ts == 2u || ts == 4u) && ((w[1] >> 8) & 1u) == 0u && w[0] != 0u;
-  // minimal expiredAt / txID encodings (EncodeEntry re-emits them as read only then)
-  ok = ok && (e0 == 1u || (win_word(w, 4 + e0) & 0xFFu) != 0u) && (e1 - e0 == 1u || (win_word(w, 4 + e1) & 0xFFu) != 0u);
+  // minimal expiredAt / txID encodings (EncodeEntry re-emits them as read only then); a 10-byte
+  // varint's last byte must be 0 or 1 (binary.Varint overflows past 64 bits: decodeHeader differs)
+  const uint32_t lb0 = win_word9(w, (4 + e0) & 31u) & 0xFFu, lb1 = win_word9(w, (4 + e1) & 31u) & 0xFFu;
+  ok = ok && (e0 == 1u || lb0 != 0u) && (e1 - e0 == 1u || lb1 != 0u) && (e0 < 10u || lb0 <= 1u) &&
+       (e1 - e0 < 10u || lb1 <= 1u);
   bool ck, cv;
-  const uint32_t uk = field_value(win_word(w, (5 + e2) & 31u), e3 - e2, &ck);
-  const uint32_t uv = field_value(win_word(w, (5 + e3) & 31u), e4 - e3, &cv);
+  const uint32_t uk = field_value(win_word9(w, (5 + e2) & 31u), e3 - e2, &ck);
+  const uint32_t uv = field_value(win_word9(w, (5 + e3) & 31u), e4 - e3, &cv);
   ok = ok && ck && cv && (uk & 1u) == 0u && uk >= 2u && (uv & 1u) == 0u;
   const uint32_t hs = 5 + e4;
   const uint32_t k = uk >> 1, vv = uv >> 1;

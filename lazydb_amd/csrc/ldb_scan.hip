@@ -923,9 +923,14 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
     return s;
   };
   // ---- 1. optimistic walkers
+  // One window of 64 consecutive flags per wave, its sources walked in order (a walker then starts
+  // from the exit an earlier walker of the same window may just have rewritten; handing the sources of
+  // one window to several waves measured 4-40x slower: walkers from stale exits walk garbage). Windows
+  // are dealt across the CUs first (wave-major), so a file with few windows still gets one CU each.
   uint32_t runs = 0;
-  for (uint64_t b = ((uint64_t)blockIdx.x * kRepWaves + wave) * 64; b < nflag;
-       b += (uint64_t)gridDim.x * kRepWaves * 64) {
+  const uint64_t nwave = (uint64_t)gridDim.x * kRepWaves;
+  for (uint64_t w = (uint64_t)wave * gridDim.x + blockIdx.x; w * 64 < nflag; w += nwave) {
+    const uint64_t b = w * 64;
     uint64_t m = __ballot(b + lane < nflag && fl[b + lane] != 0);
     while (m) {
       const int i = __builtin_ctzll(m);
@@ -1421,10 +1426,10 @@ int scan_main_grid(const ldb_ctx* c, uint64_t nreg) {
   return (int)std::min<uint64_t>((nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * per_cu);
 }
 
-// k_repair's workgroups: one wave per 64 flags, at most one workgroup per CU (they exit at once when
-// k_link found no broken link)
+// k_repair's workgroups: one per CU (fewer for tiny files; they exit at once when k_link found no
+// broken link), so the walkers of a file with many failures spread over the whole chip
 int repair_grid(const ldb_ctx* c, uint64_t nreg) {
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>((nreg + 1 + 64 * kRepWaves - 1) / (64 * kRepWaves), (uint64_t)c->n_cu));
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((nreg + 1 + 63) / 64, (uint64_t)c->n_cu));
 }
 
 int uniform_grid(const ldb_ctx* c, uint64_t bytes) {

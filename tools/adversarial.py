@@ -5,6 +5,7 @@ cut at the oracle's end_off and tiled to --mib MiB, so the log is one valid chai
   embedded  values holding complete valid entries and zero runs (speculative resyncs land inside values)
   binary    random binary keys/values (random bytes that decode as plausible headers)
   mixed     every header field varied, keys/values 0..300 B
+  txlog     Tx.Commit entries: snowflake TxIDs (10-byte varints), TxStat 1, 1-16 entries per tx
   tiny      1-byte keys, empty values (11-B entries: the densest regions)
   big       64 KiB-scale values (regions fully inside one value)
 Every case is checked against the C oracle (status, end_off, n_entries, tuples) before it is timed.
@@ -37,6 +38,19 @@ def block(case: str) -> np.ndarray:
         raw = MG.mixed(23, 1 << 20)
     elif case == "big":
         raw = MG.big_values(24, 4 << 20)
+    elif case == "txlog":   # Tx.Commit writes (tx.go:156-206): snowflake TxIDs (10-byte varints), TxStat 1
+        import random
+        rng = random.Random(25)
+        parts, used, ms = [], 0, 1_700_000_000_000
+        while used < (1 << 20):
+            ms += rng.randrange(1, 50)
+            tx = (ms << 22) | (rng.randrange(1023) << 12) | rng.randrange(4096)
+            for _ in range(rng.randrange(1, 17)):
+                e = MG.ent(key=MG.alpha(rng, rng.randrange(16, 65)), value=MG.alpha(rng, rng.randrange(32, 513)),
+                           tx_id=tx, tx_stat=1, expired_at=rng.choice([0] * 9 + [1_700_000_000 + rng.randrange(10**6)]))
+                parts.append(e)
+                used += len(e)
+        raw = b"".join(parts)
     elif case == "tiny":
         e = MG.ent(key=b"k", value=b"")
         raw = e * ((1 << 20) // len(e))
@@ -51,7 +65,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--cases", default="embedded,binary,mixed,tiny,big")
+    ap.add_argument("--cases", default="embedded,binary,mixed,txlog,tiny,big")
     args = ap.parse_args()
     import torch
     from lazydb_amd import Engine
