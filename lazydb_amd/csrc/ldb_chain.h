@@ -194,19 +194,6 @@ LDB_HD uint32_t field_value(uint32_t b, uint32_t n, bool* canon) {
   return pext7(b);
 }
 
-// Header-window bytes [b, b+4), b in [4, 31], from the window dwords w[0..8] (bytes 0..35):
-// win_word's select chain, four words further.
-LDB_HD uint32_t win_word9(const uint32_t* w, uint32_t b) {
-  const uint32_t d = b >> 2;
-  uint32_t lo = w[1], hi = w[2];
-#pragma unroll
-  for (uint32_t i = 2; i <= 7; ++i) {
-    lo = d >= i ? w[i] : lo;
-    hi = d >= i ? w[i + 1] : hi;
-  }
-  return funnel(hi, lo, b & 3u);
-}
-
 // The lean decode takes Go's whole varint range for ExpiredAt and TxID (up to 10 bytes each: a
 // snowflake TxID, tx.go:47-56, is a 9-10 byte varint), so Tx.Commit's entries stay on the lean path.
 LDB_HD bool decode_lean(const View& v, int p, Lean* o) {

@@ -330,9 +330,22 @@ LDB_HD uint64_t pack_hot(uint64_t off, const Hot& h) {
          ((uint64_t)(h.stat & 0xFF) << 52);
 }
 
-// Fast decode at region-relative p for headers whose five varints end within bytes [5, 20)
-// with ts/k/v varints <= 4 bytes and expiredAt/txID <= 5 bytes (every header LazyDB's writer
-// emits for sizes < 128 MiB). Everything else, and every status other than kCont, goes through
+// Header-window bytes [b, b+4), b in [4, 31], from the window dwords w[0..8] (bytes 0..35):
+// win_word's select chain, four words further.
+LDB_HD uint32_t win_word9(const uint32_t* w, uint32_t b) {
+  const uint32_t d = b >> 2;
+  uint32_t lo = w[1], hi = w[2];
+#pragma unroll
+  for (uint32_t i = 2; i <= 7; ++i) {
+    lo = d >= i ? w[i] : lo;
+    hi = d >= i ? w[i + 1] : hi;
+  }
+  return funnel(hi, lo, b & 3u);
+}
+
+// Fast decode at region-relative p for headers whose five varints end within bytes [5, 36)
+// with ts/k/v varints <= 4 bytes and expiredAt/txID <= 10 bytes (every header LazyDB's writer
+// emits for sizes < 128 MiB, snowflake TxIDs included). Everything else, and every status other than kCont, goes through
 // the exact byte-wise decoder (classify_entry, Go semantics).
 // Returns false when the fast path cannot decide (the caller falls back to the exact decoder).
 LDB_HD bool classify_fast(const View& v, int p, Hot* out) {
@@ -347,23 +360,24 @@ LDB_HD bool classify_fast(const View& v, int p, Hot* out) {
     const int a = p + kPre;
     const int q = a & ~3;
     const uint32_t sh = (uint32_t)(a & 3);
-    uint32_t d[7];
+    uint32_t d[10];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) d[i] = lds32(v, q + 4 * i);
-    uint32_t w[6];
+    for (int i = 0; i < 10; ++i) d[i] = lds32(v, q + 4 * i);
+    uint32_t w[9];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) w[i] = funnel(d[i + 1], d[i], sh);
-    // terminator bits (bit i <-> window byte 4 + i), bytes 5..19
-    const uint32_t M = msb4(w[1]) | (msb4(w[2]) << 4) | (msb4(w[3]) << 8) | (msb4(w[4]) << 12);
-    uint32_t T = (~M) & 0xFFFEu;
+    for (int i = 0; i < 9; ++i) w[i] = funnel(d[i + 1], d[i], sh);
+    // terminator bits (bit i <-> window byte 4 + i), bytes 5..35
+    const uint32_t M = msb4(w[1]) | (msb4(w[2]) << 4) | (msb4(w[3]) << 8) | (msb4(w[4]) << 12) | (msb4(w[5]) << 16) |
+                       (msb4(w[6]) << 20) | (msb4(w[7]) << 24) | (msb4(w[8]) << 28);
+    uint32_t T = (~M) & 0xFFFFFFFEu;
     uint32_t e[5];
     uint32_t prev = 0;
     bool fast = true;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
-      e[f] = T ? (uint32_t)__builtin_ctz(T) : 16u;
+      e[f] = T ? (uint32_t)__builtin_ctz(T) : 32u;
       T &= T - 1;
-      fast = fast && e[f] < 16u && e[f] - prev <= (f < 2 ? 5u : 4u);
+      fast = fast && e[f] < 32u && e[f] - prev <= (f < 2 ? 10u : 4u);
       prev = e[f];
     }
     if (fast) {
@@ -372,21 +386,13 @@ LDB_HD bool classify_fast(const View& v, int p, Hot* out) {
       bool canon = true;
 #pragma unroll
       for (int f = 0; f < 5; ++f) {
-        const uint32_t st = 5 + pe;               // first byte of the field (window index, 5..19)
+        const uint32_t st = 5 + pe;               // first byte of the field (window index, 5..31)
         const uint32_t n = e[f] - pe;
-        const uint32_t di = st >> 2, bs = st & 3;
-        const uint32_t lo = di == 1 ? w[1] : di == 2 ? w[2] : di == 3 ? w[3] : w[4];
-        const uint32_t hi = di == 1 ? w[2] : di == 2 ? w[3] : di == 3 ? w[4] : w[5];
-        uint32_t b = funnel(hi, lo, bs);
+        uint32_t b = win_word9(w, st & 31u);
         const uint32_t nn = n > 4 ? 4 : n;
-        uint32_t lastb;
-        if (n > 4) {  // 5-byte expiredAt / txID: its last byte is window byte 4 + e[f]
-          const uint32_t li = 4 + e[f];
-          lastb = (((li >> 2) == 2 ? w[2] : w[3]) >> (8 * (li & 3))) & 0xFFu;
-        } else {
-          lastb = (b >> (8 * (nn - 1))) & 0xFFu;
-        }
-        canon = canon && (n == 1 || lastb != 0);
+        // the field's last byte: window byte 4 + e[f] (expiredAt / txID may be up to 10 bytes)
+        const uint32_t lastb = n > 4 ? (win_word9(w, (4 + e[f]) & 31u) & 0xFFu) : ((b >> (8 * (nn - 1))) & 0xFFu);
+        canon = canon && (n == 1 || lastb != 0) && (n < 10 || lastb <= 1u);   // 10 bytes: no uint64 overflow
         if (f == 0) sign0 = b & 1u;
         if (f >= 2) {
           b &= nn == 4 ? 0xFFFFFFFFu : ((1u << (8 * nn)) - 1);

@@ -888,6 +888,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
   uint8_t* fl = fail_flags(p);
   uint32_t* claims = repair_claims(p);
   const uint64_t nflag = n_fail_flags(p);
+  bool serial_phase = false;
   auto run = [&](uint64_t r, uint32_t enter) -> RegionSum {
     const uint64_t R0 = r * (uint64_t)kW;
     // synchronous staging through registers
@@ -915,10 +916,13 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
     const RegionSum s = wl->rs;
     if (lane == 0) {
       store_region(p, r, s);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      // the serial repair reads its own summaries back coherently; a walker's reads are hints only,
+      // and an agent-scope fence per region (an L2 writeback and invalidate on gfx950) cost ~1 ms a
+      // region with many walkers writing: phase 1 fences once, before the done count
+      if (serial_phase) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (serial_phase) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     GpuWave::sync();
     return s;
   };
@@ -935,7 +939,11 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
     while (m) {
       const int i = __builtin_ctzll(m);
       m &= m - 1;
-      runs += walk_source(p, rf - 1 + (int64_t)(b + i), rd,
+      // a source region another walker has claimed is being rewritten: its exit is stale, and that
+      // walker's walk continues through it anyway
+      const int64_t src = rf - 1 + (int64_t)(b + i);
+      if (src >= rf && __hip_atomic_load(&claims[src], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) continue;
+      runs += walk_source(p, src, rd,
                           [&](uint64_t r) {   // wave-uniform: lane 0 claims, the wave follows
                             uint32_t won = 0;
                             if (lane == 0) won = atomicCAS(&claims[r], 0u, 1u) == 0u ? 1u : 0u;
@@ -946,9 +954,12 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
   }
   if (lane == 0 && runs) atomicAdd(&p.ctr[2], runs);
   // ---- 2. the last workgroup: links again, then the serial repair
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&p.ctr[6], 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) {   // the workgroup's summaries and tuples, released once
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_last = atomicAdd(&p.ctr[6], 1u) == gridDim.x - 1;
+  }
   __syncthreads();
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -968,6 +979,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (wave != 0 || __hip_atomic_load(&p.ctr[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  serial_phase = true;
   auto next_fail = [&](int64_t done) -> int64_t {   // smallest flagged source > done
     for (uint64_t b = (uint64_t)(done - (rf - 1) + 1); b < nflag; b += 64) {
       const uint64_t m = __ballot(b + lane < nflag && fl[b + lane] != 0);
