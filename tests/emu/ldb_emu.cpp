@@ -329,9 +329,13 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
     // LDB_EMU_WALKERS: "0" none (the serial repair alone), "rev" in reverse flag order (each walker
     // reads its source before an earlier walker rewrites it: stale starting points, lost claims)
     const char* wm = getenv("LDB_EMU_WALKERS");
-    const bool walk = !(wm && wm[0] == '0'), rev = wm && wm[0] == 'r';
+    // "win": windows of 64 flags in reverse order, each in flag order (GPU waves running windows
+    // concurrently, the later one first)
+    const bool walk = !(wm && wm[0] == '0'), rev = wm && wm[0] == 'r', win = wm && wm[0] == 'w';
+    const uint64_t nwin = (nflag + 63) / 64;
     for (uint64_t j = 0; walk && j < nflag; ++j) {
-      const uint64_t i = rev ? nflag - 1 - j : j;
+      const uint64_t i = rev ? nflag - 1 - j : win ? (nwin - 1 - j / 64) * 64 + j % 64 : j;
+      if (i >= nflag) continue;
       if (fl[i])
         walker_runs += walk_source(p, (int64_t)rf - 1 + (int64_t)i, Rd{&p},
                                    [&](uint64_t r) { return claims[r]++ == 0; }, run);
