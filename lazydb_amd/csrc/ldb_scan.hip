@@ -943,6 +943,10 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
       // walker's walk continues through it anyway
       const int64_t src = rf - 1 + (int64_t)(b + i);
       if (src >= rf && __hip_atomic_load(&claims[src], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) continue;
+      // the window's first source whose own region's incoming link is broken too: the previous
+      // window's wave walks through it from the true side; walking from its stale exit meanwhile
+      // writes off-chain regions the serial pass must then re-run one by one (binary values)
+      if (i == 0 && b > 0 && fl[b - 1] != 0) continue;
       runs += walk_source(p, src, rd,
                           [&](uint64_t r) {   // wave-uniform: lane 0 claims, the wave follows
                             uint32_t won = 0;

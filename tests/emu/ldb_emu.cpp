@@ -336,6 +336,7 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
     for (uint64_t j = 0; walk && j < nflag; ++j) {
       const uint64_t i = rev ? nflag - 1 - j : win ? (nwin - 1 - j / 64) * 64 + j % 64 : j;
       if (i >= nflag) continue;
+      if (i % 64 == 0 && i > 0 && fl[i - 1]) continue;   // as k_repair: left to the previous window's walker
       if (fl[i])
         walker_runs += walk_source(p, (int64_t)rf - 1 + (int64_t)i, Rd{&p},
                                    [&](uint64_t r) { return claims[r]++ == 0; }, run);
