@@ -167,6 +167,10 @@ int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg
  * its own: avg_run_ms; avg_main_ms is then the region pipeline's main kernel after it. */
 int ldb_kernel_timing_split(ldb_ctx* ctx, int enable, double* avg_run_ms, double* avg_main_ms, double* avg_total_ms,
                             uint64_t* n);
+/* The run prefix's tuple fill (k_uniform_fill: the run's INDEX tuples written as one dense sweep after
+ * k_uniform verified them) over the same launches: avg_fill_ms. Query only; the reset is
+ * ldb_kernel_timing's / ldb_kernel_timing_split's. */
+int ldb_kernel_timing_fill(ldb_ctx* ctx, double* avg_fill_ms);
 
 /* Practical HBM-read ceiling for the roofline report: a read-only XOR
  * reduction over the device image d_image[0, len), 16-B loads, `iters` timed launches after one

@@ -216,7 +216,11 @@ constexpr uint32_t kDrop = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)(uintptr_t)base;   // wave-uniform
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
+  // every field through readfirstlane: a descriptor the compiler thinks divergent becomes a waterfall
+  // loop around every buffer load (k_uniform: 1.21 ms against 0.80 when a divergent loop exit made
+  // the batch index, and with it the descriptor, look divergent)
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t x, uint32_t y, uint32_t z,
                                         uint32_t w) {
@@ -290,7 +294,44 @@ struct UniSetup {
   UniGeo g;
 };
 constexpr uint64_t kUniTabWords = kUniLevels * 1024;   // combine tables in LDS
-static_assert(kTBOff == 0, "k_uniform stages the S table at LDS word 0");
+
+// The run prefix's CRC (round 3): 2-byte slicing on LANE-PRIVATE byte tables, so a wave's table reads
+// never bank-conflict. Row i of the 64 KiB block is 256 B: dwords [0, 32) hold T16[i] = the register
+// after byte i and one zero byte, dwords [32, 64) hold T8[i] = after byte i alone, each replicated
+// once per bank; lane l reads dword l mod 32 of a half, so the 32 lanes of a ds_read_b32 group always
+// hit 32 distinct banks (MI355X_MICROARCH.md LDS: ds_read_b32 serves lanes {0-31}, {32-63}, bank
+// (a/4) mod 32). The address (byte << 8 | 4 (l mod 32)) is one v_perm_b32 and the xors v_bitop3.
+// Against the 11/11/10-bit shared tables (round 2: 60 % of LDS-active cycles were conflict cycles at
+// config 4) one lookup per byte instead of 0.75, all conflict-free (tools/microbench/mb_uni.hip:
+// config 4 verify 0.794 -> 0.724 ms on one box, within 1 % of the same loads XOR-reduced).
+constexpr uint32_t kLp2Bytes = 65536;
+__device__ __forceinline__ uint32_t lp2_read(const uint8_t* lp2, uint32_t a) {
+  return *reinterpret_cast<const uint32_t*>(lp2 + a);
+}
+__device__ __forceinline__ uint32_t lp2_xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// reg' after the 4 message bytes of w (little-endian, first byte lowest), raw register (no init/final)
+__device__ __forceinline__ uint32_t lp2_step4(const uint8_t* lp2, uint32_t lb, uint32_t reg, uint32_t w) {
+  const uint32_t x = reg ^ w;
+  const uint32_t y = lp2_xor3(x >> 16, lp2_read(lp2, __builtin_amdgcn_perm(x, lb, 0x0C0C0400u)),
+                              lp2_read(lp2, __builtin_amdgcn_perm(x, lb, 0x0C0C0500u) + 128u));
+  return lp2_xor3(y >> 16, lp2_read(lp2, __builtin_amdgcn_perm(y, lb, 0x0C0C0400u)),
+                  lp2_read(lp2, __builtin_amdgcn_perm(y, lb, 0x0C0C0500u) + 128u));
+}
+// the block from the byte table T8 (the table block's kT8Off): T16[i] = T8[T8[i] & 0xFF] ^ (T8[i] >> 8);
+// every thread of the workgroup writes 4 x 16 B (1024 threads: one quarter row each)
+__device__ __forceinline__ void lp2_build(uint8_t* lp2, const uint32_t* __restrict__ gtab) {
+  const uint32_t* t8 = gtab + kT8Off;
+  for (uint32_t q = threadIdx.x; q < 1024u; q += blockDim.x) {
+    const uint32_t row = q >> 2, part = q & 3u;
+    const uint32_t a = t8[row];
+    const uint32_t v = part < 2 ? (t8[a & 0xFFu] ^ (a >> 8)) : a;
+    uint4* d = reinterpret_cast<uint4*>(lp2 + row * 256u + part * 64u);
+    const uint4 vv = make_uint4(v, v, v, v);
+    d[0] = vv; d[1] = vv; d[2] = vv; d[3] = vv;
+  }
+}
 #ifndef LDB_UNI_NT
 // 1: k_uniform's row loads carry the non-temporal hint (cache policy bit 1 = "nt" on gfx950). Off: a
 // wave's 6-7 row instructions re-touch the same lines, and nt lines are evicted between them (config
@@ -405,9 +446,14 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 
 // One wave's share of the run prefix, S steps per lane (a compile-time count: the rows stay in
 // registers with static indices and the step loop has no per-step branch).
-template <int S, bool kChunk, bool kHash>
-__device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint32_t* stab, int lane, int wave,
-                                          uint64_t a_lo, uint64_t a_hi) {
+// kFill: the tuples of INDEX-kind scans are written afterwards by k_uniform_fill as one dense sweep, so
+// the verify loop carries no store at all (a per-batch tuple store in the loop cost 0.10-0.21 ms per
+// 4 GiB even into an L2-resident ring: the wave's next row loads then wait on the store's completion;
+// tools/microbench/mb_uni.hip wr_W1, st_S1..S6). ENTRY-kind tuples (per-entry crc) and the merge's key
+// hashes are still stored in the loop.
+template <int S, bool kChunk, bool kHash, bool kFill>
+__device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint8_t* lp2, const uint32_t* T,
+                                          int lane, int wave, uint64_t a_lo, uint64_t a_hi) {
   if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
     a_lo = 0;
     a_hi = p.len;
@@ -426,12 +472,26 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
   const uint32_t j = (uint32_t)lane & (G - 1);
   const bool last = j == G - 1;
   const uint32_t lead0 = uni_lead(su.g, j);   // bytes lane j masks at its window's start
-  const uint32_t* T = stab + 5120;
+  const uint32_t lb = ((uint32_t)lane & 31u) * 4u;   // this lane's bank in the LP2 rows
+  const uint32_t nw = su.m.nw, hrows = (nw + 2 + 3) / 4;
+  const bool fill = kFill && p.kind == LDB_TUPLE_INDEX;
   GpuWave wp{lane};
   const uint64_t nbatch = kChunk ? ~0ull : (p.len / sz + E) / E;   // !kChunk: ceil(ncand / E), ncand = len / sz + 1
+  // K as last seen: the load issued in one batch is tested at the top of the next, so its latency hides
+  // behind the batch (a batch past K only costs its own time: the run's tuples stop at K anyway)
+  uint64_t kseen = ~0ull;
   for (uint64_t b = b_first + (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
     if (kChunk && b * Esz > (all_hi ? p.len : a_hi)) break;   // wave-uniform: no candidate of this launch from here on
-    if (b * E >= __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    if (b * E >= kseen) break;
+#ifdef LDB_UNI_NOK   // A/B only: no per-batch look at K
+    const uint64_t knext = ~0ull;
+#else
+    uint64_t knext = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // uniform by construction (one address), but an atomic's result is divergent to the compiler: the
+    // loop exit on it would make b, and every descriptor built from b, divergent
+    knext = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(knext >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)knext);
+#endif
     // Opaque per-batch copies: the uniform step / level conditions and the lane masks derived from
     // them are evaluated inside the batch, not hoisted out of the loop as a bank of held SGPR masks.
     uint32_t tt = __builtin_amdgcn_readfirstlane(t), GG = __builtin_amdgcn_readfirstlane(G), c = ~j & (j + 1), lead = lead0;
@@ -445,8 +505,23 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)min(nrec, (uint64_t)0xFFFFFFFFu));
     // the group's last lane: the header (stored crc and bytes [4, 40)), in flight with the rows
     const uint32_t hx = (uint32_t)(x - base), ha = hx & ~3u, hsh = hx & 3u;
+    // the header rows the check reads: dwords [0, nw + 2) from ha (the stored crc, nw template words and
+    // the funnel's next dword), so 1 row for LazyDB's 10-13-byte Set headers, 3 at most (wave-uniform)
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-    if (last) { h0 = ld16(rs, ha); h1 = ld16(rs, ha + 16); h2 = ld16(rs, ha + 32); }
+#ifdef LDB_UNI_NOHDR   // A/B only (results wrong): no header rows
+    if (false) {
+#else
+    if (last) {
+#endif
+      h0 = ld16(rs, ha);
+#ifdef LDB_UNI_HDR3   // A/B: the round-2 form, every header row
+      h1 = ld16(rs, ha + 16);
+      h2 = ld16(rs, ha + 32);
+#else
+      if (hrows > 1) h1 = ld16(rs, ha + 16);
+      if (hrows > 2) h2 = ld16(rs, ha + 32);
+#endif
+    }
     const int32_t ws = (int32_t)hx + 4 - (int32_t)t + (int32_t)(j * P);   // < 0 only when base = 0
     const uint32_t a = (uint32_t)ws & ~3u, sh = (uint32_t)ws & 3u;
     uint32_t d[4 * R];
@@ -473,12 +548,19 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
         d[i] = ld4(rs, o < 0 ? kDrop : (uint32_t)o);
       }
     }
+    // every row (and header) load in flight before the first use: left alone, the scheduler trades them
+    // for registers and issues them one step ahead of the CRC (3 in flight: 1.26 vs 0.82 ms, mb_uni.hip)
+    __builtin_amdgcn_sched_barrier(0);
     // lane j's window: S steps from register 0, lane 0's first t bytes masked
     uint32_t reg = 0;
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       uint32_t w0 = funnel(d[2 * k + 1], d[2 * k], sh), w1 = funnel(d[2 * k + 2], d[2 * k + 1], sh);
+#ifdef LDB_UNI_NOMASK   // A/B only (results wrong): no lead masks
+      if (false) {
+#else
       if ((uint32_t)(8 * k) < tt) {   // wave-uniform
+#endif
         // masked bytes from this step's start (lane 0 only): keep bytes >= n of the 8. The opaque
         // copy keeps the compiler from hoisting every step's mask out of the batch loop.
         uint32_t ld = lead;
@@ -488,15 +570,17 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
         w1 &= n >= 8 ? 0u : (n > 4 ? 0xFFFFFFFFu << (8 * (n - 4)) : 0xFFFFFFFFu);
       }
       if (LDB_UNI_ABL == 1 || LDB_UNI_ABL == 3) reg ^= w0 ^ w1;
-      else reg = crc_step8(stab, reg, w0, w1);
+      else reg = lp2_step4(lp2, lb, lp2_step4(lp2, lb, reg, w0), w1);
     }
     if (LDB_UNI_ABL) asm volatile("" ::"v"(reg));
+#ifndef LDB_UNI_NOCOMB   // A/B only (results wrong): no combine
     uni_level<1>(wp, T, GG, c, reg);
     uni_level<2>(wp, T + 1024, GG, c, reg);
     uni_level<4>(wp, T + 2048, GG, c, reg);
     uni_level<8>(wp, T + 3072, GG, c, reg);
     uni_level<16>(wp, T + 4096, GG, c, reg);
     uni_level<32>(wp, T + 5120, GG, c, reg);
+#endif
     // the header: bytes [4, hs) against the memo's (uni_header_ok). The memo is read from LDS through
     // an opaque offset, so its words stay per-batch VGPR loads instead of SGPRs held across the loop.
     bool ok = false;
@@ -522,13 +606,18 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
       else ok = ok && crc != 0u;   // crc == 0 && kSize == 0 && vSize == 0: ErrLogEndOfFile
       uint32_t diff = 0;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) diff |= (funnel(hd[i + 2], hd[i + 1], hsh) ^ mv->w[i]) & mv->msk[i];
+      for (int i = 0; i < 9; ++i)
+        if ((uint32_t)i < nw) diff |= (funnel(hd[i + 2], hd[i + 1], hsh) ^ mv->w[i]) & mv->msk[i];   // wave-uniform
       ok = ok && diff == 0u && ((reg ^ KL) == ~crc || LDB_UNI_ABL);   // getEntryCrc == stored crc (log_file.go:141-143)
     }
+#ifdef LDB_UNI_OKALL   // A/B only (results wrong): every candidate accepted, K untouched
+    ok = true;
+#endif
     const uint64_t bad = __ballot((last && mine && !ok) ? 1 : 0);
     if (bad && lane == 0)
       atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
-    if (ok && e < p.cap) {
+    kseen = knext;
+    if (ok && e < p.cap && !fill) {
       uint32_t z = 0;
       asm volatile("" : "+v"(z));
       const UniMemo& m = *(&su.m + z);
@@ -568,21 +657,20 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
 
 // kChunk: a_lo, a_hi: image bytes [0, a_hi) are in place; candidates not already taken by a launch
 // with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
+// LDS: the 64 KiB LP2 block, the combine tables and the setup (~90 KiB): one workgroup of 16 waves per
+// CU, 4 waves per SIMD, up to 128 VGPRs.
 template <bool kChunk, bool kHash>
 __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_lo, uint64_t a_hi) {
-  __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + kUniTabWords];   // S table, combine tables
+  __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
+  __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];   // combine tables (shift by 2^i P bytes)
   __shared__ UniSetup su;
-  if (!uni_prepare(p, su, stab + 5120)) return;
-  {
-    const uint4* g = reinterpret_cast<const uint4*>(p.gtab);
-    uint4* t = reinterpret_cast<uint4*>(stab);
-    for (int i = threadIdx.x; i < 5120 / 4; i += blockDim.x) t[i] = g[i];
-  }
+  lp2_build(lp2, p.gtab);
+  if (!uni_prepare(p, su, comb)) return;   // (its __syncthreads also publish the LP2 block)
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n) case n: uni_waves<n, kChunk, kHash>(p, su, stab, lane, wave, a_lo, a_hi); break;
+#define LDB_UNI_CASE(n) case n: uni_waves<n, kChunk, kHash, !kHash>(p, su, lp2, comb, lane, wave, a_lo, a_hi); break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
 #undef LDB_UNI_CASE
@@ -591,10 +679,33 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
 }
 static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
 
+// The run's INDEX tuples as one dense sweep after k_uniform (kFill): entry e < K (and < cap) at x = e sz
+// gets {uni_pos(memo, x), k, v}. A chunked scan fills per chunk, the entries that launch's k_uniform
+// took (the same byte predicate); every one of them below the K seen now was verified by that launch
+// (a later chunk only lowers K past its own entries).
+template <bool kChunk>
+__global__ __launch_bounds__(256) void k_uniform_fill(Pipe p, uint64_t a_lo, uint64_t a_hi) {
+  if (p.kind != LDB_TUPLE_INDEX || p.dyn[2] != kUniReady) return;
+  const UniSetup* gsu = reinterpret_cast<const UniSetup*>(p.uni);
+  if (!gsu->g.ok) return;
+  const UniMemo m = gsu->m;
+  const uint64_t sz = m.sz, K = p.dyn[0];   // raw: ~0 while a chunked scan has seen no failure yet
+  uint64_t e_lo = 0, e_hi = K < p.cap ? K : p.cap;
+  if (kChunk) {   // entries whose bytes and 48 header bytes lie in [0, a_hi) but not in [0, a_lo)
+    const uint64_t need = sz > 48 ? sz : 48;
+    if (a_lo) e_lo = a_lo >= need ? (a_lo - need) / sz + 1 : 0;   // x + need > a_lo
+    if (a_hi < p.len) {
+      const uint64_t hi = a_hi >= need ? (a_hi - need) / sz + 1 : 0;   // x + need <= a_hi
+      e_hi = e_hi < hi ? e_hi : hi;
+    }
+  }
+  ldb_index_tuple* out = reinterpret_cast<ldb_index_tuple*>(p.out);
+  for (uint64_t e = e_lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e_hi; e += (uint64_t)gridDim.x * blockDim.x)
+    store_tuple(out + e, uni_pos(m, e * sz), m.k, m.v);
+}
 
 // a batched scan's run prefixes: grid.y = file. The Pipes travel as kernel arguments (not through
-// a device pointer like the other batched stages): kernarg loads stay re-loadable constants, so the
-// hot loop keeps k_uniform's register budget (8 waves per SIMD).
+// a device pointer like the other batched stages): kernarg loads stay re-loadable constants.
 constexpr int kUniBatch = 16;
 struct UniBatch {
   Pipe p[kUniBatch];
@@ -602,19 +713,16 @@ struct UniBatch {
 template <bool kHash>
 __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   const Pipe p = b.p[blockIdx.y];
-  __shared__ __attribute__((aligned(16))) uint32_t stab[5120 + kUniTabWords];   // S table, combine tables
+  __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
+  __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];
   __shared__ UniSetup su;
-  if (!uni_prepare(p, su, stab + 5120)) return;
-  {
-    const uint4* g = reinterpret_cast<const uint4*>(p.gtab);
-    uint4* t = reinterpret_cast<uint4*>(stab);
-    for (int i = threadIdx.x; i < 5120 / 4; i += blockDim.x) t[i] = g[i];
-  }
+  lp2_build(lp2, p.gtab);
+  if (!uni_prepare(p, su, comb)) return;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n) case n: uni_waves<n, false, kHash>(p, su, stab, lane, wave, 0, p.len); break;
+#define LDB_UNI_CASE(n) case n: uni_waves<n, false, kHash, false>(p, su, lp2, comb, lane, wave, 0, p.len); break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
 #undef LDB_UNI_CASE
@@ -1271,7 +1379,7 @@ struct ldb_ctx {
   bool ws_ev_live = false;
   // kernel timing: one event triple per timed launch, recorded without host synchronisation and
   // resolved when the timing is queried (or when the pool is full)
-  struct EvTriple { hipEvent_t e0, eu, e1, e2; };   // start, after k_uniform, after k_scan_main, end
+  struct EvTriple { hipEvent_t e0, eu, ef, e1, e2; };   // start, after k_uniform, after its fill, after k_scan_main, end
   std::vector<EvTriple> evs;
   size_t ev_used = 0;
   bool timing = false;
@@ -1289,7 +1397,7 @@ struct ldb_ctx {
   int n_cp = 0;
   hipStream_t cp[kMaxCp] = {};
   std::vector<hipEvent_t> chunk_ev;
-  double t_run = 0, t_main = 0, t_total = 0;
+  double t_run = 0, t_fill = 0, t_main = 0, t_total = 0;
   uint64_t t_n = 0;
   // batched scans (enqueue_scan_batch): page-locked staging of the per-file Pipes, reused once the
   // copy of the previous batch has completed (pipes_ev)
@@ -1309,11 +1417,12 @@ static int resolve_timing(ldb_ctx* c) {
   for (size_t i = 0; i < c->ev_used; ++i) {
     const ldb_ctx::EvTriple& t = c->evs[i];
     if (hipEventSynchronize(t.e2) != hipSuccess) return LDB_ERR_HIP;
-    float u = 0, a = 0, b = 0;
-    if (hipEventElapsedTime(&u, t.e0, t.eu) != hipSuccess || hipEventElapsedTime(&a, t.eu, t.e1) != hipSuccess ||
-        hipEventElapsedTime(&b, t.e0, t.e2) != hipSuccess)
+    float u = 0, f = 0, a = 0, b = 0;
+    if (hipEventElapsedTime(&u, t.e0, t.eu) != hipSuccess || hipEventElapsedTime(&f, t.eu, t.ef) != hipSuccess ||
+        hipEventElapsedTime(&a, t.ef, t.e1) != hipSuccess || hipEventElapsedTime(&b, t.e0, t.e2) != hipSuccess)
       return LDB_ERR_HIP;
     c->t_run += u;
+    c->t_fill += f;
     c->t_main += a;
     c->t_total += b;
     c->t_n += 1;
@@ -1420,6 +1529,7 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
       ldb_ctx::EvTriple t{};
       LDB_HIP(hipEventCreate(&t.e0));
       LDB_HIP(hipEventCreate(&t.eu));
+      LDB_HIP(hipEventCreate(&t.ef));
       LDB_HIP(hipEventCreate(&t.e1));
       LDB_HIP(hipEventCreate(&t.e2));
       c->evs.push_back(t);
@@ -1450,7 +1560,11 @@ int repair_grid(const ldb_ctx* c, uint64_t nreg) {
 
 int uniform_grid(const ldb_ctx* c, uint64_t bytes) {
   const uint64_t batches = bytes / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
-  return std::max(1, (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu * 2));
+  return std::max(1, (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu));
+}
+// k_uniform_fill: a dense sweep, 4 workgroups of 256 threads per CU
+int fill_grid(const ldb_ctx* c, uint64_t bytes) {
+  return std::max(1, (int)std::min<uint64_t>(bytes / 16 / 256 + 1, (uint64_t)c->n_cu * 4));
 }
 
 // An image that is still being copied in: bytes [0, avail[i]) are in place once ev[i] has fired
@@ -1509,19 +1623,29 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
       else
         hipLaunchKernelGGL((k_uniform<false, false>), dim3(ug), dim3(64 * kUniWaves), 0, s, p, lo, hi);
     };
-    if (chunked) {
+    if (chunked) {   // each chunk's run entries are filled as soon as that chunk is verified
       uint64_t lo = 0;
       for (int i = 0; i < plan->n; ++i) {
         LDB_HIP(hipStreamWaitEvent(s, plan->ev[i], 0));
         const uint64_t hi = i + 1 == plan->n ? len : std::min(plan->avail[i], len);
         launch(lo, hi);
+        if (kind == LDB_TUPLE_INDEX)
+          hipLaunchKernelGGL(k_uniform_fill<true>, dim3(fill_grid(c, hi - lo)), dim3(256), 0, s, p, lo, hi);
         lo = hi;
       }
+      if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+      if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     } else {
       launch(0, len);
+      if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+      if (kind == LDB_TUPLE_INDEX && !p.hash_out)
+        hipLaunchKernelGGL(k_uniform_fill<false>, dim3(fill_grid(c, len)), dim3(256), 0, s, p, 0, len);
+      if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
+  } else if (ev) {
+    LDB_HIP(hipEventRecord(ev->eu, s));
+    LDB_HIP(hipEventRecord(ev->ef, s));
   }
-  if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
   hipLaunchKernelGGL(k_scan_main<false>, dim3(scan_main_grid(c, L.nreg)), dim3(64 * kWPB), main_lds_bytes(), s, p, nullptr);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   const int g256 = (int)((L.nreg + 255) / 256);
@@ -1619,7 +1743,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   hipLaunchKernelGGL(k_batch_init, dim3(n), dim3(64), 0, s, d_pipes);
   // the run prefixes: the whole batch gets the workgroups one file's launch would (uniform_grid, 2
   // per CU at most), dealt evenly over its files (LDB_UNI_BATCH_BPC: workgroups per CU, A/B)
-  static const int bpc = getenv("LDB_UNI_BATCH_BPC") ? std::max(1, atoi(getenv("LDB_UNI_BATCH_BPC"))) : 2;
+  static const int bpc = getenv("LDB_UNI_BATCH_BPC") ? std::max(1, atoi(getenv("LDB_UNI_BATCH_BPC"))) : 1;
   for (int i0 = 0; i0 < nf; i0 += kUniBatch) {
     UniBatch ub{};
     const int m = std::min(kUniBatch, nf - i0);
@@ -1631,6 +1755,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
       hipLaunchKernelGGL(k_uniform_batch<false>, dim3(ugb, (unsigned)m), dim3(64 * kUniWaves), 0, s, ub);
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+  if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
   hipLaunchKernelGGL(k_scan_main<true>, dim3(mg, n), dim3(64 * kWPB), main_lds_bytes(), s, p0, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   hipLaunchKernelGGL(k_fallback<true>, dim3(c->n_cu, n), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p0, d_pipes);
@@ -1998,7 +2123,7 @@ int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_t
   if (n) *n = c->t_n;
   if (enable >= 0) {
     c->timing = enable != 0;
-    c->t_run = c->t_main = c->t_total = 0;
+    c->t_run = c->t_fill = c->t_main = c->t_total = 0;
     c->t_n = 0;
   }
   return LDB_OK;
@@ -2012,6 +2137,15 @@ int ldb_kernel_timing_split(ldb_ctx* c, int enable, double* avg_run_ms, double* 
   if (rc != LDB_OK) return rc;
   if (avg_run_ms) *avg_run_ms = c->t_n ? c->t_run / c->t_n : 0.0;
   return ldb_kernel_timing(c, enable, avg_main_ms, avg_total_ms, n);
+}
+
+int ldb_kernel_timing_fill(ldb_ctx* c, double* avg_fill_ms) {
+  if (!c || !avg_fill_ms) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  const int rc = resolve_timing(c);
+  if (rc != LDB_OK) return rc;
+  *avg_fill_ms = c->t_n ? c->t_fill / c->t_n : 0.0;
+  return LDB_OK;
 }
 
 }  // extern "C"

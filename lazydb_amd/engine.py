@@ -310,3 +310,9 @@ class Engine:
         N.check(N.lib().ldb_kernel_timing_split(self.ctx, enable, C.byref(u), C.byref(a), C.byref(b), C.byref(n)),
                 "timing_split")
         return u.value, a.value, b.value, n.value
+
+    def timing_fill(self) -> float:
+        """avg k_uniform_fill ms over the timed launches (query; reset with timing/timing_split)."""
+        f = C.c_double()
+        N.check(N.lib().ldb_kernel_timing_fill(self.ctx, C.byref(f)), "timing_fill")
+        return f.value

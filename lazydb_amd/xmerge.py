@@ -195,6 +195,9 @@ def owner_inputs(t, recv_recs, recv_keys, src_counts):
                               t.tensor(src_counts, dtype=t.int64, device=recs.device))
     q[:, 2] += kb[src]
     ord_ = (src.to(t.int64) << 32) | (q[:, 1] & 0xFFFFFFFF)
+    if keys is None or keys.numel() == 0:
+        # every received key is empty (pad16(0) = 0 bytes): the resolve still wants a key buffer
+        keys = t.zeros(16, dtype=t.uint8, device=recs.device)
     return q.view(t.uint8).view(-1), keys, ord_
 
 

@@ -119,6 +119,43 @@ def gen_log(cap_bytes: int, seed: int, ksize: int = 64, vsize: int = 256, value_
     return img, int(n), int(end.value)
 
 
+def gen_bench_log(cap_bytes: int = 512 << 20, seed: int = 1, n_entries: int = 500_000, vsize: int = 512,
+                  img: np.ndarray | None = None):
+    """The reference benchmark's log (bench/db_bench_test.go:17-36): n Sets of "bench_test_key_<i>" with
+    512-B alphabet values in one zero-preallocated file of cap_bytes (Mmap: MaxLogFileSize).
+    Returns (img, n, end_off)."""
+    L = lib()
+    if not hasattr(L.ldbo_gen_bench_log, "_typed"):
+        L.ldbo_gen_bench_log.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
+                                         C.POINTER(C.c_uint64)]
+        L.ldbo_gen_bench_log.restype = C.c_uint64
+        L.ldbo_gen_bench_log._typed = True
+    if img is None:
+        img = np.zeros(cap_bytes, dtype=np.uint8)
+    end = C.c_uint64(0)
+    n = L.ldbo_gen_bench_log(_ptr(img), cap_bytes, seed, n_entries, vsize, C.byref(end))
+    return img, int(n), int(end.value)
+
+
+def gen_writer_log(cap_bytes: int, seed: int, max_entries: int = (1 << 63), now: int = 1_760_000_000,
+                   key_space: int = 1_000_000, vmax: int = 4096, p_setex: int = 100, p_del: int = 100,
+                   p_tx: int = 100, img: np.ndarray | None = None):
+    """Writer-realistic string log (Set / SetEX / Delete / Tx.Commit interleaved, str.go, tx.go).
+    p_* in parts per 1000. Returns (img, n, end_off)."""
+    L = lib()
+    if not hasattr(L.ldbo_gen_writer_log, "_typed"):
+        L.ldbo_gen_writer_log.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, C.c_uint32,
+                                          C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]
+        L.ldbo_gen_writer_log.restype = C.c_uint64
+        L.ldbo_gen_writer_log._typed = True
+    if img is None:
+        img = np.zeros(cap_bytes, dtype=np.uint8)
+    end = C.c_uint64(0)
+    n = L.ldbo_gen_writer_log(_ptr(img), cap_bytes, seed, max_entries, now, key_space, vmax, p_setex, p_del, p_tx,
+                              C.byref(end))
+    return img, int(n), int(end.value)
+
+
 # ---------------------------------------------------------------- merge / GC (db.go:243-265, 383-427, 473-523)
 class MergeFile(C.Structure):
     _fields_ = [("d_image", C.c_void_p), ("len", C.c_uint64), ("fid", C.c_uint32), ("is_target", C.c_uint32)]

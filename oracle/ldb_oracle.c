@@ -37,6 +37,7 @@ static void crc_init_tables(void) {
  * Operates on the raw register like ldbo_crc32_reg; n >= 64, processes n & ~15 bytes. */
 #if defined(__x86_64__)
 #include <immintrin.h>
+#include <stdio.h>
 __attribute__((target("pclmul,sse4.1"))) static uint32_t crc_clmul(uint32_t crc, const uint8_t* buf, size_t len) {
   const __m128i k1k2 = _mm_set_epi64x(0x01c6e41596ll, 0x0154442bd4ll);
   const __m128i k3k4 = _mm_set_epi64x(0x00ccaa009ell, 0x01751997d0ll);
@@ -440,6 +441,82 @@ uint64_t ldbo_gen_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint32_t 
   free(key);
   free(val);
   free(cdf);
+  if (end_off) *end_off = off;
+  return n;
+}
+
+/* The reference benchmark's own log (bench/db_bench_test.go:17-36, configs[0]): n Sets of
+ * GetKey(i) = "bench_test_key_" + decimal i (16..21 bytes as i grows: the entry size changes at
+ * i = 10, 100, 1000, ...) and GetValue() = vsize bytes drawn from the 36-char alphabet (:15, :21-27;
+ * math/rand is time-seeded there, so the draws are splitmix64 here), each written by Set (str.go:22-33 ->
+ * writeLogEntry -> EncodeEntry, db.go:473-523) into one preallocated file of cap_bytes (the Mmap
+ * IOController truncates the file to MaxLogFileSize, iocontroller/mmap.go:17-30, so the bytes past the
+ * last entry are zero). Stops early when the file would roll over (db.go:485). */
+uint64_t ldbo_gen_bench_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint64_t n_entries, uint32_t vsize,
+                            uint64_t* end_off) {
+  static const char alpha[] = "abcdefghijklmnopqrstuvwxyz0123456789"; /* bench/db_bench_test.go:15 */
+  uint64_t st = seed, off = 0, n = 0;
+  uint8_t* val = (uint8_t*)malloc(vsize + 8);
+  char key[48];
+  for (; n < n_entries; ++n) {
+    int kl = snprintf(key, sizeof key, "bench_test_key_%llu", (unsigned long long)n); /* :17-19 */
+    for (uint32_t i = 0; i < vsize; i += 8) {
+      uint64_t r = ldbo_splitmix64(&st);
+      for (int b = 0; b < 8 && i + b < vsize; ++b) { val[i + b] = (uint8_t)alpha[(r & 0xff) % 36]; r >>= 8; }
+    }
+    uint64_t need = 5 + 3 + ldbo_varint_len(kl) + ldbo_varint_len(vsize) + (uint64_t)kl + vsize;
+    if (off + need > cap_bytes) break;
+    off += ldbo_encode_entry(0, 0, 0, 0, (const uint8_t*)key, (uint32_t)kl, val, vsize, img + off);
+  }
+  free(val);
+  if (end_off) *end_off = off;
+  return n;
+}
+
+/* A writer-realistic string-type log: what LazyDB's own write paths append, interleaved.
+ *   Set / MSet / Append        str.go:26, :200, :266        stat 0, ExpiredAt 0, TxID 0, TxStat 0
+ *   SetEX                      str.go:161-162               ExpiredAt = now + duration (Unix seconds)
+ *   Delete / GetDel            str.go:111, :136             Stat = SDelete, no value
+ *   Tx.Commit of a Tx.Set      tx_str.go:8-9, tx.go:157-160 TxStat = TxCommited (TxID stays 0: no write
+ *                                                           path sets it)
+ * Keys "user:" + decimal id (ids < key_space, so keys repeat as a live database's do); values of
+ * 8..vmax bytes, log-uniform; mix in parts per 1000: set, setex, del, tx (the rest: set). */
+uint64_t ldbo_gen_writer_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint64_t max_entries, int64_t now,
+                             uint32_t key_space, uint32_t vmax, uint32_t p_setex, uint32_t p_del, uint32_t p_tx,
+                             uint64_t* end_off) {
+  uint64_t st = seed, off = 0, n = 0;
+  uint8_t* val = (uint8_t*)malloc(vmax + 8);
+  char key[48];
+  double lmax = log((double)vmax / 8.0);
+  for (; n < max_entries; ++n) {
+    uint64_t r0 = ldbo_splitmix64(&st);
+    uint32_t kind = (uint32_t)(r0 % 1000);
+    uint32_t id = (uint32_t)((r0 >> 16) % key_space);
+    int kl = snprintf(key, sizeof key, "user:%u", id);
+    uint8_t stat = 0;
+    int64_t expa = 0;
+    uint16_t ts = 0;
+    uint32_t vl;
+    if (kind < p_del) {
+      stat = 1; vl = 0; /* SDelete */
+    } else {
+      double u = (double)(ldbo_splitmix64(&st) >> 11) * (1.0 / 9007199254740992.0);
+      vl = (uint32_t)(8.0 * exp(u * lmax));
+      if (vl < 8) vl = 8;
+      if (vl > vmax) vl = vmax;
+      if (kind < p_del + p_setex) expa = now + 1 + (int64_t)((r0 >> 40) % 86400); /* time.Now().Add(d).Unix() */
+      else if (kind < p_del + p_setex + p_tx) ts = 1;                             /* logfile.TxCommited */
+      for (uint32_t i = 0; i < vl; i += 8) {
+        uint64_t r = ldbo_splitmix64(&st);
+        memcpy(val + i, &r, 8);
+      }
+    }
+    uint64_t need = 5 + ldbo_varint_len(expa) + 1 + ldbo_varint_len(ts) + ldbo_varint_len(kl) + ldbo_varint_len(vl) +
+                    (uint64_t)kl + vl;
+    if (off + need > cap_bytes) break;
+    off += ldbo_encode_entry(stat, expa, 0, ts, (const uint8_t*)key, (uint32_t)kl, val, vl, img + off);
+  }
+  free(val);
   if (end_off) *end_off = off;
   return n;
 }

@@ -102,6 +102,11 @@ int ldbo_merge(int n_files, const ldb_merge_file* files, int io_type, uint32_t a
 
 /* Merge test set (config 5 shape): every key written twice (half the records stale), optional SDelete /
  * ExpiredAt mix, consecutive files of cap_bytes at imgs + f*cap_bytes. */
+uint64_t ldbo_gen_bench_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint64_t n_entries, uint32_t vsize,
+                            uint64_t* end_off);
+uint64_t ldbo_gen_writer_log(uint8_t* img, uint64_t cap_bytes, uint64_t seed, uint64_t max_entries, int64_t now,
+                             uint32_t key_space, uint32_t vmax, uint32_t p_setex, uint32_t p_del, uint32_t p_tx,
+                             uint64_t* end_off);
 uint64_t ldbo_gen_merge(uint8_t* imgs, uint32_t n_files, uint64_t cap_bytes, uint64_t n_records, uint64_t seed,
                         uint32_t ksize, uint32_t vsize, uint32_t p_delete_ppm, uint32_t p_expire_ppm, int64_t now,
                         uint64_t* end_offs);

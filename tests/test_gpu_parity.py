@@ -233,3 +233,39 @@ def test_run_prefix_capacity(eng):
     ref, rt = coracle.scan(img)
     assert res.status == -3 and res.n_entries == n and res.n_run == n
     assert np.array_equal(tup["pos"], rt["pos"][:1000])
+
+
+@pytest.mark.parametrize("io_type", [1, 0])
+def test_config1_reference_bench_log(eng, io_type):
+    """BASELINE config 1 at its stated size, in the reference benchmark's own shape
+    (bench/db_bench_test.go:17-36, :63-68): 500 K Sets of "bench_test_key_<i>" (16..21-B keys, so the
+    entry size changes at i = 10, 100, ..., 100000) with 512-B alphabet values, in one 512 MiB
+    preallocated file, scanned under the Mmap rule (IOType = 1: o + n >= len is EOF,
+    iocontroller/mmap.go:46-52) and under FileIO. Both tuple kinds, bit-exact."""
+    img, n, end = coracle.gen_bench_log(512 << 20, 11, n_entries=500_000)
+    assert n == 500_000 and end == 271_888_890
+    d = to_dev(img)
+    ref, rt = coracle.scan(img, io_type)
+    assert ref.status == 2 and ref.end_off == end and ref.n_entries == n
+    res, tup = eng.scan_dev(d, io_type=io_type, cap=n + 16)
+    assert_same(res, tup, ref, rt)
+    res1, tup1 = eng.scan_dev(d, io_type=io_type, cap=n + 16, kind=1)
+    ref1, rt1 = coracle.scan(img, io_type, tuple_kind=1)
+    assert_same(res1, tup1, ref1, rt1, kind=1)
+
+
+@pytest.mark.parametrize("io_type", [0, 1])
+def test_writer_realistic_mix(eng, io_type):
+    """What LazyDB's writers append, interleaved (str.go Set/SetEX/Delete, tx.go Commit): 64 MiB,
+    bit-exact under both IO rules, and with the file truncated mid-entry (EOF_KV / EOF_WINDOW)."""
+    img, n, end = coracle.gen_writer_log(64 << 20, 21)
+    d = to_dev(img)
+    res, tup = eng.scan_dev(d, io_type=io_type, cap=n + 16)
+    ref, rt = coracle.scan(img, io_type)
+    assert_same(res, tup, ref, rt)
+    assert res.n_entries == n
+    for cut in (end - 7, end - 300, end // 2 + 13):
+        part = np.ascontiguousarray(img[:cut])
+        res, tup = eng.scan_dev(to_dev(part), io_type=io_type, cap=n + 16)
+        ref, rt = coracle.scan(part, io_type)
+        assert_same(res, tup, ref, rt)
