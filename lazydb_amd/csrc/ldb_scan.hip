@@ -212,6 +212,8 @@ __device__ __forceinline__ void write_region_wave(const Pipe& p, uint64_t r, con
 // fixed number of them per region, so its counted vmcnt wait retires the next region's DMA
 // without waiting for the stores issued after it.
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+constexpr int kSc1 = 16;   // buffer cache-policy bit: sc1 (gfx940+: coherent past the CU's L1)
 constexpr uint32_t kDrop = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)(uintptr_t)base;   // wave-uniform
@@ -293,7 +295,12 @@ struct UniSetup {
   UniMemo m;
   UniGeo g;
 };
-constexpr uint64_t kUniTabWords = kUniLevels * 1024;   // combine tables in LDS
+// Combine tables in LDS (4 byte-indexed 256-word tables each = 1024 words): G <= kUniDirectG uses the
+// direct form, G - 1 tables "shift by d P bytes" (d = 1 .. G - 1); larger G the tree, lg tables
+// "shift by 2^i P bytes".
+constexpr uint32_t kUniDirectG = 8;
+constexpr uint64_t kUniTabWords = (kUniDirectG - 1 > kUniLevels ? kUniDirectG - 1 : kUniLevels) * 1024;
+LDB_HD inline uint32_t uni_ntab(const UniGeo& g) { return g.G <= kUniDirectG ? g.G - 1 : g.lg; }
 
 // The run prefix's CRC (round 3): 2-byte slicing on LANE-PRIVATE byte tables, so a wave's table reads
 // never bank-conflict. Row i of the 64 KiB block is 256 B: dwords [0, 32) hold T16[i] = the register
@@ -367,8 +374,8 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // scan: grid.y = file, its Pipe from the device array pb (enqueue_scan_batch).
 #define LDB_PIPE_SELECT const Pipe p = kB ? pb[blockIdx.y] : p0
 
-__device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
-  __shared__ uint32_t xn[kUniLevels];
+__device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
+  __shared__ uint32_t xn[kUniTabWords / 1024];
   __shared__ uint32_t win[2][16];   // bytes [0, 64) and [sz, sz + 64) of the image, zero past len
   __shared__ int published;
   UniSetup* gsu = reinterpret_cast<UniSetup*>(p.uni);
@@ -380,7 +387,7 @@ __device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
   __syncthreads();
   if (published) {
     if (!su.g.ok) return false;
-    for (uint32_t e = threadIdx.x; e < su.g.lg * 1024u; e += blockDim.x) T[e] = gT[e];
+    for (uint32_t e = threadIdx.x; e < uni_ntab(su.g) * 1024u; e += blockDim.x) T[e] = gT[e];
     return true;
   }
   auto stage = [&](int w, uint64_t at) {
@@ -409,7 +416,10 @@ __device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
       if (!uni_header_ok(su.m, word, su.m.sz, p.len, p.io)) su.g.ok = 0;
     }
     if (su.g.ok) {
-      for (uint32_t i = 0; i < su.g.lg; ++i) xn[i] = p.xw[su.g.P << i];
+      if (su.g.G <= kUniDirectG)
+        for (uint32_t d = 1; d < su.g.G; ++d) xn[d - 1] = p.xw[d * su.g.P];   // d P <= 7 * 96 < kW
+      else
+        for (uint32_t i = 0; i < su.g.lg; ++i) xn[i] = p.xw[su.g.P << i];
       if (blockIdx.x == 0) p.dyn[1] = su.m.sz;
     } else if (blockIdx.x == 0) {
       p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
@@ -417,7 +427,7 @@ __device__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
   }
   __syncthreads();
   if (su.g.ok)
-    for (uint32_t e = threadIdx.x; e < su.g.lg * 1024u; e += blockDim.x) {
+    for (uint32_t e = threadIdx.x; e < uni_ntab(su.g) * 1024u; e += blockDim.x) {
       const uint32_t v = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
       T[e] = v;
       if (blockIdx.x == 0) const_cast<uint32_t*>(gT)[e] = v;
@@ -451,7 +461,9 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 // 4 GiB even into an L2-resident ring: the wave's next row loads then wait on the store's completion;
 // tools/microbench/mb_uni.hip wr_W1, st_S1..S6). ENTRY-kind tuples (per-entry crc) and the merge's key
 // hashes are still stored in the loop.
-template <int S, bool kChunk, bool kHash, bool kFill>
+// kAl: every window and header starts on a dword (sz and t multiples of 4, as for LazyDB's 332-B
+// config 2/4/5 entries): no funnel shifts (22 v_alignbyte per batch at S = 11).
+template <int S, bool kChunk, bool kHash, bool kFill, bool kAl>
 __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint8_t* lp2, const uint32_t* T,
                                           int lane, int wave, uint64_t a_lo, uint64_t a_hi) {
   if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
@@ -474,28 +486,36 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
   const uint32_t lead0 = uni_lead(su.g, j);   // bytes lane j masks at its window's start
   const uint32_t lb = ((uint32_t)lane & 31u) * 4u;   // this lane's bank in the LP2 rows
   const uint32_t nw = su.m.nw, hrows = (nw + 2 + 3) / 4;
+  const uint32_t dsh = G - 1 - j;   // direct combine: this lane's shift, in windows
   const bool fill = kFill && p.kind == LDB_TUPLE_INDEX;
+  // the lead masks of every step, once per lane (loop-invariant, 2 S VGPRs): keep the window's bytes >= lead.
+  // Round 2 recomputed them per batch behind a per-step uniform branch and an opaque copy (to stay
+  // under 64 VGPRs); with the LP2 block's 4 waves per SIMD the registers are there, and the branchy
+  // form cost 0.34 ms of 1.19 at config 4 (tools/sweep_uni.sh, LDB_UNI_NOMASK)
+  uint32_t lm0[S], lm1[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const uint32_t n = lead0 > 8u * k ? lead0 - 8u * k : 0u;
+    lm0[k] = n >= 4 ? 0u : 0xFFFFFFFFu << (8 * n);
+    lm1[k] = n >= 8 ? 0u : (n > 4 ? 0xFFFFFFFFu << (8 * (n - 4)) : 0xFFFFFFFFu);
+  }
   GpuWave wp{lane};
   const uint64_t nbatch = kChunk ? ~0ull : (p.len / sz + E) / E;   // !kChunk: ceil(ncand / E), ncand = len / sz + 1
   // K as last seen: the load issued in one batch is tested at the top of the next, so its latency hides
   // behind the batch (a batch past K only costs its own time: the run's tuples stop at K anyway)
-  uint64_t kseen = ~0ull;
+  v2u32 kv = {~0u, ~0u};   // K as loaded during the previous batch (vector value: read at the next top)
+  const __amdgpu_buffer_rsrc_t krs = rsrc_of(p.dyn, 8);
   for (uint64_t b = b_first + (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
     if (kChunk && b * Esz > (all_hi ? p.len : a_hi)) break;   // wave-uniform: no candidate of this launch from here on
+    // uniform by construction (one address), but a load's result is divergent to the compiler: the
+    // loop exit on it would make b, and every descriptor built from b, divergent (waterfall loops)
+    const uint64_t kseen = ((uint64_t)__builtin_amdgcn_readfirstlane(kv[1]) << 32) | __builtin_amdgcn_readfirstlane(kv[0]);
     if (b * E >= kseen) break;
-#ifdef LDB_UNI_NOK   // A/B only: no per-batch look at K
-    const uint64_t knext = ~0ull;
-#else
-    uint64_t knext = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // uniform by construction (one address), but an atomic's result is divergent to the compiler: the
-    // loop exit on it would make b, and every descriptor built from b, divergent
-    knext = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(knext >> 32)) << 32) |
-            __builtin_amdgcn_readfirstlane((uint32_t)knext);
-#endif
+
     // Opaque per-batch copies: the uniform step / level conditions and the lane masks derived from
     // them are evaluated inside the batch, not hoisted out of the loop as a bank of held SGPR masks.
-    uint32_t tt = __builtin_amdgcn_readfirstlane(t), GG = __builtin_amdgcn_readfirstlane(G), c = ~j & (j + 1), lead = lead0;
-    asm volatile("" : "+s"(tt), "+s"(GG), "+v"(c), "+v"(lead));
+    uint32_t GG = __builtin_amdgcn_readfirstlane(G), c = ~j & (j + 1);
+    asm volatile("" : "+s"(GG), "+v"(c));
     const uint64_t e = b * E + ((uint32_t)lane >> lg);
     const uint64_t x = e * sz;
     if (kChunk && (b + 1) * Esz + need <= a_lo) continue;   // wave-uniform: below the launch's range (b_first's slack)
@@ -504,7 +524,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     const uint64_t nrec = (p.len - base + 3) & ~3ull;
     const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)min(nrec, (uint64_t)0xFFFFFFFFu));
     // the group's last lane: the header (stored crc and bytes [4, 40)), in flight with the rows
-    const uint32_t hx = (uint32_t)(x - base), ha = hx & ~3u, hsh = hx & 3u;
+    const uint32_t hx = (uint32_t)(x - base), ha = hx & ~3u, hsh = kAl ? 0u : hx & 3u;
     // the header rows the check reads: dwords [0, nw + 2) from ha (the stored crc, nw template words and
     // the funnel's next dword), so 1 row for LazyDB's 10-13-byte Set headers, 3 at most (wave-uniform)
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
@@ -523,7 +543,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
 #endif
     }
     const int32_t ws = (int32_t)hx + 4 - (int32_t)t + (int32_t)(j * P);   // < 0 only when base = 0
-    const uint32_t a = (uint32_t)ws & ~3u, sh = (uint32_t)ws & 3u;
+    const uint32_t a = (uint32_t)ws & ~3u, sh = kAl ? 0u : (uint32_t)ws & 3u;
     uint32_t d[4 * R];
     if (LDB_UNI_ABL == 2) {
 #pragma unroll
@@ -548,6 +568,13 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
         d[i] = ld4(rs, o < 0 ? kDrop : (uint32_t)o);
       }
     }
+#ifndef LDB_UNI_NOK   // A/B only: no per-batch look at K
+    // K for the next batch's exit test: a buffer load with sc1 (past this CU's L1, so it sees other CUs'
+    // atomicMin), vector memory only, consumed at the next batch's top so its latency hides behind this
+    // batch. (A relaxed atomic load compiled to a flat load, which also counts on lgkmcnt, and the
+    // compiler waited for it before issuing the rows.)
+    kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
+#endif
     // every row (and header) load in flight before the first use: left alone, the scheduler trades them
     // for registers and issues them one step ahead of the CRC (3 in flight: 1.26 vs 0.82 ms, mb_uni.hip)
     __builtin_amdgcn_sched_barrier(0);
@@ -559,27 +586,35 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
 #ifdef LDB_UNI_NOMASK   // A/B only (results wrong): no lead masks
       if (false) {
 #else
-      if ((uint32_t)(8 * k) < tt) {   // wave-uniform
+      {
 #endif
-        // masked bytes from this step's start (lane 0 only): keep bytes >= n of the 8. The opaque
-        // copy keeps the compiler from hoisting every step's mask out of the batch loop.
-        uint32_t ld = lead;
-        asm volatile("" : "+v"(ld));
-        const uint32_t n = ld > 8u * k ? ld - 8u * k : 0u;
-        w0 &= n >= 4 ? 0u : 0xFFFFFFFFu << (8 * n);
-        w1 &= n >= 8 ? 0u : (n > 4 ? 0xFFFFFFFFu << (8 * (n - 4)) : 0xFFFFFFFFu);
+        w0 &= lm0[k];
+        w1 &= lm1[k];
       }
       if (LDB_UNI_ABL == 1 || LDB_UNI_ABL == 3) reg ^= w0 ^ w1;
       else reg = lp2_step4(lp2, lb, lp2_step4(lp2, lb, reg, w0), w1);
     }
     if (LDB_UNI_ABL) asm volatile("" ::"v"(reg));
 #ifndef LDB_UNI_NOCOMB   // A/B only (results wrong): no combine
+    if (GG <= kUniDirectG) {
+      // direct: lane j shifts its register by (G - 1 - j) P bytes (4 lookups in its own table), then the
+      // group's registers are xor-reduced by DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror), so
+      // every lane of the group ends with the span's register: 4 lookups per lane against the tree's 8
+      const uint32_t* Td = T + (dsh ? dsh - 1 : 0) * 1024u;
+      const uint32_t sv = Td[reg & 0xFFu] ^ Td[256 + ((reg >> 8) & 0xFFu)] ^ Td[512 + ((reg >> 16) & 0xFFu)] ^
+                          Td[768 + (reg >> 24)];
+      reg = dsh ? sv : reg;
+      if (GG >= 2) reg ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)reg, 0xB1, 0xF, 0xF, false);
+      if (GG >= 4) reg ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)reg, 0x4E, 0xF, 0xF, false);
+      if (GG >= 8) reg ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)reg, 0x141, 0xF, 0xF, false);
+    } else {
     uni_level<1>(wp, T, GG, c, reg);
     uni_level<2>(wp, T + 1024, GG, c, reg);
     uni_level<4>(wp, T + 2048, GG, c, reg);
     uni_level<8>(wp, T + 3072, GG, c, reg);
     uni_level<16>(wp, T + 4096, GG, c, reg);
     uni_level<32>(wp, T + 5120, GG, c, reg);
+    }
 #endif
     // the header: bytes [4, hs) against the memo's (uni_header_ok). The memo is read from LDS through
     // an opaque offset, so its words stay per-batch VGPR loads instead of SGPRs held across the loop.
@@ -611,12 +646,12 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
       ok = ok && diff == 0u && ((reg ^ KL) == ~crc || LDB_UNI_ABL);   // getEntryCrc == stored crc (log_file.go:141-143)
     }
 #ifdef LDB_UNI_OKALL   // A/B only (results wrong): every candidate accepted, K untouched
+    asm volatile("" ::"v"(reg), "v"(ok));   // the CRC and the check stay live
     ok = true;
 #endif
     const uint64_t bad = __ballot((last && mine && !ok) ? 1 : 0);
     if (bad && lane == 0)
       atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
-    kseen = knext;
     if (ok && e < p.cap && !fill) {
       uint32_t z = 0;
       asm volatile("" : "+v"(z));
@@ -669,8 +704,13 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool al = (su.m.sz & 3u) == 0 && (su.g.t & 3u) == 0;   // every window and header dword-aligned
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n) case n: uni_waves<n, kChunk, kHash, !kHash>(p, su, lp2, comb, lane, wave, a_lo, a_hi); break;
+#define LDB_UNI_CASE(n)                                                                    \
+  case n:                                                                                  \
+    if (al) uni_waves<n, kChunk, kHash, !kHash, true>(p, su, lp2, comb, lane, wave, a_lo, a_hi); \
+    else uni_waves<n, kChunk, kHash, !kHash, false>(p, su, lp2, comb, lane, wave, a_lo, a_hi); \
+    break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
 #undef LDB_UNI_CASE
@@ -721,8 +761,13 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool al = (su.m.sz & 3u) == 0 && (su.g.t & 3u) == 0;   // every window and header dword-aligned
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n) case n: uni_waves<n, false, kHash, false>(p, su, lp2, comb, lane, wave, 0, p.len); break;
+#define LDB_UNI_CASE(n)                                                                         \
+  case n:                                                                                       \
+    if (al) uni_waves<n, false, kHash, false, true>(p, su, lp2, comb, lane, wave, 0, p.len);  \
+    else uni_waves<n, false, kHash, false, false>(p, su, lp2, comb, lane, wave, 0, p.len);    \
+    break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
 #undef LDB_UNI_CASE
