@@ -244,15 +244,16 @@ def measure_traffic(img, cap, args, kernel):
     path = os.path.join(shm, f"ldb_pmc_{os.getpid()}.bin")
     try:
         img.tofile(path)
+        # the device path's instance only (k_uniform<false, false>, k_scan_main<false>): not k_uniform_fill
         cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--pmc", "FETCH_SIZE", "--kernel-include-regex",
-               kernel, "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
+               kernel + "<false", "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", f"{path}:{cap}", "--io", str(args.io), "--kind", str(args.kind)]
         p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
         per = {}
         for f in glob.glob(os.path.join(tmp, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    if kernel in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+                    if kernel + "<false" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
                         key = r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id")
                         per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
         if not per:

@@ -299,7 +299,11 @@ struct UniSetup {
 // direct form, G - 1 tables "shift by d P bytes" (d = 1 .. G - 1); larger G the tree, lg tables
 // "shift by 2^i P bytes".
 constexpr uint32_t kUniDirectG = 8;
-constexpr uint64_t kUniTabWords = (kUniDirectG - 1 > kUniLevels ? kUniDirectG - 1 : kUniLevels) * 1024;
+#ifndef LDB_UNI_CH2
+#define LDB_UNI_CH2 0   // 1: each lane's window as two independent CRC chains (half the dependent LDS round trips)
+#endif
+constexpr uint32_t kUniHalfTab = (kUniDirectG - 1 > kUniLevels ? kUniDirectG - 1 : kUniLevels);   // its table index
+constexpr uint64_t kUniTabWords = (kUniHalfTab + (LDB_UNI_CH2 ? 1 : 0)) * 1024;
 LDB_HD inline uint32_t uni_ntab(const UniGeo& g) { return g.G <= kUniDirectG ? g.G - 1 : g.lg; }
 
 // The run prefix's CRC (round 3): 2-byte slicing on LANE-PRIVATE byte tables, so a wave's table reads
@@ -312,6 +316,7 @@ LDB_HD inline uint32_t uni_ntab(const UniGeo& g) { return g.G <= kUniDirectG ? g
 // config 4) one lookup per byte instead of 0.75, all conflict-free (tools/microbench/mb_uni.hip:
 // config 4 verify 0.794 -> 0.724 ms on one box, within 1 % of the same loads XOR-reduced).
 constexpr uint32_t kLp2Bytes = 65536;
+constexpr int kFillThreads = 1024;   // k_uniform_fill workgroup
 __device__ __forceinline__ uint32_t lp2_read(const uint8_t* lp2, uint32_t a) {
   return *reinterpret_cast<const uint32_t*>(lp2 + a);
 }
@@ -387,7 +392,7 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_
   __syncthreads();
   if (published) {
     if (!su.g.ok) return false;
-    for (uint32_t e = threadIdx.x; e < uni_ntab(su.g) * 1024u; e += blockDim.x) T[e] = gT[e];
+    for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) T[e] = gT[e];
     return true;
   }
   auto stage = [&](int w, uint64_t at) {
@@ -420,6 +425,7 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_
         for (uint32_t d = 1; d < su.g.G; ++d) xn[d - 1] = p.xw[d * su.g.P];   // d P <= 7 * 96 < kW
       else
         for (uint32_t i = 0; i < su.g.lg; ++i) xn[i] = p.xw[su.g.P << i];
+      if (LDB_UNI_CH2) xn[kUniHalfTab] = p.xw[8 * (su.g.S - su.g.S / 2)];   // the second chain's length
       if (blockIdx.x == 0) p.dyn[1] = su.m.sz;
     } else if (blockIdx.x == 0) {
       p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
@@ -427,7 +433,8 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_
   }
   __syncthreads();
   if (su.g.ok)
-    for (uint32_t e = threadIdx.x; e < uni_ntab(su.g) * 1024u; e += blockDim.x) {
+    for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) {
+      if (e >= uni_ntab(su.g) * 1024u && e < kUniHalfTab * 1024u) continue;
       const uint32_t v = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
       T[e] = v;
       if (blockIdx.x == 0) const_cast<uint32_t*>(gT)[e] = v;
@@ -578,8 +585,10 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     // every row (and header) load in flight before the first use: left alone, the scheduler trades them
     // for registers and issues them one step ahead of the CRC (3 in flight: 1.26 vs 0.82 ms, mb_uni.hip)
     __builtin_amdgcn_sched_barrier(0);
-    // lane j's window: S steps from register 0, lane 0's first t bytes masked
-    uint32_t reg = 0;
+    // lane j's window: S steps from register 0, lane 0's first t bytes masked. LDB_UNI_CH2: steps
+    // [0, S/2) on register ra, [S/2, S) on reg, joined by ra's shift over the second half's bytes.
+    constexpr int kSA = (LDB_UNI_CH2 && S >= 4) ? S / 2 : 0;
+    uint32_t reg = 0, ra = 0;
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       uint32_t w0 = funnel(d[2 * k + 1], d[2 * k], sh), w1 = funnel(d[2 * k + 2], d[2 * k + 1], sh);
@@ -592,7 +601,12 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
         w1 &= lm1[k];
       }
       if (LDB_UNI_ABL == 1 || LDB_UNI_ABL == 3) reg ^= w0 ^ w1;
+      else if (k < kSA) ra = lp2_step4(lp2, lb, lp2_step4(lp2, lb, ra, w0), w1);
       else reg = lp2_step4(lp2, lb, lp2_step4(lp2, lb, reg, w0), w1);
+    }
+    if (kSA) {
+      const uint32_t* Th = T + kUniHalfTab * 1024u;
+      reg ^= Th[ra & 0xFFu] ^ Th[256 + ((ra >> 8) & 0xFFu)] ^ Th[512 + ((ra >> 16) & 0xFFu)] ^ Th[768 + (ra >> 24)];
     }
     if (LDB_UNI_ABL) asm volatile("" ::"v"(reg));
 #ifndef LDB_UNI_NOCOMB   // A/B only (results wrong): no combine
@@ -724,7 +738,7 @@ static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
 // took (the same byte predicate); every one of them below the K seen now was verified by that launch
 // (a later chunk only lowers K past its own entries).
 template <bool kChunk>
-__global__ __launch_bounds__(256) void k_uniform_fill(Pipe p, uint64_t a_lo, uint64_t a_hi) {
+__global__ __launch_bounds__(kFillThreads) void k_uniform_fill(Pipe p, uint64_t a_lo, uint64_t a_hi) {
   if (p.kind != LDB_TUPLE_INDEX || p.dyn[2] != kUniReady) return;
   const UniSetup* gsu = reinterpret_cast<const UniSetup*>(p.uni);
   if (!gsu->g.ok) return;
@@ -1607,9 +1621,10 @@ int uniform_grid(const ldb_ctx* c, uint64_t bytes) {
   const uint64_t batches = bytes / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
   return std::max(1, (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu));
 }
-// k_uniform_fill: a dense sweep, 4 workgroups of 256 threads per CU
+// k_uniform_fill: a dense sweep, 2 workgroups of 1024 threads per CU (tools/microbench/mb_uni.hip wr_W0:
+// 207 MB of tuples in 34 us)
 int fill_grid(const ldb_ctx* c, uint64_t bytes) {
-  return std::max(1, (int)std::min<uint64_t>(bytes / 16 / 256 + 1, (uint64_t)c->n_cu * 4));
+  return std::max(1, (int)std::min<uint64_t>(bytes / 16 / kFillThreads + 1, (uint64_t)c->n_cu * 2));
 }
 
 // An image that is still being copied in: bytes [0, avail[i]) are in place once ev[i] has fired
@@ -1675,7 +1690,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
         const uint64_t hi = i + 1 == plan->n ? len : std::min(plan->avail[i], len);
         launch(lo, hi);
         if (kind == LDB_TUPLE_INDEX)
-          hipLaunchKernelGGL(k_uniform_fill<true>, dim3(fill_grid(c, hi - lo)), dim3(256), 0, s, p, lo, hi);
+          hipLaunchKernelGGL(k_uniform_fill<true>, dim3(fill_grid(c, hi - lo)), dim3(kFillThreads), 0, s, p, lo, hi);
         lo = hi;
       }
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
@@ -1684,7 +1699,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
       launch(0, len);
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
       if (kind == LDB_TUPLE_INDEX && !p.hash_out)
-        hipLaunchKernelGGL(k_uniform_fill<false>, dim3(fill_grid(c, len)), dim3(256), 0, s, p, 0, len);
+        hipLaunchKernelGGL(k_uniform_fill<false>, dim3(fill_grid(c, len)), dim3(kFillThreads), 0, s, p, 0, len);
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
   } else if (ev) {

@@ -12,6 +12,10 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    for k, v in (("k_uniform_fill", "k_uniform_fill"), ("k_uniform_batch", "k_uniform_batch"),
+                 ("k_uniform<true", "k_uniform_chunk"), ("k_uniform<false, true>", "k_uniform_hash")):
+        if k in name:
+            return v
     for k in ("k_uniform", "k_scan_main", "k_link", "k_repair", "k_combine", "k_final", "k_compact", "k_serial", "k_fallback",
               "k_locate", "k_insert", "k_live", "k_scan_reduce", "k_scan_tiles", "k_scan_write", "k_pack",
               "k_emit_copy"):
@@ -26,7 +30,7 @@ def main(d: str) -> None:
         with open(f) as fh:
             rows = list(csv.DictReader(fh))
         for r in rows:
-            print(f"{short(r['Name']):14s} calls={r['Calls']:>6s} avg_ms={float(r['AverageNs']) / 1e6:9.4f} "
+            print(f"{short(r['Name']):16s} calls={r['Calls']:>6s} avg_ms={float(r['AverageNs']) / 1e6:9.4f} "
                   f"min_ms={float(r['MinNs']) / 1e6:9.4f} max_ms={float(r['MaxNs']) / 1e6:9.4f} pct={float(r['Percentage']):6.2f}")
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
