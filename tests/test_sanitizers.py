@@ -1,0 +1,22 @@
+"""ASan + UBSan over the CPU wave emulator (the engine's own phase code: ldb_engine.h, ldb_chain.h,
+ldb_wave.h, ldb_pipeline.h, as tests/emu compiles them) and the C oracle: tests/san/san_main.cpp runs
+both over every golden fixture (and ragged cuts of each), generated fixed / Zipf / reference-bench /
+writer-mix logs and a corrupt one, under both IO rules, with the run prefix on and off, and compares
+every tuple with the oracle. A sanitizer report aborts the run (halt_on_error)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_emulator_and_oracle_under_asan_ubsan():
+    p = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "san"), "run"], capture_output=True, text=True,
+                       timeout=900)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out[-4000:]
+    assert "0 mismatches" in out, out[-2000:]
+    assert "runtime error" not in out and "ERROR: AddressSanitizer" not in out, out[-4000:]
