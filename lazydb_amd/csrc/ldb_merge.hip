@@ -1239,7 +1239,11 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
   // 4.482 ms against 4.602 without (replay 1.58 vs 1.23 ms, liveness 1.56 vs 2.03; gpurun_out/m3_h*).
   // LDB_MERGE_SCAN_HASH=0 turns it off. Measured and rejected: the entry's G lanes hashing key chunks in
   // parallel (shuffle-combined): replay 1.88-1.97 ms.
-  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") == nullptr || atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
+  // Round 3: off by default. With the run prefix's verify loop free of stores (k_uniform_fill), the
+  // scan-side hash became the most expensive part of the replay: in the loop 1.64 vs 0.97 ms, as a
+  // separate pass over the keys 1.84 vs 0.97 ms, against +0.46 ms of liveness when k_insert hashes the
+  // key it reads anyway (config 5: 4.58 ms off, 4.74 / 4.94 ms on; gpurun_out/mg1, mg2).
+  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") != nullptr && atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
   // every file's replay scan in ONE batched pipeline (ldb_scan.hip enqueue_scan_batch) on the
   // caller's context and stream; a set the batch does not take (a tiny image) goes file by file
   {

@@ -666,7 +666,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     const uint64_t bad = __ballot((last && mine && !ok) ? 1 : 0);
     if (bad && lane == 0)
       atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
-    if (ok && e < p.cap && !fill) {
+    if (ok && e < p.cap && (!fill || kHash)) {
       uint32_t z = 0;
       asm volatile("" : "+v"(z));
       const UniMemo& m = *(&su.m + z);
@@ -738,7 +738,7 @@ static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
 // took (the same byte predicate); every one of them below the K seen now was verified by that launch
 // (a later chunk only lowers K past its own entries).
 template <bool kChunk>
-__global__ __launch_bounds__(kFillThreads) void k_uniform_fill(Pipe p, uint64_t a_lo, uint64_t a_hi) {
+__device__ __forceinline__ void uni_fill(const Pipe& p, uint64_t a_lo, uint64_t a_hi) {
   if (p.kind != LDB_TUPLE_INDEX || p.dyn[2] != kUniReady) return;
   const UniSetup* gsu = reinterpret_cast<const UniSetup*>(p.uni);
   if (!gsu->g.ok) return;
@@ -757,6 +757,10 @@ __global__ __launch_bounds__(kFillThreads) void k_uniform_fill(Pipe p, uint64_t 
   for (uint64_t e = e_lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e_hi; e += (uint64_t)gridDim.x * blockDim.x)
     store_tuple(out + e, uni_pos(m, e * sz), m.k, m.v);
 }
+template <bool kChunk>
+__global__ __launch_bounds__(kFillThreads) void k_uniform_fill(Pipe p, uint64_t a_lo, uint64_t a_hi) {
+  uni_fill<kChunk>(p, a_lo, a_hi);
+}
 
 // a batched scan's run prefixes: grid.y = file. The Pipes travel as kernel arguments (not through
 // a device pointer like the other batched stages): kernarg loads stay re-loadable constants.
@@ -764,6 +768,38 @@ constexpr int kUniBatch = 16;
 struct UniBatch {
   Pipe p[kUniBatch];
 };
+// the batched scan's fill: grid.y = file. With hashes (merge mode) the same pass also emits each run
+// entry's key hash (ldb::key_hash_w): one thread per entry reads its key as dword-aligned 16-B pieces.
+// In the verify loop the hash was serial work on one lane in G plus key loads issued after the CRC and
+// waited for at once (config 5 replay: 1.64 ms with it there, 0.97 without).
+template <bool kHash>
+__global__ __launch_bounds__(kFillThreads) void k_uniform_fill_batch(UniBatch b) {
+  const Pipe p = b.p[blockIdx.y];
+  uni_fill<false>(p, 0, p.len);
+  if (!kHash || p.dyn[2] != kUniReady) return;
+  const UniSetup* gsu = reinterpret_cast<const UniSetup*>(p.uni);
+  if (!gsu->g.ok) return;
+  const uint64_t sz = gsu->m.sz, K = p.dyn[0];
+  const uint32_t hs = gsu->m.hs, kl = gsu->m.k;
+  const uint64_t n = K < p.cap ? K : p.cap;
+  // a wave's 64 entries share one descriptor based at its first entry's key (descriptors must be
+  // wave-uniform: rsrc_of reads lane 0's base), each lane at its own offset from there
+  for (uint64_t e0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); e0 < n; e0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = e0 + (threadIdx.x & 63u);
+    const uint64_t wb = (e0 * sz + hs) & ~3ull;
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + wb, (uint32_t)min((p.len - wb + 3) & ~3ull, (uint64_t)0xFFFFFFFFu));
+    if (e >= n) continue;
+    const uint32_t kx = (uint32_t)(e * sz + hs - wb), ka = kx & ~3u, s0 = kx & 3u;
+    p.hash_out[e] = key_hash_w(
+        [&](uint32_t i, uint64_t* w) {
+          const uint4 q = ld16(rs, ka + i);
+          const uint32_t q4 = ld4(rs, ka + i + 16);
+          w[0] = (uint64_t)funnel(q.y, q.x, s0) | ((uint64_t)funnel(q.z, q.y, s0) << 32);
+          w[1] = (uint64_t)funnel(q.w, q.z, s0) | ((uint64_t)funnel(q4, q.w, s0) << 32);
+        },
+        kl);
+  }
+}
 template <bool kHash>
 __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   const Pipe p = b.p[blockIdx.y];
@@ -779,8 +815,8 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
 #define LDB_UNI_CASE(n)                                                                         \
   case n:                                                                                       \
-    if (al) uni_waves<n, false, kHash, false, true>(p, su, lp2, comb, lane, wave, 0, p.len);  \
-    else uni_waves<n, false, kHash, false, false>(p, su, lp2, comb, lane, wave, 0, p.len);    \
+    if (al) uni_waves<n, false, false, true, true>(p, su, lp2, comb, lane, wave, 0, p.len);  \
+    else uni_waves<n, false, false, true, false>(p, su, lp2, comb, lane, wave, 0, p.len);    \
     break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
@@ -1809,10 +1845,16 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     const int m = std::min(kUniBatch, nf - i0);
     const int ugb = std::min(ug, std::max(1, (c->n_cu * bpc + m - 1) / m));
     for (int i = 0; i < m; ++i) ub.p[i] = c->h_pipes[i0 + i];
-    if (hashed)
-      hipLaunchKernelGGL(k_uniform_batch<true>, dim3(ugb, (unsigned)m), dim3(64 * kUniWaves), 0, s, ub);
-    else
-      hipLaunchKernelGGL(k_uniform_batch<false>, dim3(ugb, (unsigned)m), dim3(64 * kUniWaves), 0, s, ub);
+    hipLaunchKernelGGL(k_uniform_batch<false>, dim3(ugb, (unsigned)m), dim3(64 * kUniWaves), 0, s, ub);
+    if (kind == LDB_TUPLE_INDEX || hashed) {
+      uint64_t maxlen = 0;
+      for (int i = 0; i < m; ++i) maxlen = std::max(maxlen, ub.p[i].len);
+      const int fg = std::max(1, std::min(fill_grid(c, maxlen), (c->n_cu * 2 + m - 1) / m));
+      if (hashed)
+        hipLaunchKernelGGL(k_uniform_fill_batch<true>, dim3(fg, (unsigned)m), dim3(kFillThreads), 0, s, ub);
+      else
+        hipLaunchKernelGGL(k_uniform_fill_batch<false>, dim3(fg, (unsigned)m), dim3(kFillThreads), 0, s, ub);
+    }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
   if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
