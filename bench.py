@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--xsim", type=int, default=0,
                     help="config 5 --xmerge: play K ranks in this one process and time each rank's phases")
     ap.add_argument("--e2e", type=int, default=3, help="iterations of the PCIe-inclusive host-API leg (0: skip)")
-    ap.add_argument("--legs", default="2,3",
-                    help="extra single-GPU configs timed after the main line at N = 1 (comma list; '' = none)")
+    ap.add_argument("--legs", default="1,2,3,w,5",
+                    help="extra single-GPU configs timed after the main line at N = 1 (comma list; '' = none): "
+                         "1 the reference bench's log (Mmap), 2, 3, w the writer-realistic mix, 5 the merge")
     ap.add_argument("--leg-steps", type=int, default=20)
     ap.add_argument("--pmc", type=int, default=1,
                     help="measure roofline.traffic in this run: a rocprofv3 --pmc FETCH_SIZE child process scans "
@@ -119,24 +120,34 @@ def rehearse_launch(args):
         dist.destroy_process_group()
 
 
-def make_image(cfg: int, rank: int):
+def make_image(cfg, rank: int):
+    """Synthetic image of a bench config. Returns (img, entries, end_off, workload text, IO rule or None
+    for the command line's)."""
     from oracle import coracle  # format producer (writeLogEntry restatement) for synthetic inputs
+    io = None
     if cfg == 1:
-        # bench/db_bench_test.go shape: 500 000 STRING entries, close, reopen;
-        # the file is preallocated to MaxLogFileSize = 512 MiB (fileio.go:66-68), so the replay ends at
-        # the zero sentinel
-        img, n, end = coracle.gen_log(512 << 20, 1 + rank, ksize=64, vsize=256, max_entries=500_000)
-        wl = "reopen replay of 500K entries, 64B key / 256B value, 512 MiB preallocated file"
+        # BASELINE config 1 in the reference benchmark's own shape (bench/db_bench_test.go:17-36, :63-68):
+        # 500 000 Sets of "bench_test_key_<i>" (16..21-B keys: the entry size changes at i = 10, 100, ...)
+        # with 512-B alphabet values, in one file preallocated to MaxLogFileSize = 512 MiB, reopened under
+        # the Mmap IOController (opts.IOType = 1: o + n >= len is EOF, iocontroller/mmap.go:46-52)
+        img, n, end = coracle.gen_bench_log(512 << 20, 1 + rank, n_entries=500_000)
+        wl = "reference bench log: 500K Sets, bench_test_key_<i> keys, 512B values, 512 MiB preallocated, Mmap rule"
+        io = 1
     elif cfg == 2:
         img, n, end = coracle.gen_log(1 << 30, 1 + rank, ksize=64, vsize=256)
         wl = "1GiB log file, 64B key / 256B value (332B entries), FileIO bound"
     elif cfg == 3:
         img, n, end = coracle.gen_log(8 << 30, 2 + rank, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
         wl = "8GiB log file, 64B key, value 16*Zipf(1.1,[1,4096]) B"
+    elif cfg == "w":
+        # what LazyDB's writers append, interleaved (str.go Set / SetEX / Delete, tx.go Commit): variable
+        # keys and values, 10 % SetEX (5-byte ExpiredAt), 10 % SDelete, 10 % TxCommited
+        img, n, end = coracle.gen_writer_log(1 << 30, 30 + rank)
+        wl = "1GiB writer-realistic log: Set/SetEX/Delete/Tx.Commit mix, user:<id> keys, 8B-4KiB log-uniform values"
     else:
         img, n, end = coracle.gen_log(4 << 30, 10 + rank, ksize=64, vsize=256)
         wl = "4GiB log file per GPU, 64B key / 256B value"
-    return img, n, end, wl
+    return img, n, end, wl, io
 
 
 def _host_threads() -> int:
@@ -296,6 +307,64 @@ def init_dist(world: int, local: int) -> int:
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
     return local
+
+
+def merge_leg(eng, args, dev):
+    """BASELINE config 5 as a leg of the N = 1 line: the same merge as main_merge, verified against the
+    oracle's merge (whose run is also the CPU baseline: the C port of Merge, one thread), then timed."""
+    import numpy as np
+    import torch
+    from oracle import coracle   # format producer for the synthetic input; checker; CPU baseline
+    now = 1_700_000_000
+    imgs, n, ends = coracle.gen_merge(16, 256 << 20, 16 * 808_540, 3, ksize=64, vsize=256)
+    files = [(torch.from_numpy(imgs[i]).to(dev), i + 1, i < 15) for i in range(16)]
+    kw = dict(active_fid=16, active_off=ends[15], max_file_size=256 << 20, now=now)
+    out = eng.merge_dev(files, **kw)
+    r = out["result"]
+    verified, cpu = None, None
+    if not args.no_verify:
+        t0 = time.perf_counter()
+        ref, stream, pos, segs, live, stats = coracle.merge([(imgs[i], i + 1, i < 15) for i in range(16)], 16,
+                                                            ends[15], 256 << 20, now)
+        dt = time.perf_counter() - t0
+        verified = bool((r.status, r.n_emit, r.emit_bytes, r.end_fid, r.end_off) ==
+                        (ref.status, ref.n_emit, ref.emit_bytes, ref.end_fid, ref.end_off)
+                        and out["pos"].tobytes() == pos.tobytes()
+                        and torch.equal(out["stream"], torch.from_numpy(stream).to(dev)))
+        cpu = {"value": round(sum(ends) / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": "the full 16-file set: oracle replay + map-based index + EncodeEntry rewrite, 1 thread "
+                         "(the verification run, timed)"}
+        del stream, pos, live
+    caps = dict(stream_cap=int(r.emit_bytes) + 16, pos_cap=int(r.n_emit) + 16, seg_cap=64,
+                live_cap=int(r.n_records) + 16, fetch_pos=False)
+    for _ in range(2):
+        eng.merge_dev(files, **kw, **caps)
+    torch.cuda.synchronize()
+    ph = np.zeros(3)
+    steps = args.leg_steps
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.merge_dev(files, **kw, **caps)
+        ph += np.array(eng.merge_timing())
+    torch.cuda.synchronize()
+    step = (time.perf_counter() - t0) / steps
+    ph /= steps
+    dev_ms = float(ph.sum())
+    alg = sum(ends) + 2 * int(r.emit_bytes)   # replay read + compacted stream read and written
+    leg = {"config": 5, "workload": "merge/GC: 16 log files x 256 MiB, 64B key / 256B value, 50% stale, 15 targets",
+           "input_bytes": int(sum(ends)), "records": int(r.n_records), "emitted": int(r.n_emit),
+           "emit_bytes": int(r.emit_bytes), "segments": int(r.n_segments), "steps": steps,
+           "ms_per_step": round(step * 1e3, 4), "GiB_per_s": round(sum(ends) / step / 2**30, 3),
+           "phases_ms": {"replay_scans": round(ph[0], 3), "liveness": round(ph[1], 3), "compaction": round(ph[2], 3)},
+           "roofline": {"bound": "hbm", "kernel": "whole merge pipeline (device time)",
+                        "achieved": round(alg / (dev_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(alg / (dev_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_launch": alg,
+                        "note": "algorithmic bytes = sum of end_off (replay read) + 2 x emitted bytes"},
+           "verified_vs_oracle": verified, "cpu_baseline": cpu}
+    del files, imgs
+    torch.cuda.empty_cache()
+    return leg
 
 
 def main_merge(args):
@@ -571,7 +640,7 @@ def timed_scans(eng, S, fid, args, steps, world, stream):
     import torch.distributed as dist
 
     def step():
-        eng.scan_dev_async(S.d, fid=fid, io_type=args.io, kind=args.kind, out=S.out, cap=S.cap, result=S.res,
+        eng.scan_dev_async(S.d, fid=fid, io_type=S.io, kind=args.kind, out=S.out, cap=S.cap, result=S.res,
                            stream=stream)
 
     for _ in range(args.warmup):
@@ -628,19 +697,21 @@ def prepare(eng, cfg, rank, args, dev, verify: bool):
     workload text)."""
     import torch
     from lazydb_amd import _native as N
-    img, n_expect, end_expect, workload = make_image(cfg, rank)
+    img, n_expect, end_expect, workload, io = make_image(cfg, rank)
+    S_io = args.io if io is None else io
     cap = n_expect + 1024
     S = Resident(eng, img, cap, args.kind, dev)
+    S.io = S_io
     eng.reserve(img.size)
     stream = torch.cuda.current_stream(dev)
-    eng.scan_dev_async(S.d, fid=1 + rank, io_type=args.io, kind=args.kind, out=S.out, cap=cap, result=S.res,
+    eng.scan_dev_async(S.d, fid=1 + rank, io_type=S_io, kind=args.kind, out=S.out, cap=cap, result=S.res,
                        stream=stream)
     torch.cuda.synchronize()
     r = N.ScanResult.from_buffer_copy(S.res.cpu().numpy().tobytes())
     verified = None
     if verify:
         from oracle import coracle   # checker only
-        ref, rt = coracle.scan(img, args.io, fid=1 + rank, tuple_kind=args.kind, cap=cap)
+        ref, rt = coracle.scan(img, S_io, fid=1 + rank, tuple_kind=args.kind, cap=cap)
         n = int(min(r.n_entries, cap))
         got = S.out[: n * (16 if args.kind == 0 else 48)].cpu().numpy().tobytes()
         verified = (r.status, r.end_off, r.n_entries) == (ref.status, ref.end_off, ref.n_entries) and \
@@ -667,6 +738,7 @@ def run_leg(eng, cfg, args, dev):
            "run_entries": int(r.n_run), "roofline_kernel": kname, "roofline_bytes": kbytes,
            "roofline_frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
            "status": int(r.status), "fast_regions": int(r.n_fast), "regions": int(r.n_regions),
+           "regions_rerun": int(r.n_repairs), "io_type": "FileIO" if S.io == 0 else "Mmap",
            "verified_vs_oracle": verified}
     del S, img
     torch.cuda.empty_cache()
@@ -727,8 +799,11 @@ def main():
         gt = multi.max_over_ranks(time.perf_counter() - g0, dev)
         if rank == 0:
             tot = sum(int(x.numel()) for x in got)
-            gather = {"bytes_to_rank0": tot, "ms": round(gt * 1e3, 3), "GB_per_s": round(tot / gt / 1e9, 2),
-                      "backend": dist.get_backend()}
+            moved = multi.gather_tuples.last_bytes
+            gather = {"bytes_to_rank0": tot, "bytes_moved": moved, "ms": round(gt * 1e3, 3),
+                      "GB_per_s": round(moved / gt / 1e9, 2), "backend": dist.get_backend(),
+                      "method": "gatherv: all_gather of the counts, then batched isend/irecv of exactly those bytes",
+                      "exact": tot == int(tot_entries) * (16 if args.kind == 0 else 48)}
             del got
     e2e = None
     cap = S.cap
@@ -777,8 +852,11 @@ def main():
     if world == 1 and args.legs:
         del S
         torch.cuda.empty_cache()
-        for cfg in [int(x) for x in args.legs.split(",") if x.strip()]:
-            if cfg != args.config and cfg in (1, 2, 3, 4):
+        for tok in [x.strip() for x in args.legs.split(",") if x.strip()]:
+            cfg = tok if tok == "w" else int(tok)
+            if cfg == 5:
+                legs.append(merge_leg(eng, args, dev))
+            elif cfg != args.config and cfg in (1, 2, 3, 4, "w"):
                 legs.append(run_leg(eng, cfg, args, dev))
     if rank == 0:
         achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else None

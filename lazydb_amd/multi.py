@@ -41,25 +41,34 @@ def sum_over_ranks(xs, device):
 
 
 def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0):
-    """Gather every rank's tuple byte buffer (uint8, 1-D, on the rank's device) to `dst`.
+    """Gather every rank's tuple byte buffer (uint8, 1-D, on the rank's device) to `dst`: a gatherv.
 
-    One all_gather of the byte counts, then one gather of buffers padded to the largest count.
-    Returns the list of per-rank buffers (trimmed, rank order) on `dst`, None elsewhere.
+    One all_gather of the byte counts, then point-to-point transfers of exactly those bytes (one
+    batched group of isend / irecv: over RCCL the receives run concurrently on dst's xGMI links), so
+    unequal files ship no padding. Returns the list of per-rank buffers (rank order) on `dst`, None
+    elsewhere; gather_tuples.last_bytes is the byte total that crossed to dst.
     """
     assert tuple_bytes.dtype == torch.uint8 and tuple_bytes.dim() == 1
     world = dist.get_world_size()
     rank = dist.get_rank()
-    tuple_bytes = tuple_bytes.to(coll_device(tuple_bytes.device))
+    tuple_bytes = tuple_bytes.to(coll_device(tuple_bytes.device)).contiguous()
     dev = tuple_bytes.device
     n = torch.tensor([tuple_bytes.numel()], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
-    mx = max(max(counts), 1)
-    send = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    send[: tuple_bytes.numel()] = tuple_bytes
-    bufs = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == dst else None
-    dist.gather(send, bufs, dst=dst)
-    if rank != dst:
-        return None
-    return [b[:c] for b, c in zip(bufs, counts)]
+    gather_tuples.last_bytes = sum(c for r, c in enumerate(counts) if r != dst)
+    if rank == dst:
+        bufs = [tuple_bytes if r == dst else torch.empty(counts[r], dtype=torch.uint8, device=dev)
+                for r in range(world)]
+        ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in range(world) if r != dst and counts[r]]
+    else:
+        bufs = None
+        ops = [dist.P2POp(dist.isend, tuple_bytes, dst)] if counts[rank] else []
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return bufs
+
+
+gather_tuples.last_bytes = 0

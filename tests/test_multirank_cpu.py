@@ -77,3 +77,37 @@ def test_files_for_rank_round_robin():
     assert multi.files_for_rank([5, 1, 3, 2, 4], 0, 2) == [1, 3, 5]
     assert multi.files_for_rank([5, 1, 3, 2, 4], 1, 2) == [2, 4]
     assert multi.files_for_rank([1], 1, 8) == []
+
+
+def _gatherv_worker(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lazydb_amd import multi
+        # unequal byte counts, one rank with nothing: the gatherv ships exactly the bytes (no padding)
+        sizes = [48, 0, 16 * 1001]
+        mine = torch.arange(sizes[rank], dtype=torch.int64).to(torch.uint8) ^ rank
+        got = multi.gather_tuples(mine)
+        if rank == 0:
+            q.put(([g.numpy().tobytes() for g in got], multi.gather_tuples.last_bytes))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_three_rank_gatherv_unequal_sizes():
+    world = 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gatherv_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, moved = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sizes = [48, 0, 16 * 1001]
+    for r, g in enumerate(got):
+        assert g == (torch.arange(sizes[r], dtype=torch.int64).to(torch.uint8) ^ r).numpy().tobytes()
+    assert moved == sizes[1] + sizes[2]   # exactly the other ranks' bytes crossed to rank 0

@@ -1,0 +1,40 @@
+"""Scan one synthetic image a few times on cuda:0 (for rocprofv3 kernel traces of a single workload).
+usage: python tools/scan_one.py <cfg: 1|2|3|4|w|adv:<case>> [reps] [io]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from lazydb_amd import Engine
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "w"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    io_arg = int(sys.argv[3]) if len(sys.argv) > 3 else None
+    sys.argv = sys.argv[:1]
+    import bench
+    img, n, end, wl, io = bench.make_image(cfg if cfg == "w" else int(cfg), 0)
+    io = io_arg if io_arg is not None else (io or 0)
+    eng = Engine(0)
+    d = torch.from_numpy(img).to("cuda:0")
+    eng.reserve(img.size)
+    res, _ = eng.scan_dev(d, io_type=io, cap=n + 1024)
+    torch.cuda.synchronize()
+    eng.timing_split(1)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res, _ = eng.scan_dev(d, io_type=io, cap=n + 1024)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    u, m, tot, k = eng.timing_split(0)
+    print(f"{wl}: status {res.status} entries {res.n_entries} end {res.end_off} run {res.n_run} fast {res.n_fast}/"
+          f"{res.n_regions} repairs {res.n_repairs} broken {res.n_broken} | {dt * 1e3:.3f} ms/scan wall, k_uniform "
+          f"{u:.4f} k_scan_main {m:.4f} pipeline {tot:.4f} ms")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
