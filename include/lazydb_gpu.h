@@ -142,7 +142,10 @@ int ldb_scan_file(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t f
 
 /* Page-lock a host range (e.g. an mmap'd log file, mmap/mmap_linux.go:14-20) for the lifetime of the
  * mapping, so ldb_scan_file's host-to-device copy runs as direct DMA at PCIe rate instead of through
- * the runtime's pageable staging. Optional: ldb_scan_file works on any host memory. */
+ * the runtime's pageable staging. Optional: ldb_scan_file works on any host memory. A tuple array
+ * registered here for at least cap tuples is written in place by the kernels; any other output
+ * array (unregistered, pinned elsewhere, or registered shorter than cap tuples) is staged on the
+ * device and copied back. */
 int ldb_host_register(ldb_ctx* ctx, const void* h_ptr, uint64_t len);
 int ldb_host_unregister(ldb_ctx* ctx, const void* h_ptr);
 

@@ -1209,7 +1209,7 @@ int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_fil
 
 int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* files, int io_type,
                ldb_scan_result* d_res, std::vector<FileDesc>& fdh, uint64_t& n, ldb_merge_file_stat* h_stats,
-               ldb_merge_result* h_result, hipStream_t s, bool use_cache) {
+               ldb_merge_result* h_result, hipStream_t s, bool use_cache, bool produce_cache) {
   fdh.assign(nf + 1, FileDesc{});
   std::vector<ldb_scan_result> rh(nf);
   bool hit = use_cache && m->cache_ok && m->cache_io == io_type && m->cache_files.size() == nf;
@@ -1359,7 +1359,7 @@ int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_fil
   fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0, nullptr, 0, gbase};
   h_result->n_records = n;
   if (n >= 0xFFFFFFFFull) return h_result->status = LDB_ERR_ARG;   // record ids are 32-bit
-  m->cache_ok = true;
+  m->cache_ok = produce_cache;   // only ldb_merge_route_dev's scan is offered to the next apply
   m->cache_io = io_type;
   m->cache_files.assign(files, files + nf);
   m->cache_fdh = fdh;
@@ -1413,7 +1413,7 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   MHIP(hipEventRecord(m->ev[0], s));
   std::vector<FileDesc> fdh;
   uint64_t n = 0;
-  rc = merge_scan(ctx, m, nf, files, io_type, d_res, fdh, n, h_stats, h_result, s, ext_live);
+  rc = merge_scan(ctx, m, nf, files, io_type, d_res, fdh, n, h_stats, h_result, s, ext_live, false);
   if (rc != LDB_OK) return rc;
   if (ext_live && n && !last_in) return h_result->status = LDB_ERR_ARG;   // liveness flags for n records
   MHIP(hipEventRecord(m->ev[1], s));
@@ -1590,7 +1590,7 @@ extern "C" int ldb_merge_route_dev(ldb_ctx* ctx, int n_files, const ldb_merge_fi
   unsigned long long* d_cur = d_base + 2 * kMaxOwners;
   std::vector<FileDesc> fdh;
   uint64_t n = 0;
-  rc = merge_scan(ctx, m, nf, files, io_type, d_res, fdh, n, nullptr, h_result, s, false);
+  rc = merge_scan(ctx, m, nf, files, io_type, d_res, fdh, n, nullptr, h_result, s, false, true);
   if (rc != LDB_OK) return rc;
   rc = grow(&m->seqbuf, &m->seqbuf_bytes, align256(8 * (n + 1)));
   if (rc != LDB_OK) return rc;

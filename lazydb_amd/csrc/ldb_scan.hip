@@ -1501,6 +1501,15 @@ struct ldb_ctx {
   hipEvent_t pipes_ev = nullptr;
   bool pipes_ev_live = false;
   void* merge = nullptr;       // merge/GC workspace (ldb_merge.hip), created on first use
+  // host ranges page-locked through ldb_host_register: ldb_scan_file reads or writes a host buffer
+  // in place only when one of them covers it whole (the device mapping alone says nothing of its size)
+  std::vector<std::pair<uintptr_t, uint64_t>> regs;
+  bool registered(const void* p, uint64_t n) const {
+    const uintptr_t a = (uintptr_t)p;
+    for (const auto& r : regs)
+      if (a >= r.first && n <= r.second && a - r.first <= r.second - n) return true;
+    return false;
+  }
 };
 
 // internal hooks for ldb_merge.hip (not part of the C ABI)
@@ -2056,13 +2065,21 @@ int ldb_scan_files_dev(ldb_ctx* c, int n_files, const uint8_t* const* d_images, 
 int ldb_host_register(ldb_ctx* c, const void* h_ptr, uint64_t len) {
   if (!c || !h_ptr || !len) return LDB_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
-  return hipHostRegister(const_cast<void*>(h_ptr), len, hipHostRegisterDefault) == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+  if (hipHostRegister(const_cast<void*>(h_ptr), len, hipHostRegisterDefault) != hipSuccess) return LDB_ERR_HIP;
+  c->regs.emplace_back((uintptr_t)h_ptr, len);
+  return LDB_OK;
 }
 
 int ldb_host_unregister(ldb_ctx* c, const void* h_ptr) {
   if (!c || !h_ptr) return LDB_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
-  return hipHostUnregister(const_cast<void*>(h_ptr)) == hipSuccess ? LDB_OK : LDB_ERR_HIP;
+  if (hipHostUnregister(const_cast<void*>(h_ptr)) != hipSuccess) return LDB_ERR_HIP;
+  for (size_t i = 0; i < c->regs.size(); ++i)
+    if (c->regs[i].first == (uintptr_t)h_ptr) {
+      c->regs.erase(c->regs.begin() + (long)i);
+      break;
+    }
+  return LDB_OK;
 }
 
 int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
@@ -2077,15 +2094,18 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
   // (opt-in, LDB_DIRECT_IMAGE=1: measured slower than the staged copy, 23.7 vs 21.0 ms at config 2 --
   // the CUs' PCIe reads reach 52 GB/s against the DMA engines' 57.6)
   void* mapped = nullptr;
-  if (len && getenv("LDB_DIRECT_IMAGE") != nullptr &&
+  if (len && getenv("LDB_DIRECT_IMAGE") != nullptr && c->registered(h_image, len) &&
       (hipHostGetDevicePointer(&mapped, const_cast<uint8_t*>(h_image), 0) != hipSuccess || ((uintptr_t)mapped & 15))) {
     mapped = nullptr;   // pageable (the error is expected) or not 16-B aligned: the staged copy
     (void)hipGetLastError();
   }
   // a page-locked output array is written in place too (the tuple writes cross PCIe while the scan
-  // runs, in the other direction), else the tuples are staged on the device and copied back
+  // runs, in the other direction), else the tuples are staged on the device and copied back. Only a
+  // range this context registered for all cap tuples qualifies: a shorter registration would let the
+  // kernels write past the mapping
   void* out_mapped = nullptr;
-  if (cap && getenv("LDB_NO_DIRECT_OUT") == nullptr && hipHostGetDevicePointer(&out_mapped, h_out, 0) != hipSuccess) {
+  if (cap && getenv("LDB_NO_DIRECT_OUT") == nullptr && c->registered(h_out, cap * tsz) &&
+      hipHostGetDevicePointer(&out_mapped, h_out, 0) != hipSuccess) {
     out_mapped = nullptr;
     (void)hipGetLastError();
   }

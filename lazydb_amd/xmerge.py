@@ -281,6 +281,30 @@ def _all_gather_varlen(x, dist):
     return [b[:k].to(x.device) for b, k in zip(bufs, ns)]
 
 
+def check_fid_blocks(files, dist):
+    """Both cross-GPU merges take last-writer-wins order from the rank order (rank r's block below rank
+    r+1's): a round-robin or misordered split would give wrong liveness silently, so it is refused.
+    One all-gather of each rank's (min fid, max fid); an empty block is skipped."""
+    import torch
+    cpu = dist.get_backend() == "gloo"
+    dev = "cpu" if cpu else files[0][0].device if files else "cpu"
+    fids = [int(f) for _, f, _ in files]
+    if fids != sorted(fids) or len(set(fids)) != len(fids):
+        raise ValueError(f"rank {dist.get_rank()}: fids not strictly ascending: {fids}")
+    mine = torch.tensor([min(fids), max(fids)] if fids else [-1, -1], dtype=torch.int64, device=dev)
+    allb = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(allb, mine)
+    prev = None
+    for r, b in enumerate(allb):
+        lo, hi = int(b[0]), int(b[1])
+        if lo < 0:
+            continue
+        if prev is not None and lo <= prev:
+            raise ValueError(f"fid blocks not ascending in rank order: rank {r} starts at fid {lo}, "
+                             f"an earlier rank ends at {prev}")
+        prev = hi
+
+
 def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int, max_file_size: int, now: int,
                       io_type: int = N.FILEIO, fetch_pos: bool = True):
     """Config 5 over the ranks of torch.distributed: this rank's contiguous fid block `files`
@@ -290,6 +314,7 @@ def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
+    check_fid_blocks(files, dist)
     if world == 1:
         allsum = []
     else:   # rank r reads the summaries of ranks r+1..: nobody reads rank 0's
@@ -345,6 +370,7 @@ def merge_hashed_distributed(eng, files, active_fid: int, active_off: int, max_f
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
+    check_fid_blocks(files, dist)
     ro = route_phase(eng, files, world, io_type)
     rc = [ro["recs"][sum(ro["rec_splits"][:o]): sum(ro["rec_splits"][:o + 1])] for o in range(world)]
     kc = [ro["keys"][sum(ro["key_splits"][:o]): sum(ro["key_splits"][:o + 1])] for o in range(world)]

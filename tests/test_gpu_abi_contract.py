@@ -295,6 +295,16 @@ def test_host_register_path(gpu_engine):
                 eng.host_unregister(img)
         finally:
             eng.host_unregister(hout)
+        # registered for fewer bytes than cap tuples: staged and copied back, never written in place
+        # past the registration
+        half = hout[: hout.size // 2]
+        eng.host_register(half)
+        try:
+            hout[:] = np.zeros(1, dtype=N.INDEX_TUPLE)
+            res, tup = eng.scan_host(img, fid=7, out=hout)
+            same(res, tup, *coracle.scan(img, 0, fid=7))
+        finally:
+            eng.host_unregister(half)
 
 
 def test_fresh_context_first_merge_after_dirty_release():

@@ -150,3 +150,41 @@ def test_merge_distributed_two_ranks(hashed):
     assert got[1][6] == got[0][7] and got[-1][7] == (ref.end_fid, ref.end_off)
     n_seg = sum(len(g[4]) // coracle.MERGE_SEGMENT.itemsize for g in got)
     assert n_seg in (ref.n_segments, ref.n_segments + 1)   # + 1 when the rank boundary splits a run
+
+
+def _fid_block_worker(rank, world, port, q, blocks):
+    _init(rank, world, port)
+    try:
+        from lazydb_amd.xmerge import check_fid_blocks
+        files = [(None, f, False) for f in blocks[rank]]
+        try:
+            check_fid_blocks(files, dist)
+            q.put((rank, "ok"))
+        except ValueError as e:
+            q.put((rank, "refused: " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("blocks,ok", [
+    ([[0, 1], [2, 3]], True),
+    ([[0, 1], []], True),                      # an empty block is skipped
+    ([[0, 2], [1, 3]], False),                 # round-robin split: refused, not silently wrong
+    ([[2, 3], [0, 1]], False),                 # blocks descending in rank order
+])
+def test_fid_blocks_checked_gloo(blocks, ok):
+    """Both cross-GPU merges take last-writer-wins order from rank order: a split whose
+    fid blocks are not ascending by rank raises on every rank instead of producing wrong liveness."""
+    world = len(blocks)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fid_block_worker, args=(r, world, port, q, blocks)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert (got[r] == "ok") == ok, got
