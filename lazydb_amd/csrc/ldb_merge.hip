@@ -1269,7 +1269,9 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
   if (rc != LDB_OK) return rc;
   if (nf) MHIP(hipMemcpyAsync(rh.data(), d_res, sizeof(ldb_scan_result) * nf, hipMemcpyDeviceToHost, s));
   MHIP(hipStreamSynchronize(s));
-  return merge_scan_finish(ctx, m, nf, files, io_type, d_res, fdh, n, h_stats, h_result, s, sbase, rh, scan_hash);
+  rc = merge_scan_finish(ctx, m, nf, files, io_type, d_res, fdh, n, h_stats, h_result, s, sbase, rh, scan_hash);
+  if (!produce_cache) m->cache_ok = false;   // only ldb_merge_route_dev's scan is offered to the next apply
+  return rc;
 }
 
 // the replay scans file by file, dealt round-robin over the caller's context and the aux contexts
@@ -1359,7 +1361,7 @@ int merge_scan_finish(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_fil
   fdh[nf] = FileDesc{nullptr, nullptr, n, 0, 0, nullptr, 0, gbase};
   h_result->n_records = n;
   if (n >= 0xFFFFFFFFull) return h_result->status = LDB_ERR_ARG;   // record ids are 32-bit
-  m->cache_ok = produce_cache;   // only ldb_merge_route_dev's scan is offered to the next apply
+  m->cache_ok = true;
   m->cache_io = io_type;
   m->cache_files.assign(files, files + nf);
   m->cache_fdh = fdh;

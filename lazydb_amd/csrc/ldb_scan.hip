@@ -1,8 +1,9 @@
 // ldb_scan.hip — gfx950 kernels + C ABI of the LazyDB log-scan engine (liblazydb_gpu.so).
 //
 // Pipeline per file (all on one HIP stream, no host round trip):
-//   k_scan_main  : one wavefront per 5 KiB region, LDS-DMA ring staging, speculative
-//                  decode + CRC-32 per region (region_process, ldb_wave.h)   <- the hot kernel
+//   k_uniform    : the run prefix: equal-sized entries verified in parallel (then k_uniform_fill)
+//   k_scan_main  : one wavefront per run of 5 KiB regions, LDS-DMA ring staging, the chained lean path
+//                  (region_chained, ldb_chain.h) or the general routine inline (region_process, ldb_wave.h)
 //   k_link       : verify region-to-region links of the ReadLogEntry chain
 //   k_repair     : one wavefront re-walks the true chain from each broken link (rare)
 //   k_combine    : CRC-verify entries crossing region boundaries; terminal reduction
@@ -230,13 +231,15 @@ __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t rs, uint32_t off,
   __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, 0, 0);
 }
 // A 48-B region summary from wave-uniform values: lanes 0-2 store 16 B each (one instruction).
-__device__ __forceinline__ void store_summary(const Pipe& p, uint64_t r, const RegionSum& s, int lane) {
+// drop: the instruction still issues (k_scan_main's counted vmcnt waits) but writes nothing
+__device__ __forceinline__ void store_summary(const Pipe& p, uint64_t r, const RegionSum& s, int lane, bool drop = false) {
   uint32_t w[12];
   __builtin_memcpy(w, &s, sizeof(w));
   uint32_t d[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) d[j] = lane == 0 ? w[j] : (lane == 1 ? w[4 + j] : w[8 + j]);
-  store16(rsrc_of(p.rs + r, (uint32_t)sizeof(RegionSum)), lane < 3 ? (uint32_t)lane * 16u : kDrop, d[0], d[1], d[2], d[3]);
+  store16(rsrc_of(p.rs + r, (uint32_t)sizeof(RegionSum)), lane < 3 && !drop ? (uint32_t)lane * 16u : kDrop, d[0], d[1],
+          d[2], d[3]);
 }
 constexpr int kStoresPerRegion = 1;   // lean path: the summary (tuples are stored before the release)
 
@@ -379,8 +382,42 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // scan: grid.y = file, its Pipe from the device array pb (enqueue_scan_batch).
 #define LDB_PIPE_SELECT const Pipe p = kB ? pb[blockIdx.y] : p0
 
-__device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T) {
+// Header probes (the unpublished path only): threads 0..63 each compare one candidate's header bytes
+// with the memo (uni_header_ok), at entries 2^(t+2) for t < 24 and evenly over the candidates in [0,
+// probe_hi) for the rest. A candidate whose header differs fails, so K <= the smallest such e: *bound
+// (~0 when none) is that e, and workgroup 0 lowers K to it, so the waves stop below it from their
+// first batch instead of verifying the whole file before a run that breaks early is seen (the
+// reference bench's log breaks at entry 10, where its keys grow a digit: config 1, 0.19 ms -> ).
+__device__ __forceinline__ uint64_t uni_probe(const Pipe& p, const UniMemo& m, uint64_t probe_hi) {
+  __shared__ unsigned long long pb;
+  if (threadIdx.x == 0) pb = ~0ull;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t sz = m.sz, need = sz > 48 ? sz : 48;
+    const uint64_t ncand = p.len / sz + 1;
+    const uint64_t e = t < 24 ? (4ull << t) : (ncand * (uint64_t)(t - 23)) / 41;
+    const uint64_t x = e * sz;
+    if (e >= 2 && e < ncand && x + need <= probe_hi) {
+      auto word = [&](int i) -> uint32_t {
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b) {
+          const uint64_t a = x + 4 * (uint64_t)i + b;
+          w |= (a < p.len ? (uint32_t)p.img[a] : 0u) << (8 * b);
+        }
+        return w;
+      };
+      if (!uni_header_ok(m, word, x, p.len, p.io)) atomicMin(&pb, (unsigned long long)e);
+    }
+  }
+  __syncthreads();
+  return pb;
+}
+
+__device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T, uint64_t probe_hi,
+                                            uint64_t& bound) {
   __shared__ uint32_t xn[kUniTabWords / 1024];
+  bound = ~0ull;
   __shared__ uint32_t win[2][16];   // bytes [0, 64) and [sz, sz + 64) of the image, zero past len
   __shared__ int published;
   UniSetup* gsu = reinterpret_cast<UniSetup*>(p.uni);
@@ -411,6 +448,10 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_
   __syncthreads();
   if (su.g.ok) stage(1, su.m.sz);
   __syncthreads();
+  if (su.g.ok) {
+    bound = uni_probe(p, su.m, probe_hi);
+    if (bound != ~0ull && blockIdx.x == 0 && threadIdx.x == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)bound);
+  }
   if (threadIdx.x == 0) {
     if (su.g.ok) {
       const uint8_t* h = reinterpret_cast<const uint8_t*>(win[1]);
@@ -472,7 +513,7 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 // config 2/4/5 entries): no funnel shifts (22 v_alignbyte per batch at S = 11).
 template <int S, bool kChunk, bool kHash, bool kFill, bool kAl>
 __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint8_t* lp2, const uint32_t* T,
-                                          int lane, int wave, uint64_t a_lo, uint64_t a_hi) {
+                                          int lane, int wave, uint64_t a_lo, uint64_t a_hi, uint64_t bound) {
   if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
     a_lo = 0;
     a_hi = p.len;
@@ -510,7 +551,8 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
   const uint64_t nbatch = kChunk ? ~0ull : (p.len / sz + E) / E;   // !kChunk: ceil(ncand / E), ncand = len / sz + 1
   // K as last seen: the load issued in one batch is tested at the top of the next, so its latency hides
   // behind the batch (a batch past K only costs its own time: the run's tuples stop at K anyway)
-  v2u32 kv = {~0u, ~0u};   // K as loaded during the previous batch (vector value: read at the next top)
+  v2u32 kv = {(uint32_t)bound, (uint32_t)(bound >> 32)};   // K as loaded during the previous batch (vector value:
+                                                           // read at the next top); first the probes' bound
   const __amdgpu_buffer_rsrc_t krs = rsrc_of(p.dyn, 8);
   for (uint64_t b = b_first + (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
     if (kChunk && b * Esz > (all_hi ? p.len : a_hi)) break;   // wave-uniform: no candidate of this launch from here on
@@ -714,7 +756,8 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];   // combine tables (shift by 2^i P bytes)
   __shared__ UniSetup su;
   lp2_build(lp2, p.gtab);
-  if (!uni_prepare(p, su, comb)) return;   // (its __syncthreads also publish the LP2 block)
+  uint64_t bound;
+  if (!uni_prepare(p, su, comb, kChunk ? a_hi : p.len, bound)) return;   // (its __syncthreads also publish the LP2 block)
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -722,8 +765,8 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
 #define LDB_UNI_CASE(n)                                                                    \
   case n:                                                                                  \
-    if (al) uni_waves<n, kChunk, kHash, !kHash, true>(p, su, lp2, comb, lane, wave, a_lo, a_hi); \
-    else uni_waves<n, kChunk, kHash, !kHash, false>(p, su, lp2, comb, lane, wave, a_lo, a_hi); \
+    if (al) uni_waves<n, kChunk, kHash, !kHash, true>(p, su, lp2, comb, lane, wave, a_lo, a_hi, bound); \
+    else uni_waves<n, kChunk, kHash, !kHash, false>(p, su, lp2, comb, lane, wave, a_lo, a_hi, bound); \
     break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
@@ -807,7 +850,8 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];
   __shared__ UniSetup su;
   lp2_build(lp2, p.gtab);
-  if (!uni_prepare(p, su, comb)) return;
+  uint64_t bound;
+  if (!uni_prepare(p, su, comb, p.len, bound)) return;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -815,8 +859,8 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
 #define LDB_UNI_CASE(n)                                                                         \
   case n:                                                                                       \
-    if (al) uni_waves<n, false, false, true, true>(p, su, lp2, comb, lane, wave, 0, p.len);  \
-    else uni_waves<n, false, false, true, false>(p, su, lp2, comb, lane, wave, 0, p.len);    \
+    if (al) uni_waves<n, false, false, true, true>(p, su, lp2, comb, lane, wave, 0, p.len, bound);  \
+    else uni_waves<n, false, false, true, false>(p, su, lp2, comb, lane, wave, 0, p.len, bound);    \
     break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
@@ -862,21 +906,28 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     st.on = 2;
     st.x = chain_x0(p);
   }
+  // Warm-up: a run after the first starts kWarm regions early and processes those dry (no tuple, no
+  // summary), so the speculative entry has settled onto the chain by the run's first region (a chain
+  // from a false start falls back onto the true one within a few entries): far fewer broken links
+  // between runs for k_repair to walk.
+  const uint64_t warm = (count && rb > rf) ? min((uint64_t)kWarm, rb - rf) : 0;
+  const uint64_t r00 = rb - warm, total = count + warm;
   uint32_t n_fast = 0;
+  uint32_t declines = 0;        // consecutive lean declines (give-up mode, below)
   // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
   // has read it for the last time (buffer_free), so the DMA overlaps the summary, its stores and
   // the next region's wait.
   for (int b = 0; b < kNB; ++b)
-    if ((uint64_t)b < count) stage_dma(p.img, p.len, rb + (uint64_t)b, ring_lds + b * kBuf, lane);
-  for (uint64_t i = 0; i < count; ++i) {
+    if ((uint64_t)b < total) stage_dma(p.img, p.len, r00 + (uint64_t)b, ring_lds + b * kBuf, lane);
+  for (uint64_t i = 0; i < total; ++i) {
     // Wait for region i's DMA: vmcnt(N) retires all but the N youngest VM ops (issue order, global
     // ops only in this kernel). Younger than DMA(i) are, in steady state, the kStoresPerRegion
-    // buffer stores of iteration i-kNB (a finished lean region always issues exactly those after
-    // its release; a deferred region drains vmcnt on its atomic) and, for kNB > 1, the DMAs of regions
+    // buffer stores of iteration i-kNB (every region, lean or general, dry or not, issues exactly
+    // those after its next region's DMA) and, for kNB > 1, the DMAs of regions
     // i+1 .. i+kNB-1 (kG instructions each; their stores are not counted: conservative).
     // Near the end of the run fewer DMAs were issued after DMA(i) (none past the run's last region).
     {
-      const uint64_t left = count - 1 - i;
+      const uint64_t left = total - 1 - i;
       const uint64_t ahead = left < (uint64_t)(kNB - 1) ? left : (uint64_t)(kNB - 1);   // DMAs issued after DMA(i)
       if (ahead == (uint64_t)(kNB - 1) && i >= (uint64_t)kNB) wait_vm<(kNB - 1) * kG + kStoresPerRegion>();
       else if (kNB >= 3 && ahead >= 2) wait_vm<2 * kG>();
@@ -885,7 +936,8 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     }
     GpuWave::sync();
     wp.stamp(6);
-    const uint64_t r = rb + i;
+    const uint64_t r = r00 + i;
+    const bool dry = i < warm;   // warm-up: every store of the region dropped (still issued: the counted waits)
     const uint32_t slot = (uint32_t)(i % kNB);
     View v;
     v.buf = ring + slot * kBuf;
@@ -906,14 +958,14 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
         const SliceRows rows = load_rows(v, lane * kS);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         GpuWave::sync();
-        if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
+        if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
         cq.O = crc_slice_raw2(v.tab, rows);
         if (LDB_ABLATE >= 64) lane_scan(wp, v.tab, [&](int) -> ChainPriv& { return cq; });
         acc = wp.from(kLanes - 1, [&](int) { return cq.O; });
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         GpuWave::sync();
-        if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
+        if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
       }
       RegionSum s;
       s.start = kNone64; s.exitp = 0; s.soff = 0; s.status = kCont; s.count = 0; s.rpre = acc; s.rout = 0;
@@ -928,43 +980,75 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
       // (ldb_chain.h zero_region)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       GpuWave::sync();
-      if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
-      store_summary(p, r, zero_summary(), lane);
-      ++n_fast;
+      if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
+      store_summary(p, r, zero_summary(), lane, dry);
+      n_fast += dry ? 0u : 1u;
+      declines = 0;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       GpuWave::sync();
       continue;
     }
     bool released = false;
-    const bool fast = region_chained(
+    // after 2 declines in a row the next 8 regions go straight to region_process (one lean attempt
+    // after each 8: a log of short entries stops paying for attempts that cannot succeed)
+    const bool skip = declines >= 2 && declines < 10;
+    const bool fast = !skip && region_chained(
         wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },
         [&](bool valid, uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
-          store16(sc_rs, valid ? slot_ * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
+          store16(sc_rs, valid && !dry ? slot_ * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
         },
         [&] {   // the buffer's last read is behind us: stage the run's region i + kNB into it
           const uint64_t nx = i + kNB;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           GpuWave::sync();
-          if (nx < count) stage_dma(p.img, p.len, rb + nx, ring_lds + slot * kBuf, lane);
+          if (nx < total) stage_dma(p.img, p.len, r00 + nx, ring_lds + slot * kBuf, lane);
           released = true;
         },
-        [] {},   // a deferred region is re-read from global memory by k_fallback
-        [&](const RegionSum& s) { store_summary(p, r, s, lane); });
+        [] {},   // a declined region is reloaded below
+        [&](const RegionSum& s) { store_summary(p, r, s, lane, dry); });
     if (fast) {
-      ++n_fast;
+      n_fast += dry ? 0u : 1u;
+      declines = 0;
     } else {
-      // leave the region to k_fallback (the exact general routine); the run goes on speculatively
-      if (!released) {
+      // The exact general routine, inline (run_region, ldb_chain.h): entered at the chain's position
+      // when the chain is on, else speculating; its exit carries the chain into the next region. A
+      // log whose regions mostly decline (entries < kMinFast) is thus replayed chained within each
+      // wave's run instead of speculated region by region in a later kernel, whose wrong starts the
+      // repair then re-ran (1 GiB writer mix: 6039 region re-runs, 8.6 ms of k_repair).
+      if (released) {   // the ring slot may already hold region i + kNB: reload this one
+        wait_vm<0>();
+        GpuWave::sync();
+        for (int k = lane; k < (kW + kHalo) / 16; k += 64) {
+          const uint64_t off = v.R0 + (uint64_t)k * 16;
+          uint4 x = make_uint4(0, 0, 0, 0);
+          if (off < p.len) x = *reinterpret_cast<const uint4*>(p.img + off);
+          *reinterpret_cast<uint4*>(ring + slot * kBuf + kPre + k * 16) = x;
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         GpuWave::sync();
-        if (i + kNB < count) stage_dma(p.img, p.len, rb + i + kNB, ring_lds + slot * kBuf, lane);
       }
-      if (lane == 0) {
-        const uint32_t di = atomicAdd(&p.ctr[4], 1u);
-        if (di < p.nreg) p.defer[di] = (uint32_t)r;   // at most one deferral per region
-        else atomicOr(&p.ctr[5], 1u);                 // unreachable: reported as LDB_ERR_INTERNAL
-      }
-      st.on = 0;
+      uint32_t enter = kForceSpec;
+      if (st.on && st.x >= v.R0) enter = st.x - v.R0 < (uint64_t)v.rlen ? (uint32_t)(st.x - v.R0) : kForceNone;
+      LanePriv q;
+      region_process(
+          wp, v, wl->sh, enter, &wl->rs, [&](int) -> LanePriv& { return q; },
+          [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
+            store16(sc_rs, dry ? kDrop : slot_ * 16u, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
+          },
+          [] {});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      GpuWave::sync();
+      const RegionSum o = wl->rs;
+      // the next region's DMA, then this region's one summary store (the counted waits above)
+      if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
+      store_summary(p, r, o, lane, dry);
+      // continue chained only from a clean straddle-out whose register at the region end is known
+      st.on = o.status == kCont && o.start != kNone64 && o.sflag == kStraddle && o.exitp >= v.R0 + (uint64_t)kW &&
+              v.rlen == (uint32_t)kW;
+      st.x = o.exitp;
+      st.I = o.rout;
+      st.owner = o.scrc;
+      if (++declines >= 11) declines = 2;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
@@ -975,55 +1059,6 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
   if (lane == 0)
     for (int k = 0; k < kStampSlots; ++k) atomicAdd((unsigned long long*)&g_stamps[k], (unsigned long long)wp.acc[k]);
 #endif
-}
-
-// ---------------------------------------------------------------- k_fallback
-// The regions k_scan_main deferred, each through region_process (speculative entry, exactly as
-// the pre-chain pipeline did every region); k_link / k_repair / k_combine then verify them like
-// any other region. Staging is synchronous (rare regions).
-constexpr int kFbWaves = 16;   // 16 waves per CU (118 VGPRs, 149 KB of LDS)
-template <bool kB>
-__global__ __launch_bounds__(64 * kFbWaves) void k_fallback(Pipe p0, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
-  const uint32_t n = (uint32_t)min((uint64_t)p.ctr[4], p.nreg);
-  if ((uint64_t)blockIdx.x * kFbWaves >= n) return;   // no deferred region for this block
-  __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  copy_tables(tab, p.gtab);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  WaveLds* wl = reinterpret_cast<WaveLds*>(smem + wave * (sizeof(WaveLds) + kBuf));
-  uint8_t* buf = smem + wave * (sizeof(WaveLds) + kBuf) + sizeof(WaveLds);
-  GpuWave wp{lane};
-  for (uint32_t d = blockIdx.x * kFbWaves + wave; d < n; d += gridDim.x * kFbWaves) {
-    const uint64_t r = p.defer[d];
-    const uint64_t R0 = r * (uint64_t)kW;
-    for (int k = lane; k < (kW + kHalo) / 16; k += 64) {
-      const uint64_t off = R0 + (uint64_t)k * 16;
-      uint4 x = make_uint4(0, 0, 0, 0);
-      if (off < p.len) x = *reinterpret_cast<const uint4*>(p.img + off);
-      *reinterpret_cast<uint4*>(buf + kPre + k * 16) = x;
-    }
-    GpuWave::sync();
-    View v;
-    v.buf = buf;
-    v.tab = tab;
-    v.xw = p.xw;
-    v.gsh = p.gsh;
-    v.R0 = R0;
-    v.rlen = region_len(p, r);
-    v.len = p.len;
-    v.io = p.io;
-    ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
-    LanePriv q;
-    region_process(
-        wp, v, wl->sh, kForceSpec, &wl->rs, [&](int) -> LanePriv& { return q; },
-        [&](uint32_t slot, uint64_t pos, uint32_t k, uint32_t vv) { store_tuple(sc + slot, pos, k, vv); }, [] {});
-    write_region_wave(p, r, &wl->rs, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    GpuWave::sync();
-  }
 }
 
 // ---------------------------------------------------------------- k_link
@@ -1119,6 +1154,8 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
     const RegionSum s = wl->rs;
     if (lane == 0) {
       store_region(p, r, s);
+      if (serial_phase && s.status != kCont && s.start != kNone64)   // keep the terminal bits a superset
+        atomicOr((unsigned long long*)&term_bits(p)[r / 64], 1ull << (r % 64));
       // the serial repair reads its own summaries back coherently; a walker's reads are hints only,
       // and an agent-scope fence per region (an L2 writeback and invalidate on gfx950) cost ~1 ms a
       // region with many walkers writing: phase 1 fences once, before the done count
@@ -1156,7 +1193,13 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
                             if (lane == 0) won = atomicCAS(&claims[r], 0u, 1u) == 0u ? 1u : 0u;
                             return __shfl((int)won, 0) != 0;
                           },
-                          run);
+                          run,
+                          // a region the walk would re-run as covered but whose incoming link k_link
+                          // found intact is left alone: it sits on a chain with its predecessor, and a
+                          // walk from a false source (a speculated header whose size reaches far ahead)
+                          // re-running such regions started cascades of re-runs the serial pass redid
+                          // one by one (emulated, walkers in reverse order: 1898 + 1723 runs against 180)
+                          [&](uint64_t k) { return k > (uint64_t)rf && fl[k - (uint64_t)rf] == 0; });
     }
   }
   if (lane == 0 && runs) atomicAdd(&p.ctr[2], runs);
@@ -1171,15 +1214,30 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   uint32_t nb = 0;
-  for (uint64_t r = (uint64_t)rf + threadIdx.x; r < p.nreg; r += blockDim.x) {
-    bool bad = link_broken(p, r);
-    if ((int64_t)r == rf) {
-      const bool b0 = rd.start(r) != chain_x0(p);
-      fl[0] = b0 ? 1 : 0;
-      nb += b0 ? 1u : 0u;
+  // the flags again, 64 to a thread, with their bitmap word; then the terminal bits (flag_bits)
+  uint64_t* fb = flag_bits(p);
+  uint64_t* tb = term_bits(p);
+  const uint64_t nfw = (nflag + 63) / 64, ntw = (p.nreg + 63) / 64;
+  for (uint64_t w = threadIdx.x; w < nfw; w += blockDim.x) {
+    uint64_t bits = 0;
+    for (uint32_t b = 0; b < 64; ++b) {
+      const uint64_t i = 64 * w + b;
+      if (i >= nflag) break;
+      const bool bad = i == 0 ? rd.start((uint64_t)rf) != chain_x0(p) : link_broken(p, (uint64_t)rf - 1 + i);
+      fl[i] = bad ? 1 : 0;
+      bits |= (uint64_t)(bad ? 1u : 0u) << b;
     }
-    fl[r - rf + 1] = bad ? 1 : 0;
-    nb += bad ? 1u : 0u;
+    fb[w] = bits;
+    nb += (uint32_t)__builtin_popcountll(bits);
+  }
+  for (uint64_t w = (uint64_t)rf / 64 + threadIdx.x; w < ntw; w += blockDim.x) {
+    uint64_t bits = 0;
+    for (uint32_t b = 0; b < 64; ++b) {
+      const uint64_t r = 64 * w + b;
+      if (r >= p.nreg) break;
+      if (r >= (uint64_t)rf && p.rs[r].status != kCont && p.rs[r].start != kNone64) bits |= 1ull << b;
+    }
+    tb[w] = bits;
   }
   if (nb) atomicAdd(&p.ctr[7], nb);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1187,25 +1245,35 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (wave != 0 || __hip_atomic_load(&p.ctr[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   serial_phase = true;
-  auto next_fail = [&](int64_t done) -> int64_t {   // smallest flagged source > done
-    for (uint64_t b = (uint64_t)(done - (rf - 1) + 1); b < nflag; b += 64) {
-      const uint64_t m = __ballot(b + lane < nflag && fl[b + lane] != 0);
-      if (m) return rf - 1 + (int64_t)(b + __builtin_ctzll(m));
-    }
-    return INT64_MAX;
-  };
-  auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {
-    for (int64_t b = lo + 1 > rf ? lo + 1 : rf; b <= hi; b += 64) {
-      const int64_t r = b + lane;
-      bool t = false;
-      if (r >= 0 && r <= hi && (uint64_t)r < p.nreg) {
-        const int32_t st = __hip_atomic_load(&p.rs[r].status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = st != kCont && rd.start((uint64_t)r) != kNone64;
+  // the lowest set bit at index >= a in bitmap words [0, nw): a lane per word, 64 words per round
+  auto next_bit = [&](const uint64_t* bm, uint64_t nw, uint64_t a, bool coherent) -> uint64_t {
+    for (uint64_t w0 = a / 64; w0 < nw; w0 += 64) {
+      const uint64_t w = w0 + lane;
+      uint64_t bits = 0;
+      if (w < nw) bits = coherent ? __hip_atomic_load(&bm[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : bm[w];
+      if (w == a / 64) bits &= ~0ull << (a % 64);
+      const uint64_t m = __ballot(bits != 0);
+      if (m) {
+        const int L = __builtin_ctzll(m);
+        const uint64_t bw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), L) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, L);
+        return 64 * (w0 + (uint64_t)L) + (uint64_t)__builtin_ctzll(bw);
       }
-      const uint64_t m = __ballot(t ? 1 : 0);
-      if (m) return b + __builtin_ctzll(m);
     }
-    return -1;
+    return ~0ull;
+  };
+  auto next_fail = [&](int64_t done) -> int64_t {   // smallest flagged source > done
+    const uint64_t i = next_bit(fb, nfw, (uint64_t)(done - (rf - 1) + 1), false);
+    return i < nflag ? rf - 1 + (int64_t)i : INT64_MAX;
+  };
+  auto first_term = [&](int64_t lo, int64_t hi) -> int64_t {   // candidates from the bits, checked live
+    for (uint64_t a = (uint64_t)(lo + 1 > rf ? lo + 1 : rf);;) {
+      const uint64_t r = next_bit(tb, ntw, a, true);
+      if (r >= p.nreg || (int64_t)r > hi) return -1;
+      const int32_t st = __hip_atomic_load(&p.rs[r].status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (st != kCont && rd.start(r) != kNone64) return (int64_t)r;
+      a = r + 1;
+    }
   };
   const uint32_t n = repair(p, next_fail, rd, first_term, run);
   if (lane == 0 && n) atomicAdd(&p.ctr[2], n);
@@ -1450,8 +1518,6 @@ __global__ __launch_bounds__(256) void k_read_reduce(const uint4* __restrict__ p
 
 size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
 size_t repair_lds_bytes() { return kRepWaves * (sizeof(WaveLds) + kBuf); }
-size_t fallback_lds_bytes() { return kFbWaves * (sizeof(WaveLds) + kBuf); }
-static_assert(kFbWaves * (sizeof(WaveLds) + kBuf) + kTabBytes <= 160 * 1024, "k_fallback: LDS per workgroup");
 static_assert(kRepWaves * (sizeof(WaveLds) + kBuf) + kTabBytes + 64 <= 160 * 1024, "k_repair: LDS per workgroup");
 
 }  // namespace
@@ -1539,7 +1605,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_defer, o_ctr, o_tpos, o_dyn, o_uni, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_dyn, o_uni, o_blk, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -1562,7 +1628,6 @@ WsLayout layout(uint64_t len) {
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1) + 64);   // fail flags + walker claims (ldb_pipeline.h fail_flags)
-  L.o_defer = take(4 * L.nreg);
   L.o_scratch = take(sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg);
   L.total = o;
   return L;
@@ -1600,7 +1665,6 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.rs = reinterpret_cast<RegionSum*>(w + L.o_rs);
   p.scratch = reinterpret_cast<ldb_index_tuple*>(w + L.o_scratch);
   p.fail_src = reinterpret_cast<int64_t*>(w + L.o_fail);
-  p.defer = reinterpret_cast<uint32_t*>(w + L.o_defer);
   p.ctr = reinterpret_cast<uint32_t*>(w + L.o_ctr);
   p.tpos = reinterpret_cast<uint64_t*>(w + L.o_tpos);
   p.blk = reinterpret_cast<uint64_t*>(w + L.o_blk);
@@ -1754,7 +1818,6 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   hipLaunchKernelGGL(k_scan_main<false>, dim3(scan_main_grid(c, L.nreg)), dim3(64 * kWPB), main_lds_bytes(), s, p, nullptr);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   const int g256 = (int)((L.nreg + 255) / 256);
-  hipLaunchKernelGGL(k_fallback<false>, dim3(c->n_cu), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p, nullptr);
   hipLaunchKernelGGL(k_link<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
   hipLaunchKernelGGL(k_repair<false>, dim3(repair_grid(c, L.nreg)), dim3(64 * kRepWaves), repair_lds_bytes(), s, p,
                      nullptr);
@@ -1869,7 +1932,6 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
   hipLaunchKernelGGL(k_scan_main<true>, dim3(mg, n), dim3(64 * kWPB), main_lds_bytes(), s, p0, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
-  hipLaunchKernelGGL(k_fallback<true>, dim3(c->n_cu, n), dim3(64 * kFbWaves), fallback_lds_bytes(), s, p0, d_pipes);
   hipLaunchKernelGGL(k_link<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
   hipLaunchKernelGGL(k_repair<true>, dim3(repair_grid(c, max_nreg), n), dim3(64 * kRepWaves), repair_lds_bytes(), s,
                      p0, d_pipes);
@@ -1975,11 +2037,7 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
       hipFuncSetAttribute((const void*)k_repair<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)repair_lds_bytes()) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_repair<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)repair_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_fallback<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)fallback_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_fallback<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)fallback_lds_bytes()) != hipSuccess) {
+                          (int)repair_lds_bytes()) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }

@@ -113,7 +113,7 @@ struct Emu {
     v.io = p.io;
     return v;
   }
-  // one region of a wavefront's run (k_scan_main): the lean path, or deferred to k_fallback
+  // one region of a wavefront's run (k_scan_main): the lean path (false: the caller runs region_process)
   bool run_chained(const Pipe& p, uint64_t r, ChainState& st) {
     stage(p, r);
     const View v = view(p, r);
@@ -283,17 +283,41 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
   if (run_len == 0) {
     for (uint64_t r = rf; r < nreg; ++r) emu.run(p, r, kForceSpec);
   } else {
-    std::vector<uint64_t> deferred;
-    for (uint64_t r0 = rf; r0 < nreg; r0 += run_len) {   // k_scan_main
+    for (uint64_t r0 = rf; r0 < nreg; r0 += run_len) {   // k_scan_main: one wave's run
       ChainState st;
       chain_reset(st);
       if (r0 == rf) { st.on = 2; st.x = x0; }   // as k_scan_main: the replay's entry point
-      for (uint64_t r = r0; r < nreg && r < r0 + run_len; ++r) {
-        if (emu.run_chained(p, r, st)) ++n_fast;
-        else deferred.push_back(r);
+      const uint64_t warm = r0 > rf ? std::min<uint64_t>(kWarm, r0 - rf) : 0;   // dry warm-up regions
+      uint32_t declines = 0;
+      std::vector<RegionSum> keep;
+      for (uint64_t r = r0 - warm; r < nreg && r < r0 + run_len; ++r) {
+        const bool dry = r < r0;
+        const RegionSum saved = rs[r];   // a dry region's summary and tuples belong to the previous run
+        std::vector<ldb_index_tuple> saved_sc;
+        if (dry) saved_sc.assign(scratch.begin() + r * (uint64_t)kRegionCap, scratch.begin() + (r + 1) * (uint64_t)kRegionCap);
+        const bool skip = declines >= 2 && declines < 10;   // give-up mode
+        if (!skip && emu.run_chained(p, r, st)) {
+          n_fast += dry ? 0u : 1u;
+          declines = 0;
+        } else {
+          // the general routine inline (run_region, ldb_chain.h)
+          uint32_t enter = kForceSpec;
+          if (st.on && st.x >= r * (uint64_t)kW)
+            enter = st.x - r * (uint64_t)kW < (uint64_t)region_len(p, r) ? (uint32_t)(st.x - r * (uint64_t)kW) : kForceNone;
+          const RegionSum o = emu.run(p, r, enter);
+          st.on = o.status == kCont && o.start != kNone64 && o.sflag == kStraddle && o.exitp >= r * (uint64_t)kW + kW &&
+                  region_len(p, r) == (uint32_t)kW;
+          st.x = o.exitp;
+          st.I = o.rout;
+          st.owner = o.scrc;
+          if (++declines >= 11) declines = 2;
+        }
+        if (dry) {
+          rs[r] = saved;
+          std::copy(saved_sc.begin(), saved_sc.end(), scratch.begin() + r * (uint64_t)kRegionCap);
+        }
       }
     }
-    for (uint64_t r : deferred) emu.run(p, r, kForceSpec);   // k_fallback
   }
   // k_link: every flag of the pipeline (ldb_pipeline.h fail_flags), claims cleared
   uint8_t* fl = fail_flags(p);
@@ -333,13 +357,18 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
     // concurrently, the later one first)
     const bool walk = !(wm && wm[0] == '0'), rev = wm && wm[0] == 'r', win = wm && wm[0] == 'w';
     const uint64_t nwin = (nflag + 63) / 64;
+    const std::vector<uint8_t> fl0(fl, fl + nflag);   // k_link's flags, as the walkers read them
+    // as k_repair: hold covered re-runs of linked regions (bit 0); LDB_EMU_HOLD A/Bs the rules
+    const int hold = getenv("LDB_EMU_HOLD") ? atoi(getenv("LDB_EMU_HOLD")) : 1;
     for (uint64_t j = 0; walk && j < nflag; ++j) {
       const uint64_t i = rev ? nflag - 1 - j : win ? (nwin - 1 - j / 64) * 64 + j % 64 : j;
       if (i >= nflag) continue;
       if (i % 64 == 0 && i > 0 && fl[i - 1]) continue;   // as k_repair: left to the previous window's walker
       if (fl[i])
         walker_runs += walk_source(p, (int64_t)rf - 1 + (int64_t)i, Rd{&p},
-                                   [&](uint64_t r) { return claims[r]++ == 0; }, run);
+                                   [&](uint64_t r) { return claims[r]++ == 0; }, run,
+                                   [&](uint64_t r) { return (hold & 1) && r > rf && fl0[r - rf] == 0; },
+                                   [&](uint64_t r) { return (hold & 2) && r > rf && fl0[r - rf] == 0; });
     }
     n2 = relink();
   }
