@@ -38,6 +38,7 @@ struct Pipe {
   void* out;
   uint64_t cap;
   int kind;
+  int fill_main;              // k_scan_main writes the run prefix's INDEX tuples (no k_uniform_fill launch)
   ldb_scan_result* result;
 };
 

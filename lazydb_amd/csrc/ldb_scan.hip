@@ -879,6 +879,9 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
   // ctr[] was zeroed by the hipMemsetAsync that opens every pipeline (enqueue_scan); the terminal
   // words start at "none" (read only by the later kernels, stream-ordered after this one)
   if (blockIdx.x == 0 && threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
+  // the run prefix's tuples (uni_fill, k_uniform_fill's sweep) by the whole grid first: one launch and
+  // one launch gap fewer per scan, and a file the run covers leaves right after (config 4)
+  if (!kB && p.fill_main) uni_fill<false>(p, 0, p.len);
   {   // a workgroup whose waves have no region (the run prefix took them) leaves before the table copy
     const uint64_t rf0 = first_region(p), nr0 = p.nreg - rf0, nw0 = (uint64_t)gridDim.x * kWPB;
     if (rf0 + (uint64_t)blockIdx.x * kWPB * ((nr0 + nw0 - 1) / nw0) >= p.nreg) return;
@@ -1313,8 +1316,6 @@ __global__ __launch_bounds__(256) void k_combine(Pipe p0, const Pipe* __restrict
   if (threadIdx.x == 0) p.blk[blockIdx.x] = s_sum[0];   // blockDim == kBlkRegions
 }
 
-// ---------------------------------------------------------------- k_compact
-// One workgroup per 1024-region block; each wavefront copies whole regions.
 __device__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out) {
   struct G {
     const uint8_t* q;
@@ -1338,6 +1339,63 @@ __device__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out)
   *out = e;
 }
 
+// ---------------------------------------------------------------- k_serial
+// One lane walks the chain exactly like index.go:84-95 (global memory, byte-wise CRC).
+__device__ void serial_walk(const Pipe& p) {
+  struct G {
+    const uint8_t* q;
+    __device__ uint32_t operator()(int i) const { return q[i]; }
+  };
+  uint64_t off = chain_x0(p), n = run_k(p);   // after the run prefix (0, 0 on the serial test path)
+  int st;
+  for (;;) {
+    EntryInfo e;
+    if (read_eof(p.len, p.io, (int64_t)off, kMaxHeader)) {
+      e.status = LDB_EOF_WINDOW;
+    } else {
+      e = classify_entry(G{p.img + off}, p.len, p.io, off);
+    }
+    if (e.status != kCont) { st = e.status; break; }
+    uint32_t crc = 0;
+    if (e.h.size > 4) crc = ~g_crc_bytes(p, 0xFFFFFFFFu, off + 4, off + e.size);
+    if (crc != e.h.crc) { st = LDB_ERR_CRC; break; }
+    if (n < p.cap) {
+      if (p.kind == LDB_TUPLE_ENTRY) {
+        decode_entry_global(p, off, reinterpret_cast<ldb_entry*>(p.out) + n);
+      } else {
+        ldb_index_tuple t;
+        t.pos = pack_pos(off, e.h);
+        t.k_size = e.h.k_size;
+        t.v_size = e.h.v_size;
+        reinterpret_cast<ldb_index_tuple*>(p.out)[n] = t;
+      }
+    }
+    ++n;
+    off += e.size;
+  }
+  ldb_scan_result res;
+  res.status = n > p.cap ? LDB_ERR_CAPACITY : st;
+  res.fid = p.fid;
+  res.n_entries = n;
+  res.end_off = off;
+  res.n_repairs = 0;
+  res.n_regions = (uint32_t)p.nreg;
+  res.n_fast = 0;
+  res.n_broken = 0;
+  res.n_run = run_k(p);
+  *p.result = res;
+}
+template <bool kB>
+__global__ __launch_bounds__(64) void k_serial(Pipe p0, int only_on_overflow, const Pipe* __restrict__ pb) {
+  LDB_PIPE_SELECT;
+  if (threadIdx.x != 0) return;
+  if (only_on_overflow && !p.ctr[1]) return;
+  serial_walk(p);
+}
+
+// ---------------------------------------------------------------- k_compact
+// One workgroup per 1024-region block; each wavefront copies whole regions.
+
 // One workgroup per kBlkRegions regions: its output base is the sum of the earlier blocks'
 // counts (k_combine), its regions are scanned in LDS, and tuples are copied flat (thread j of
 // the block's output range finds its region by binary search). The block holding the terminal
@@ -1345,6 +1403,10 @@ __device__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out)
 template <bool kB>
 __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
+  if (p.ctr[1]) {   // a region overflowed its tuple slots (k_combine): the serial walker redoes the scan
+    if (blockIdx.x == 0 && threadIdx.x == 0) serial_walk(p);
+    return;
+  }
   __shared__ uint32_t s_off[kBlkRegions + 1];
   __shared__ uint32_t s_wsum[kBlkRegions / 64];
   __shared__ uint64_t s_part[kBlkRegions / 64];
@@ -1440,57 +1502,6 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __
     if (p.kind == LDB_TUPLE_ENTRY) decode_entry_global(p, t.pos & 0xFFFFFFFFFFull, reinterpret_cast<ldb_entry*>(p.out) + dst);
     else reinterpret_cast<ldb_index_tuple*>(p.out)[dst] = t;
   }
-}
-
-// ---------------------------------------------------------------- k_serial
-// One lane walks the chain exactly like index.go:84-95 (global memory, byte-wise CRC).
-template <bool kB>
-__global__ __launch_bounds__(64) void k_serial(Pipe p0, int only_on_overflow, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
-  if (threadIdx.x != 0) return;
-  if (only_on_overflow && !p.ctr[1]) return;
-  struct G {
-    const uint8_t* q;
-    __device__ uint32_t operator()(int i) const { return q[i]; }
-  };
-  uint64_t off = chain_x0(p), n = run_k(p);   // after the run prefix (0, 0 on the serial test path)
-  int st;
-  for (;;) {
-    EntryInfo e;
-    if (read_eof(p.len, p.io, (int64_t)off, kMaxHeader)) {
-      e.status = LDB_EOF_WINDOW;
-    } else {
-      e = classify_entry(G{p.img + off}, p.len, p.io, off);
-    }
-    if (e.status != kCont) { st = e.status; break; }
-    uint32_t crc = 0;
-    if (e.h.size > 4) crc = ~g_crc_bytes(p, 0xFFFFFFFFu, off + 4, off + e.size);
-    if (crc != e.h.crc) { st = LDB_ERR_CRC; break; }
-    if (n < p.cap) {
-      if (p.kind == LDB_TUPLE_ENTRY) {
-        decode_entry_global(p, off, reinterpret_cast<ldb_entry*>(p.out) + n);
-      } else {
-        ldb_index_tuple t;
-        t.pos = pack_pos(off, e.h);
-        t.k_size = e.h.k_size;
-        t.v_size = e.h.v_size;
-        reinterpret_cast<ldb_index_tuple*>(p.out)[n] = t;
-      }
-    }
-    ++n;
-    off += e.size;
-  }
-  ldb_scan_result res;
-  res.status = n > p.cap ? LDB_ERR_CAPACITY : st;
-  res.fid = p.fid;
-  res.n_entries = n;
-  res.end_off = off;
-  res.n_repairs = 0;
-  res.n_regions = (uint32_t)p.nreg;
-  res.n_fast = 0;
-  res.n_broken = 0;
-  res.n_run = run_k(p);
-  *p.result = res;
 }
 
 // Read-only reduction over the image (ldb_read_ceiling): four 16-B loads in flight per thread.
@@ -1674,16 +1685,26 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.out = out;
   p.cap = cap;
   p.kind = kind;
+  p.fill_main = 0;
   p.result = res;
   return p;
 }
 
-// Record the end of the pipeline just enqueued on `s` (see ldb_ctx::ws_ev).
+// Note the stream of the pipeline just enqueued (see ldb_ctx::ws_ev). The event itself is recorded
+// only when a pipeline on another stream wants the workspace (ws_wait): everything enqueued on the
+// old stream by then includes that pipeline, and a scan stream used alone pays no marker packet per
+// pipeline (one was ~10 us between the config-4 pipelines).
 int fence_ws(ldb_ctx* c, hipStream_t s) {
-  if (!c->ws_ev && hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess) return LDB_ERR_HIP;
-  LDB_HIP(hipEventRecord(c->ws_ev, s));
   c->ws_stream = s;
   c->ws_ev_live = true;
+  return LDB_OK;
+}
+// the workspace is free for stream s once the last pipeline enqueued on another stream has finished
+int ws_wait(ldb_ctx* c, hipStream_t s) {
+  if (!c->ws_ev_live || c->ws_stream == s) return LDB_OK;
+  if (!c->ws_ev && hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess) return LDB_ERR_HIP;
+  LDB_HIP(hipEventRecord(c->ws_ev, c->ws_stream));
+  LDB_HIP(hipStreamWaitEvent(s, c->ws_ev, 0));
   return LDB_OK;
 }
 
@@ -1710,6 +1731,12 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
   LDB_HIP(hipEventRecord(ev->e0, s));
   *out = ev;
   return LDB_OK;
+}
+
+// the control words every region pipeline starts from (enqueue_scan)
+__global__ __launch_bounds__(64) void k_init(uint32_t* ctr, uint64_t* dyn, uint64_t dyn_val) {
+  if (threadIdx.x < 8) ctr[threadIdx.x] = 0u;
+  if (threadIdx.x < 4) dyn[threadIdx.x] = dyn_val;
 }
 
 // persistent k_scan_main workgroups: exactly those resident at once (LDS-limited), so no second
@@ -1763,14 +1790,16 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   Pipe p = make_pipe(c, L, d_img, len, fid, io, kind, d_out, cap, d_res);
   p.hash_out = hash_out;
   // the workspace is free once the last pipeline enqueued on another stream has finished
-  if (c->ws_ev_live && c->ws_stream != s) LDB_HIP(hipStreamWaitEvent(s, c->ws_ev, 0));
+  rc = ws_wait(c, s);
+  if (rc != LDB_OK) return rc;
   // every pipeline starts from zeroed control words, in stream order: nothing depends on how the
   // previous pipeline on this workspace ended, or on what a fresh allocation held
-  LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
+  // (the region pipeline's control words are set by k_init below; the serial path's here)
   const bool chunked = plan && plan->n > 0 && !serial && len >= (uint64_t)kMaxHeader && !no_run;
   if (plan && !chunked)   // nothing overlaps the copy: the whole image first
     for (int i = 0; i < plan->n; ++i) LDB_HIP(hipStreamWaitEvent(s, plan->ev[i], 0));
   if (serial || len < (uint64_t)kMaxHeader) {
+    LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
     LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
     LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0, 32, s));   // no run prefix: the walk starts at 0
     hipLaunchKernelGGL(k_serial<false>, dim3(1), dim3(64), 0, s, p, 0, nullptr);
@@ -1781,7 +1810,9 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   rc = timing_begin(c, s, &ev);
   if (rc != LDB_OK) return rc;
   // the run prefix: K = ~0 until k_uniform lowers it to the first entry outside the run
-  LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, no_run ? 0 : 0xFF, 32, s));   // K = ~0, setup not published
+  // ctr zero; K = ~0 and the setup not published (no_run: K = 0): one tiny launch instead of two
+  // memsets (a blit launch each, ~10 us of the config-4 step between them)
+  hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, s, p.ctr, p.dyn, no_run ? 0ull : ~0ull);
   if (!no_run) {
     auto launch = [&](uint64_t lo, uint64_t hi) {
       const int ug = uniform_grid(c, hi - lo);
@@ -1807,8 +1838,12 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
     } else {
       launch(0, len);
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-      if (kind == LDB_TUPLE_INDEX && !p.hash_out)
-        hipLaunchKernelGGL(k_uniform_fill<false>, dim3(fill_grid(c, len)), dim3(kFillThreads), 0, s, p, 0, len);
+      // the run's INDEX tuples are written by k_scan_main's grid before its regions (p.fill_main);
+      // timed (ldb_kernel_timing), by k_uniform_fill in series, for the split
+      if (kind == LDB_TUPLE_INDEX && !p.hash_out) {
+        if (ev) hipLaunchKernelGGL(k_uniform_fill<false>, dim3(fill_grid(c, len)), dim3(kFillThreads), 0, s, p, 0, len);
+        else p.fill_main = 1;
+      }
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
   } else if (ev) {
@@ -1823,7 +1858,6 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
                      nullptr);
   hipLaunchKernelGGL(k_combine<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
   hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)L.nblk), dim3(kBlkRegions), 0, s, p, nullptr);
-  hipLaunchKernelGGL(k_serial<false>, dim3(1), dim3(64), 0, s, p, 1, nullptr);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
@@ -1900,7 +1934,8 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   }
   const Pipe* d_pipes = reinterpret_cast<const Pipe*>(c->ws);
   const Pipe p0{};   // unused by the kB instances
-  if (c->ws_ev_live && c->ws_stream != s) LDB_HIP(hipStreamWaitEvent(s, c->ws_ev, 0));
+  rc = ws_wait(c, s);
+  if (rc != LDB_OK) return rc;
   LDB_HIP(hipMemcpyAsync(const_cast<Pipe*>(d_pipes), c->h_pipes, sizeof(Pipe) * (size_t)nf, hipMemcpyHostToDevice, s));
   LDB_HIP(hipEventRecord(c->pipes_ev, s));
   c->pipes_ev_live = true;
@@ -1937,7 +1972,6 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
                      p0, d_pipes);
   hipLaunchKernelGGL(k_combine<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
   hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)nblk, n), dim3(kBlkRegions), 0, s, p0, d_pipes);
-  hipLaunchKernelGGL(k_serial<true>, dim3(1, n), dim3(64), 0, s, p0, 1, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
@@ -2067,6 +2101,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   for (const ldb_ctx::EvTriple& t : c->evs) {
     (void)hipEventDestroy(t.e0);
     (void)hipEventDestroy(t.eu);
+    (void)hipEventDestroy(t.ef);
     (void)hipEventDestroy(t.e1);
     (void)hipEventDestroy(t.e2);
   }
