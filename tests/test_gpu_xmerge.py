@@ -165,3 +165,18 @@ def test_xmerge_hashed_config5_8_ranks(eng, engs):
     ref = check(eng, files, dict(active_fid=16, active_off=ends[15], max_file_size=256 << 20, now=MC.NOW), 8,
                 hashed_engs=engs)
     assert ref.n_live == n // 2
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_xmerge_hashed_all_empty_keys(eng, engs, world):
+    """every record has the empty key (str.go accepts nil keys; the golden fixtures hold
+    them). The owner of "" receives route records but no key bytes (pad16(0) = 0), which must still
+    resolve: last-writer-wins over the one key, an SDelete in between."""
+    from tests.merge_cases import _log
+    a = _log([dict(key=b"", value=b"v%d" % i) for i in range(5)], 4096)
+    b = _log([dict(key=b"", value=b"", stat=1)] + [dict(key=b"", value=b"w%d" % i) for i in range(3)], 4096)
+    c = np.zeros(4096, dtype=np.uint8)   # the empty active file
+    files = [(a, 1, True), (b, 2, True), (c, 3, False)]
+    ref = check(eng, files, dict(active_fid=3, active_off=0, max_file_size=1 << 20, now=MC.NOW), world,
+                hashed_engs=engs)
+    assert ref.n_live == 1 and ref.n_emit == 1
