@@ -841,12 +841,30 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   if (tail <= 4) { r.sflag |= kSkip; r.rout = 0; }
   store(r);
   st = nm;
-  st.on = tail > 4 ? 1u : 0u;   // after a kSkip straddler the next region starts speculative
+  st.on = tail > 4 ? 1u : 2u;   // after a kSkip straddler: the entry is known, its CRC state not (k_combine)
   st.x = r.exitp;
   st.I = r.rout;
   st.owner = r.scrc;
   wp.stamp(15);
   return true;
+}
+
+// The chain after region_process entered with `enter`: on (1) from a clean straddle-out whose register
+// at the region end is known; entry known but CRC state not (2, the next region's straddler is then
+// verified by k_combine, as after the run prefix) from any other straddle-out, or through a region the
+// open entry covers; off (speculate) after a terminal status. Round 3: rounds 1-2 speculated after
+// every kSkip / kNoCrc straddle-out too, and each wrong speculation was a walker's stretch of re-runs.
+LDB_HD void chain_after_general(ChainState& st, const RegionSum& o, const View& v, uint32_t enter) {
+  if (o.status == kCont && o.start != kNone64 && o.exitp >= v.R0 + (uint64_t)kW) {
+    st.on = (o.sflag == kStraddle && v.rlen == (uint32_t)kW) ? 1u : 2u;
+    st.x = o.exitp;
+    st.I = o.rout;
+    st.owner = o.scrc;
+  } else if (o.status == kCont && o.start == kNone64 && enter == kForceNone && st.on) {
+    st.on = 2;   // still inside the entry that covers the region: x unchanged
+  } else {
+    st.on = 0;
+  }
 }
 
 // One region of a wavefront's run: the chained fast path when the chain state allows it,
@@ -863,13 +881,7 @@ LDB_HD bool run_region(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, ChainSt
   uint32_t enter = kForceSpec;
   if (st.on && st.x >= v.R0) enter = st.x - v.R0 < (uint64_t)v.rlen ? (uint32_t)(st.x - v.R0) : kForceNone;
   region_process(wp, v, sh, enter, out, priv, emit, buffer_free);
-  const RegionSum r = *out;
-  // continue chained only from a clean straddle-out whose register at the region end is known
-  st.on = r.status == kCont && r.start != kNone64 && r.sflag == kStraddle && r.exitp >= v.R0 + (uint64_t)kW &&
-          v.rlen == (uint32_t)kW;
-  st.x = r.exitp;
-  st.I = r.rout;
-  st.owner = r.scrc;
+  chain_after_general(st, *out, v, enter);
   return false;
 }
 

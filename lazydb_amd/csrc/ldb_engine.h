@@ -86,6 +86,11 @@ constexpr uint32_t kNoCrc = 4u;      // its decoded header size <= 4: getEntryCr
 
 constexpr int kOverflow = 100;       // internal: region needs more than kRegionCap tuple slots
 constexpr uint64_t kWarm = 2;        // k_scan_main: regions a wave's run starts early, processed dry (chain warm-up)
+#ifndef LDB_SWALLOW_LOG2
+#define LDB_SWALLOW_LOG2 18
+#endif
+constexpr uint64_t kWarmSwallow = 1ull << LDB_SWALLOW_LOG2;   // (256 KiB) a speculated entry whose chain leaves a region inside an
+                                                // entry reaching this far ahead is taken for false (k_scan_main)
 
 // ---------------------------------------------------------------- table building (host)
 inline void build_tables(uint32_t* tab) {

@@ -992,6 +992,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
       continue;
     }
     bool released = false;
+    const bool spec_entry = !st.on;   // this region's entry is speculated (run start, warm-up, after a terminal)
     // after 2 declines in a row the next 8 regions go straight to region_process (one lean attempt
     // after each 8: a log of short entries stops paying for attempts that cannot succeed)
     const bool skip = declines >= 2 && declines < 10;
@@ -1045,14 +1046,14 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
       // the next region's DMA, then this region's one summary store (the counted waits above)
       if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
       store_summary(p, r, o, lane, dry);
-      // continue chained only from a clean straddle-out whose register at the region end is known
-      st.on = o.status == kCont && o.start != kNone64 && o.sflag == kStraddle && o.exitp >= v.R0 + (uint64_t)kW &&
-              v.rlen == (uint32_t)kW;
-      st.x = o.exitp;
-      st.I = o.rout;
-      st.owner = o.scrc;
+      chain_after_general(st, o, v, enter);
       if (++declines >= 11) declines = 2;
     }
+    // A speculated entry that leaves the chain inside an entry reaching more than kWarmSwallow past
+    // this region: most likely a false header (random value bytes decode to random varint sizes),
+    // whose covered regions a walker would later re-run one after another. The next region speculates
+    // afresh instead; a true entry that long only costs that region a speculation.
+    if (spec_entry && st.on && st.x > v.R0 + kWarmSwallow) chain_reset(st);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     GpuWave::sync();
     wp.stamp(7);

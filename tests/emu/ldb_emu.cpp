@@ -135,8 +135,7 @@ struct Emu {
           sc[slot].v_size = vv;
         },
         [&] { released = true; }, [] {}, [&](const RegionSum& rs) { store_region(p, r, rs); });
-    if (!fast) st.on = 0;
-    (void)released;
+    (void)released;   // a decline leaves st untouched: the caller runs region_process from it (k_scan_main)
     EMU_FOLD();
     return fast;
   }
@@ -292,10 +291,15 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
       std::vector<RegionSum> keep;
       for (uint64_t r = r0 - warm; r < nreg && r < r0 + run_len; ++r) {
         const bool dry = r < r0;
+        const bool spec_entry = !st.on;
         const RegionSum saved = rs[r];   // a dry region's summary and tuples belong to the previous run
         std::vector<ldb_index_tuple> saved_sc;
         if (dry) saved_sc.assign(scratch.begin() + r * (uint64_t)kRegionCap, scratch.begin() + (r + 1) * (uint64_t)kRegionCap);
         const bool skip = declines >= 2 && declines < 10;   // give-up mode
+        static const long dbg_r = getenv("LDB_EMU_DBG_R") ? atol(getenv("LDB_EMU_DBG_R")) : -1;
+        if ((long)r == dbg_r || (long)r + 1 == dbg_r)
+          fprintf(stderr, "region %llu dry=%d st.on=%u st.x=%llu declines=%u skip=%d\n", (unsigned long long)r, (int)dry,
+                  st.on, (unsigned long long)st.x, declines, (int)skip);
         if (!skip && emu.run_chained(p, r, st)) {
           n_fast += dry ? 0u : 1u;
           declines = 0;
@@ -305,13 +309,13 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
           if (st.on && st.x >= r * (uint64_t)kW)
             enter = st.x - r * (uint64_t)kW < (uint64_t)region_len(p, r) ? (uint32_t)(st.x - r * (uint64_t)kW) : kForceNone;
           const RegionSum o = emu.run(p, r, enter);
-          st.on = o.status == kCont && o.start != kNone64 && o.sflag == kStraddle && o.exitp >= r * (uint64_t)kW + kW &&
-                  region_len(p, r) == (uint32_t)kW;
-          st.x = o.exitp;
-          st.I = o.rout;
-          st.owner = o.scrc;
+          chain_after_general(st, o, emu.view(p, r), enter);
           if (++declines >= 11) declines = 2;
         }
+        if (spec_entry && st.on && st.x > r * (uint64_t)kW + kWarmSwallow) chain_reset(st);   // as k_scan_main
+        if ((long)r == dbg_r)
+          fprintf(stderr, "  -> start=%llu exit=%llu status=%d sflag=%u | st.on=%u st.x=%llu\n", (unsigned long long)rs[r].start,
+                  (unsigned long long)rs[r].exitp, rs[r].status, rs[r].sflag, st.on, (unsigned long long)st.x);
         if (dry) {
           rs[r] = saved;
           std::copy(saved_sc.begin(), saved_sc.end(), scratch.begin() + r * (uint64_t)kRegionCap);

@@ -10,8 +10,11 @@ import torch
 from lazydb_amd import Engine, _native as N
 from oracle import coracle
 
-cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-if cfg == 3:
+cfg = sys.argv[1] if len(sys.argv) > 1 else "2"
+cfg = cfg if cfg == "w" else int(cfg)
+if cfg == "w":   # the writer-realistic mix (bench.py leg w)
+    img, n, end = coracle.gen_writer_log(1 << 30, 30)
+elif cfg == 3:
     img, n, end = coracle.gen_log(8 << 30, 2, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
 else:
     img, n, end = coracle.gen_log(1 << 30, 1, ksize=64, vsize=256)
