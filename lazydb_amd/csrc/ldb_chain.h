@@ -553,8 +553,9 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   if (known) {
     const uint64_t xr64 = st.x - v.R0;
     if (xr64 >= (uint64_t)kW) {   // the open entry runs through the region: no header can start here
-      if (spec) return LDB_DECLINE(1);
-      covered(true);
+      // entry known but CRC state not (st.on == 2): the region's raw register goes to k_combine, which
+      // carries the open entry's check across it; the chain state stays as it is
+      covered(!spec);
       return true;
     }
     xr = (uint32_t)xr64;

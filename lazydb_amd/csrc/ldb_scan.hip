@@ -991,6 +991,12 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
       GpuWave::sync();
       continue;
     }
+    // The warm-up ended inside an entry covering the run's whole first region: most often a false
+    // header the warm-up speculated onto (its size a random varint), which would leave the run on a
+    // false chain until its CRC fails and a walker re-runs the run region by region. The run's first
+    // region speculates afresh instead (1 GiB writer mix, emulated: 6 broken links and 190 serial
+    // re-runs -> none); a true entry that long costs one speculation, which finds it covered.
+    if (i == warm && warm && st.on && st.x >= v.R0 + (uint64_t)kW) chain_reset(st);
     bool released = false;
     const bool spec_entry = !st.on;   // this region's entry is speculated (run start, warm-up, after a terminal)
     // after 2 declines in a row the next 8 regions go straight to region_process (one lean attempt

@@ -292,6 +292,8 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
       for (uint64_t r = r0 - warm; r < nreg && r < r0 + run_len; ++r) {
         const bool dry = r < r0;
         const bool spec_entry = !st.on;
+        // as k_scan_main: the warm-up ended inside an entry that covers the run's whole first region
+        if (r == r0 && warm && st.on && st.x >= r0 * (uint64_t)kW + kW) chain_reset(st);
         const RegionSum saved = rs[r];   // a dry region's summary and tuples belong to the previous run
         std::vector<ldb_index_tuple> saved_sc;
         if (dry) saved_sc.assign(scratch.begin() + r * (uint64_t)kRegionCap, scratch.begin() + (r + 1) * (uint64_t)kRegionCap);
