@@ -489,18 +489,23 @@ LDB_HD uint32_t find_start(const View& v, int B, int Eeff, Hot* h) {
     const int64_t lim = (int64_t)(v.len - v.R0) - kMaxHeader + (v.io == LDB_IO_MMAP ? 0 : 1);
     if (lim < (int64_t)pe) pe = lim < (int64_t)B ? B : (int)lim;
   }
-  // stat bytes of positions B..B+79 are bytes B+4..B+83: dwords 1..20 of the rows at B
+  // stat bytes of positions B..B+79 are bytes B+4..B+83: dwords 1..20 of the rows at B. A plausible
+  // start also has a non-negative ExpiredAt, so the byte after its stat byte is even (zig-zag sign
+  // bit): candidates whose next byte is odd are dropped before the decode (about half the stat-byte
+  // hits in random value bytes; the plausible set is unchanged, an odd byte fails the check anyway)
   const Row16* row = reinterpret_cast<const Row16*>(v.buf + kPre + B);
-  uint32_t cand[3] = {0, 0, 0};  // bit i <-> position B + i
+  uint32_t dw[24];
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     const Row16 q = row[k];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int qd = 4 * k + j - 1;   // dword qd + 1 of the slice holds stat bytes of positions 4qd..4qd+3
-      if (qd < 0 || qd >= kS / 4) continue;
-      cand[qd >> 3] |= msb4(small_bytes(q.w[j])) << (4 * (qd & 7));
-    }
+    for (int j = 0; j < 4; ++j) dw[4 * k + j] = q.w[j];
+  }
+  uint32_t cand[3] = {0, 0, 0};  // bit i <-> position B + i
+#pragma unroll
+  for (int qd = 0; qd < kS / 4; ++qd) {   // dword qd + 1 holds the stat bytes of positions 4qd..4qd+3
+    const uint32_t w = dw[qd + 1], nx = (w >> 8) | (dw[qd + 2] << 24);
+    cand[qd >> 3] |= msb4(small_bytes(w) & ~((nx << 7) & 0x80808080u)) << (4 * (qd & 7));
   }
   const int nvalid = pe - B;  // positions [B, pe) are decodable
   uint32_t m0 = cand[0], m1 = cand[1], m2 = cand[2];
