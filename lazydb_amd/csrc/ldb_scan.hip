@@ -368,6 +368,8 @@ __device__ __forceinline__ uint32_t ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 #endif
 constexpr uint64_t kUniReady = 0x5E7A11ED5E7A11EDull;   // dyn[2]: the setup in p.uni is complete
 constexpr uint64_t kUniSetupBytes = 1024;                // UniSetup, then the combine tables
+constexpr uint32_t kUniWin = 8192;                       // image bytes uni_prepare stages (entries 0 and 1)
+static_assert(kUniMaxSize + 48 <= kUniWin, "entry 1's header lies in the staged window");
 static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // The first k_uniform launch of a pipeline derives the run's parameters in every workgroup (no
 // separate setup launch) and its workgroup 0 publishes them to p.uni, so the later launches of a
@@ -388,6 +390,9 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // (~0 when none) is that e, and workgroup 0 lowers K to it, so the waves stop below it from their
 // first batch instead of verifying the whole file before a run that breaks early is seen (the
 // reference bench's log breaks at entry 10, where its keys grow a digit: config 1, 0.19 ms -> ).
+#ifndef LDB_UNI_NOPROBE
+#define LDB_UNI_NOPROBE 0   // A/B: no header probes
+#endif
 __device__ __forceinline__ uint64_t uni_probe(const Pipe& p, const UniMemo& m, uint64_t probe_hi) {
   __shared__ unsigned long long pb;
   if (threadIdx.x == 0) pb = ~0ull;
@@ -416,9 +421,7 @@ __device__ __forceinline__ uint64_t uni_probe(const Pipe& p, const UniMemo& m, u
 
 __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T, uint64_t probe_hi,
                                             uint64_t& bound) {
-  __shared__ uint32_t xn[kUniTabWords / 1024];
   bound = ~0ull;
-  __shared__ uint32_t win[2][16];   // bytes [0, 64) and [sz, sz + 64) of the image, zero past len
   __shared__ int published;
   UniSetup* gsu = reinterpret_cast<UniSetup*>(p.uni);
   const uint32_t* gT = reinterpret_cast<const uint32_t*>(p.uni + kUniSetupBytes);
@@ -432,29 +435,26 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_
     for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) T[e] = gT[e];
     return true;
   }
-  auto stage = [&](int w, uint64_t at) {
-    if (threadIdx.x < 64) {
-      const uint64_t a = at + threadIdx.x;
-      reinterpret_cast<uint8_t*>(win[w])[threadIdx.x] = a < p.len ? p.img[a] : 0;
+  // bytes [0, kUniWin) of the image, zero past len, staged once: entry 0's header and entry 1's (sz <=
+  // kUniMaxSize) come from the same round trip (round 2 staged them in two dependent rounds)
+  __shared__ uint32_t win[kUniWin / 4];
+  for (uint32_t i = threadIdx.x; i < kUniWin / 4; i += blockDim.x) {
+    const uint64_t a0 = 4ull * i;
+    uint32_t w = 0;
+    if (a0 + 4 <= p.len) {
+      w = *reinterpret_cast<const uint32_t*>(p.img + a0);
+    } else {
+      for (uint32_t k = 0; k < 4; ++k) w |= (a0 + k < p.len ? (uint32_t)p.img[a0 + k] : 0u) << (8 * k);
     }
-  };
-  stage(0, 0);
+    win[i] = w;
+  }
   __syncthreads();
+  const uint8_t* wb = reinterpret_cast<const uint8_t*>(win);
   if (threadIdx.x == 0) {
-    const uint8_t* h = reinterpret_cast<const uint8_t*>(win[0]);
-    su.m = uni_memo([&](int i) -> uint32_t { return i < 64 ? h[i] : 0u; }, p.len, p.io);
+    su.m = uni_memo([&](int i) -> uint32_t { return i < (int)kUniWin ? wb[i] : 0u; }, p.len, p.io);
     su.g = su.m.ok ? uni_geometry(p.xw, (uint32_t)(su.m.sz - 4)) : UniGeo{};
-  }
-  __syncthreads();
-  if (su.g.ok) stage(1, su.m.sz);
-  __syncthreads();
-  if (su.g.ok) {
-    bound = uni_probe(p, su.m, probe_hi);
-    if (bound != ~0ull && blockIdx.x == 0 && threadIdx.x == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)bound);
-  }
-  if (threadIdx.x == 0) {
     if (su.g.ok) {
-      const uint8_t* h = reinterpret_cast<const uint8_t*>(win[1]);
+      const uint8_t* h = wb + su.m.sz;   // sz + 40 < kUniWin
       auto word = [&](int i) -> uint32_t {
         return (uint32_t)h[4 * i] | ((uint32_t)h[4 * i + 1] << 8) | ((uint32_t)h[4 * i + 2] << 16) |
                ((uint32_t)h[4 * i + 3] << 24);
@@ -462,24 +462,41 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_
       if (!uni_header_ok(su.m, word, su.m.sz, p.len, p.io)) su.g.ok = 0;
     }
     if (su.g.ok) {
-      if (su.g.G <= kUniDirectG)
-        for (uint32_t d = 1; d < su.g.G; ++d) xn[d - 1] = p.xw[d * su.g.P];   // d P <= 7 * 96 < kW
-      else
-        for (uint32_t i = 0; i < su.g.lg; ++i) xn[i] = p.xw[su.g.P << i];
-      if (LDB_UNI_CH2) xn[kUniHalfTab] = p.xw[8 * (su.g.S - su.g.S / 2)];   // the second chain's length
       if (blockIdx.x == 0) p.dyn[1] = su.m.sz;
     } else if (blockIdx.x == 0) {
       p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
     }
   }
   __syncthreads();
-  if (su.g.ok)
+  if (su.g.ok && !LDB_UNI_NOPROBE) {
+    bound = uni_probe(p, su.m, probe_hi);
+    if (bound != ~0ull && blockIdx.x == 0 && threadIdx.x == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)bound);
+  }
+  if (su.g.ok) {
+    // The combine tables T[t][q][b] = shift(b << 8q, n_t bytes) are linear in b: 32 basis registers per
+    // table (one multmodp each, one thread each), then every entry an xor of its bits' basis values.
+    // (Round 2: one 32-step multmodp per entry, 3 x 1024 of them per workgroup: most of the setup.)
+    __shared__ uint32_t basis[kUniTabWords / 1024][32];
+    const uint32_t nt = uni_ntab(su.g);
+    const uint32_t t = threadIdx.x >> 5, bit = threadIdx.x & 31u;
+    if (t < nt) {
+      const uint32_t xt = su.g.G <= kUniDirectG ? p.xw[(t + 1) * su.g.P] : p.xw[su.g.P << t];   // d P <= 7 * 96 < kW
+      basis[t][bit] = multmodp(xt, 1u << bit);
+    }
+    if (LDB_UNI_CH2 && threadIdx.x >= 1024 - 32) {   // the second chain's length (kUniHalfTab)
+      basis[kUniHalfTab][bit] = multmodp(p.xw[8 * (su.g.S - su.g.S / 2)], 1u << bit);
+    }
+    __syncthreads();
     for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) {
-      if (e >= uni_ntab(su.g) * 1024u && e < kUniHalfTab * 1024u) continue;
-      const uint32_t v = multmodp(xn[e >> 10], (e & 255u) << (8 * ((e >> 8) & 3u)));
+      if (e >= nt * 1024u && e < kUniHalfTab * 1024u) continue;
+      const uint32_t tt = e >> 10, q = (e >> 8) & 3u, b = e & 255u;
+      uint32_t v = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i) v ^= ((b >> i) & 1u) ? basis[tt][8 * q + i] : 0u;
       T[e] = v;
       if (blockIdx.x == 0) const_cast<uint32_t*>(gT)[e] = v;
     }
+  }
   if (blockIdx.x == 0) {   // publish: the tables and the setup, then the flag (release)
     if (threadIdx.x == 0) *gsu = su;
     __threadfence();
@@ -755,10 +772,25 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
   __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];   // combine tables (shift by 2^i P bytes)
   __shared__ UniSetup su;
+#ifdef LDB_STAMPS   // setup cost: slot 9 the LP2 block, slot 17 uni_prepare (thread 0 of every workgroup)
+  uint64_t t0_, t1_, t2_;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_) :: "memory");
+#endif
   lp2_build(lp2, p.gtab);
+#ifdef LDB_STAMPS
+  __syncthreads();
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_) :: "memory");
+#endif
   uint64_t bound;
   if (!uni_prepare(p, su, comb, kChunk ? a_hi : p.len, bound)) return;   // (its __syncthreads also publish the LP2 block)
   __syncthreads();
+#ifdef LDB_STAMPS
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2_) :: "memory");
+  if (threadIdx.x == 0) {
+    atomicAdd((unsigned long long*)&g_stamps[9], (unsigned long long)(t1_ - t0_));
+    atomicAdd((unsigned long long*)&g_stamps[17], (unsigned long long)(t2_ - t1_));
+  }
+#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool al = (su.m.sz & 3u) == 0 && (su.g.t & 3u) == 0;   // every window and header dword-aligned

@@ -30,6 +30,8 @@ def build(name: str) -> str:
         defs = ["-DLDB_SCAN_BPERM=1", "-DLDB_LATE_RELEASE=1"]
     elif name.startswith("abl"):
         defs = [f"-DLDB_ABLATE={int(name[3:])}"]
+    elif name == "stampsnoprobe":
+        defs = ["-DLDB_STAMPS=1", "-DLDB_UNI_NOPROBE=1"]
     elif name == "nowin":
         defs = ["-DLDB_NO_WINCHK=1"]
     elif name.startswith("git_"):   # the library as of a commit (A/B timing on one box)

@@ -1,0 +1,32 @@
+"""k_uniform setup phases from an LDB_STAMPS build (tools/build_variants.py stamps): s_memtime cycles per
+workgroup for the LP2 block and for uni_prepare. usage: LAZYDB_GPU_LIB=.../var_stamps.so python tools/uni_stamps.py"""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from lazydb_amd import Engine, _native as N
+from oracle import coracle
+
+eng = Engine(0)
+L = N.lib()
+L.ldb_debug_stamps.argtypes = [C.c_void_p, C.c_int]
+buf = np.zeros(18, np.uint64)
+for name, (img, n, end) in (("cfg4-shape 64 MiB", coracle.gen_log(64 << 20, 1, ksize=64, vsize=256)),
+                             ("cfg1 bench log", coracle.gen_bench_log(512 << 20, 1, n_entries=500_000))):
+    d = torch.from_numpy(img).cuda()
+    io = 1 if name.startswith("cfg1") else 0
+    eng.scan_dev(d, io_type=io, cap=n + 16)
+    torch.cuda.synchronize()
+    L.ldb_debug_stamps(buf.ctypes.data, 1)
+    reps = 10
+    for _ in range(reps):
+        eng.scan_dev(d, io_type=io, cap=n + 16)
+    torch.cuda.synchronize()
+    L.ldb_debug_stamps(buf.ctypes.data, 1)
+    nwg = 256
+    print(f"{name}: LP2 block {buf[9] / (reps * nwg):8.0f} cyc/WG, uni_prepare {buf[17] / (reps * nwg):8.0f} cyc/WG "
+          f"(s_memtime: 100 MHz on gfx9 -> x10 ns)")
