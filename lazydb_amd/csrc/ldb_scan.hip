@@ -1455,9 +1455,8 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __
   int32_t ts = term_status(T);
   if (T == ~0ull) { tp = p.len; ts = LDB_ERR_MALFORMED; }  // unreachable: the chain always stops
   const uint64_t rf = first_region(p), K = run_k(p);      // the run prefix's tuples are out[0, K)
-  const uint64_t b = blockIdx.x, r0 = b * kBlkRegions;
   if (rf >= p.nreg) {   // the replay stops right after the run: io.EOF at x0 (log_file.go:117-122)
-    if (b == 0 && tid == 0) {
+    if (blockIdx.x == 0 && tid == 0) {
       ldb_scan_result res;
       res.status = LDB_EOF_WINDOW;
       res.fid = p.fid;
@@ -1475,7 +1474,11 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __
   }
   const uint64_t regT = tp / kW;                          // may be nreg when tp == len == nreg * kW
   const uint64_t lastR = regT < p.nreg ? regT : p.nreg - 1;
-  if (r0 > lastR) return;
+  // a capped grid strides over the blocks (a file the run prefix took whole launches few workgroups)
+  const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
+  for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+  const uint64_t r0 = b * kBlkRegions;
+  if (r0 > lastR) break;
   // base = sum of the counts of every earlier block (all their regions precede the terminal)
   uint64_t part = 0;
   for (uint64_t i = tid; i < b; i += kBlkRegions) part += p.blk[i];
@@ -1540,6 +1543,8 @@ __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __
     const ldb_index_tuple t = p.scratch[(r0 + lo) * (uint64_t)kRegionCap + (j - s_off[lo])];
     if (p.kind == LDB_TUPLE_ENTRY) decode_entry_global(p, t.pos & 0xFFFFFFFFFFull, reinterpret_cast<ldb_entry*>(p.out) + dst);
     else reinterpret_cast<ldb_index_tuple*>(p.out)[dst] = t;
+  }
+  __syncthreads();   // s_off / s_wsum / s_part are reused by the next block
   }
 }
 
@@ -1896,7 +1901,8 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   hipLaunchKernelGGL(k_repair<false>, dim3(repair_grid(c, L.nreg)), dim3(64 * kRepWaves), repair_lds_bytes(), s, p,
                      nullptr);
   hipLaunchKernelGGL(k_combine<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
-  hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)L.nblk), dim3(kBlkRegions), 0, s, p, nullptr);
+  hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)std::min<uint64_t>(L.nblk, 4ull * c->n_cu)), dim3(kBlkRegions), 0, s, p,
+                     nullptr);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
@@ -2010,7 +2016,8 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   hipLaunchKernelGGL(k_repair<true>, dim3(repair_grid(c, max_nreg), n), dim3(64 * kRepWaves), repair_lds_bytes(), s,
                      p0, d_pipes);
   hipLaunchKernelGGL(k_combine<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
-  hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)nblk, n), dim3(kBlkRegions), 0, s, p0, d_pipes);
+  hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)std::min<uint64_t>(nblk, 4ull * c->n_cu), n), dim3(kBlkRegions), 0, s,
+                     p0, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
