@@ -1979,6 +1979,15 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   }
   const Pipe* d_pipes = reinterpret_cast<const Pipe*>(c->ws);
   const Pipe p0{};   // unused by the kB instances
+  // the region pipeline and the repair walkers: the chip's resident workgroups dealt over the files,
+  // not one file's grid per file (16 files of 256 MiB launched 16 x 256 k_scan_main workgroups that
+  // queue behind each other even when every run prefix covered its file; LDB_BATCH_SPREAD=0: A/B)
+  static const bool spread = getenv("LDB_BATCH_SPREAD") == nullptr || atoi(getenv("LDB_BATCH_SPREAD")) != 0;
+  int rg = repair_grid(c, max_nreg);
+  if (spread) {
+    mg = std::min(mg, std::max(1, (scan_main_grid(c, ~0ull >> 8) + nf - 1) / nf));
+    rg = std::min(rg, std::max(1, (c->n_cu + nf - 1) / nf));
+  }
   rc = ws_wait(c, s);
   if (rc != LDB_OK) return rc;
   LDB_HIP(hipMemcpyAsync(const_cast<Pipe*>(d_pipes), c->h_pipes, sizeof(Pipe) * (size_t)nf, hipMemcpyHostToDevice, s));
@@ -2013,7 +2022,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   hipLaunchKernelGGL(k_scan_main<true>, dim3(mg, n), dim3(64 * kWPB), main_lds_bytes(), s, p0, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
   hipLaunchKernelGGL(k_link<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
-  hipLaunchKernelGGL(k_repair<true>, dim3(repair_grid(c, max_nreg), n), dim3(64 * kRepWaves), repair_lds_bytes(), s,
+  hipLaunchKernelGGL(k_repair<true>, dim3(rg, n), dim3(64 * kRepWaves), repair_lds_bytes(), s,
                      p0, d_pipes);
   hipLaunchKernelGGL(k_combine<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
   hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)std::min<uint64_t>(nblk, 4ull * c->n_cu), n), dim3(kBlkRegions), 0, s,
