@@ -58,6 +58,11 @@ def parse():
                     help="extra single-GPU configs timed after the main line at N = 1 (comma list; '' = none): "
                          "1 the reference bench's log (Mmap), 2, 3, w the writer-realistic mix, 5 the merge")
     ap.add_argument("--leg-steps", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="after the W warm-up steps, keep stepping (untimed) until this much wall time has passed: "
+                         "the GPU's clocks move for the first ~20 ms of sustained load (a kernel trace of 64 "
+                         "back-to-back config-4 scans: k_uniform 0.74 -> 0.95 -> 0.755 ms, profiles/r04_dvfs_transient.txt), "
+                         "so K timed steps right after 5 warm-up steps measure the transient, not the rate")
     ap.add_argument("--pmc", type=int, default=1,
                     help="measure roofline.traffic in this run: a rocprofv3 --pmc FETCH_SIZE child process scans "
                          "the same image (N = 1, rank 0; 0: skip)")
@@ -339,6 +344,7 @@ def merge_leg(eng, args, dev):
                 live_cap=int(r.n_records) + 16, fetch_pos=False)
     for _ in range(2):
         eng.merge_dev(files, **kw, **caps)
+    settle(lambda: eng.merge_dev(files, **kw, **caps), args.settle_ms)
     torch.cuda.synchronize()
     ph = np.zeros(3)
     steps = args.leg_steps
@@ -413,6 +419,7 @@ def main_merge(args):
                 live_cap=int(r.n_records) + 16, fetch_pos=False)
     for _ in range(args.warmup):
         eng.merge_dev(files, **kw, **caps)
+    settle(lambda: eng.merge_dev(files, **kw, **caps), args.settle_ms)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -591,6 +598,8 @@ def main_xmerge(args):
             verified = bool(verified and int(ends_ok.item())) if rank == 0 else verified
     for _ in range(args.warmup):
         step_once()
+    for _ in range(8 if args.settle_ms > 0 else 0):   # a fixed count: step_once holds collectives, so every
+        step_once()                                    # rank must take the same number of steps
     if world > 1:
         dist.barrier()
     sync()
@@ -619,6 +628,29 @@ def main_xmerge(args):
         dist.destroy_process_group()
 
 
+def settle(step, ms: float, max_steps: int = 2000):
+    """Untimed steps after the warm-up until `ms` of wall time has passed (at least one synchronised
+    round): the device's clocks settle after the first ~20 ms of back-to-back launches (DVFS; see
+    --settle-ms). Steps are enqueued in rounds of 8 and each round is synchronised, so the host never
+    runs far ahead of the device."""
+    import torch
+    if ms <= 0:
+        return 0
+    t0, n = time.perf_counter(), 0
+    while n < max_steps:
+        for _ in range(8):
+            step()
+        n += 8
+        torch.cuda.synchronize()
+        if (time.perf_counter() - t0) * 1e3 >= ms:
+            break
+    settle.last_steps = n
+    return n
+
+
+settle.last_steps = 0
+
+
 class Resident:
     """One log-file image in HBM with its output tuple array and result slot."""
 
@@ -645,12 +677,14 @@ def timed_scans(eng, S, fid, args, steps, world, stream):
 
     for _ in range(args.warmup):
         step()
+    settle(step, args.settle_ms)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    timed_scans.enqueue_ms = (time.perf_counter() - t0) * 1e3   # host time to enqueue the K steps (diagnostic)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -843,11 +877,14 @@ def main():
         e2e["GB_per_s"] = round(int(r.end_off) / (e2e["ms"] * 1e-3) / 1e9, 2)
     ms_step = t_max / args.steps * 1e3
     value = tot_bytes / (t_max / args.steps) / 2**30
-    traffic, traffic_src = (measure_traffic(img, cap, args, kname) if rank == 0 and world == 1 and args.io == 0
-                            else (None, "not measured (N > 1 or Mmap rule)"))
+    # every rank's dominant kernel, so the N > 1 line carries a roofline per rank (one all-gather)
+    per_rank = multi.gather_floats([kbytes, kms, run_ms, main_ms, total_ms, t / args.steps * 1e3], dev)
+    traffic, traffic_src = (measure_traffic(img, cap, args, kname) if rank == 0 and args.io == 0
+                            else (None, "not measured (Mmap rule)"))
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(img, end_expect, args.cpu_sample_mib)
+    if rank == 0 and not args.no_cpu:
+        # N > 1: a quarter of the sample (rank 0's host share; the other ranks wait at the final barrier)
+        cpu = cpu_baseline(img, end_expect, args.cpu_sample_mib if world == 1 else max(64, args.cpu_sample_mib // 4))
     legs = []
     if world == 1 and args.legs:
         del S
@@ -909,6 +946,15 @@ def main():
             "fast_regions": int(r.n_fast),
             "regions": int(r.n_regions),
         }
+        line["settle_steps"] = settle.last_steps
+        line["host_enqueue_ms_per_step"] = round(timed_scans.enqueue_ms / args.steps, 4)
+        if world > 1:
+            line["roofline"]["per_rank"] = [
+                {"rank": i, "kernel": kname, "avg_kernel_ms": round(v[1], 4),
+                 "achieved": round(v[0] / (v[1] * 1e-3) / 1e9, 1) if v[1] > 0 else None,
+                 "frac": round(v[0] / (v[1] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if v[1] > 0 else None,
+                 "avg_k_uniform_ms": round(v[2], 4), "avg_k_scan_main_ms": round(v[3], 4),
+                 "avg_pipeline_ms": round(v[4], 4), "wall_ms_per_step": round(v[5], 4)} for i, v in enumerate(per_rank)]
         if gather:
             line["gather"] = gather
         if e2e:

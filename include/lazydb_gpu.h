@@ -131,7 +131,10 @@ uint64_t ldb_workspace_bytes(uint64_t len);
  * bytes can fault. The values of those bytes never affect any result (tests/test_gpu_abi_contract.py
  * poisons them).  d_out: device array of `cap` tuples of `tuple_kind`.  d_result: device
  * ldb_scan_result written at the end of the stream work.
- * Asynchronous with respect to the host: enqueues work on `stream` and returns. */
+ * Asynchronous with respect to the host: enqueues work on `stream` and returns. A context may be
+ * driven from several streams: a call on a stream other than the previous call's first waits for
+ * the context's earlier work (a device-wide drain when the earlier stream is the caller's, which may
+ * have been destroyed since), so streams may be created and destroyed freely between calls. */
 int ldb_scan_file_dev(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, uint32_t fid, int io_type,
                       int tuple_kind, void* d_out, uint64_t cap, ldb_scan_result* d_result, void* stream);
 
@@ -145,7 +148,9 @@ int ldb_scan_file(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t f
  * the runtime's pageable staging. Optional: ldb_scan_file works on any host memory. A tuple array
  * registered here for at least cap tuples is written in place by the kernels; any other output
  * array (unregistered, pinned elsewhere, or registered shorter than cap tuples) is staged on the
- * device and copied back. */
+ * device and copied back. Likewise only an image registered through THIS context for all `len`
+ * bytes may be read in place by the kernels (the opt-in direct-image mode); any other image is
+ * copied to HBM first (at DMA rate when the runtime knows it as pinned, however it was pinned). */
 int ldb_host_register(ldb_ctx* ctx, const void* h_ptr, uint64_t len);
 int ldb_host_unregister(ldb_ctx* ctx, const void* h_ptr);
 

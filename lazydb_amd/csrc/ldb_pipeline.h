@@ -32,13 +32,13 @@ struct Pipe {
   uint64_t* tpos;             // [0] min terminal position, [1] its status (packed with position)
   uint64_t* blk;              // per kBlkRegions-region block: count sum (k_combine)
   uint64_t* dyn;              // [0] K: entries of the equal-sized run k_uniform verified, [1] their size,
-                              // [2] kUniReady once a k_uniform launch published its setup to `uni`
+                              // [2] kUniReady once a k_uniform launch published its setup to `uni`,
+                              // [3] kUniDone once the run prefix ended the scan (uni_finish), [4] its counter
   uint8_t* uni;               // the run prefix's published setup (memo, slicing, combine tables)
   uint64_t* hash_out;         // merge mode (nullable): ldb::key_hash_w of the key of run entry k at [k]
   void* out;
   uint64_t cap;
   int kind;
-  int fill_main;              // k_scan_main writes the run prefix's INDEX tuples (no k_uniform_fill launch)
   ldb_scan_result* result;
 };
 

@@ -35,7 +35,9 @@ using namespace ldb;
 namespace {
 
 #ifndef LDB_WPB
-#define LDB_WPB 16
+// 16 waves per CU fit beside the round-3 table block (62.8 KB); the LP2 block (70 KB, ldb_engine.h)
+// leaves room for 14 staging rings of 6.1 KiB
+#define LDB_WPB (LDB_LP2 ? 14 : 16)
 #endif
 #ifndef LDB_NB
 #define LDB_NB 1
@@ -763,6 +765,74 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
   }
 }
 
+// kPost: the run's INDEX tuples, written by each workgroup once its waves' verify loops are done, as a
+// dense sweep of its own slice of the tuple array (so the stores of early workgroups overlap the loads
+// of the others, and no fill launch follows). A tuple's bytes depend only on its index (uni_pos of
+// e sz and the memo's sizes), not on who verified the entry, so the slice covers every e below K as
+// visible now and below cap: every e below the final K is written, and one at or past the final K (K
+// may still drop) lies beyond n_entries, where the region pipeline writes its own tuples from K on.
+// (Round 4: per-wave stores of each wave's own batches, 4 scattered 256-B pieces per instruction, cost
+// 61 us at config 4 against 33 for the separate dense sweep.)
+__device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniMemo& m) {
+  __syncthreads();
+  const uint64_t sz = m.sz, ncand = p.len / sz + 1;
+  const uint64_t K = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t n = K < ncand ? K : ncand;
+  n = n < p.cap ? n : p.cap;
+  const uint64_t per = (ncand + gridDim.x - 1) / gridDim.x;
+  const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  ldb_index_tuple* out = reinterpret_cast<ldb_index_tuple*>(p.out);
+  for (uint64_t e = lo + threadIdx.x; e < hi; e += blockDim.x) store_tuple(out + e, uni_pos(m, e * sz), m.k, m.v);
+}
+
+// The device path's run prefix, finished (the last k_uniform workgroup to be done, after every
+// workgroup's K update): when the chain stops right at x0 = K sz -- the header window there is
+// unreadable (io.EOF), or it decodes as the zero sentinel (ErrLogEndOfFile), a key/value read past the
+// bound (io.EOF) or a malformed header (log_file.go:116-139) -- the scan is complete: this writes the
+// ldb_scan_result and sets dyn[3] = kUniDone, and the region pipeline's kernels leave at once. A file
+// the run covers to its terminal (BASELINE configs 2, 4, 5) then pays no region kernel work.
+constexpr uint64_t kUniDone = 0xD0E5CA11D0E5CA11ull;
+__device__ __forceinline__ void uni_finish(const Pipe& p, uint64_t sz) {
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_last = atomicAdd((unsigned long long*)&p.dyn[4], 1ull) == (unsigned long long)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last || threadIdx.x != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  p.dyn[4] = 0;
+  const uint64_t K = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (K == ~0ull) return;   // (unreachable: the candidate at or past len always fails)
+  const uint64_t x0 = K * sz;
+  int32_t st;
+  if (read_eof(p.len, p.io, (int64_t)x0, kMaxHeader)) {
+    st = LDB_EOF_WINDOW;
+  } else {
+    struct G {
+      const uint8_t* q;
+      __device__ uint32_t operator()(int i) const { return q[i]; }
+    };
+    st = classify_entry(G{p.img + x0}, p.len, p.io, x0).status;
+  }
+  if (st != LDB_EOF_WINDOW && st != LDB_EOF_SENTINEL && st != LDB_EOF_KV && st != LDB_ERR_MALFORMED) return;
+  ldb_scan_result res;
+  res.status = K > p.cap ? LDB_ERR_CAPACITY : st;
+  res.fid = p.fid;
+  res.n_entries = K;
+  res.end_off = x0;
+  res.n_repairs = 0;
+  res.n_regions = 0;
+  res.n_fast = 0;
+  res.n_broken = 0;
+  res.n_run = K;
+  *p.result = res;
+  p.dyn[3] = kUniDone;
+}
+// the region pipeline's kernels: nothing to do once the run prefix finished the scan
+__device__ __forceinline__ bool scan_done(const Pipe& p) { return p.dyn[3] == kUniDone; }
+
 // kChunk: a_lo, a_hi: image bytes [0, a_hi) are in place; candidates not already taken by a launch
 // with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
 // LDS: the 64 KiB LP2 block, the combine tables and the setup (~90 KiB): one workgroup of 16 waves per
@@ -794,6 +864,7 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool al = (su.m.sz & 3u) == 0 && (su.g.t & 3u) == 0;   // every window and header dword-aligned
+  constexpr bool kPost = !kChunk && !kHash;
   switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
 #define LDB_UNI_CASE(n)                                                                    \
   case n:                                                                                  \
@@ -805,6 +876,8 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
 #undef LDB_UNI_CASE
     default: break;
   }
+  if (kPost && p.kind == LDB_TUPLE_INDEX) uni_post_fill(p, su.m);
+  if (!kChunk || a_hi >= p.len) uni_finish(p, su.m.sz);
 }
 static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
 
@@ -908,12 +981,10 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
   // folds the table base into the ds_read offset field
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // ctr[] was zeroed by the hipMemsetAsync that opens every pipeline (enqueue_scan); the terminal
-  // words start at "none" (read only by the later kernels, stream-ordered after this one)
+  if (scan_done(p)) return;   // the run prefix ended on the chain's terminal (uni_finish)
+  // ctr[] was zeroed by k_init, which opens every pipeline (enqueue_scan); the terminal words start
+  // at "none" (read only by the later kernels, stream-ordered after this one)
   if (blockIdx.x == 0 && threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
-  // the run prefix's tuples (uni_fill, k_uniform_fill's sweep) by the whole grid first: one launch and
-  // one launch gap fewer per scan, and a file the run covers leaves right after (config 4)
-  if (!kB && p.fill_main) uni_fill<false>(p, 0, p.len);
   {   // a workgroup whose waves have no region (the run prefix took them) leaves before the table copy
     const uint64_t rf0 = first_region(p), nr0 = p.nreg - rf0, nw0 = (uint64_t)gridDim.x * kWPB;
     if (rf0 + (uint64_t)blockIdx.x * kWPB * ((nr0 + nw0 - 1) / nw0) >= p.nreg) return;
@@ -1110,6 +1181,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
 template <bool kB>
 __global__ void k_link(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
+  if (scan_done(p)) return;
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t rf = first_region(p);
   if (r >= p.nreg || r < rf) return;
@@ -1146,11 +1218,11 @@ struct CohRd {
 // 2. the last workgroup to finish (ctr[6]) re-checks every link over the summaries as they now are
 //    (the same flags, rewritten), and its first wave runs the serial repair() from those flags.
 // ctr[2] = regions re-run (both phases).
-constexpr int kRepWaves = 16;
+constexpr int kRepWaves = LDB_LP2 ? 14 : 16;   // k_repair: as many waves as fit beside the table block
 template <bool kB>
 __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
-  if (p.ctr[0] == 0) return;
+  if (p.ctr[0] == 0 || scan_done(p)) return;
   // CRC tables in a static LDS array: its address is a link-time constant, so every table read
   // folds the table base into the ds_read offset field
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
@@ -1325,7 +1397,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
 template <bool kB>
 __global__ __launch_bounds__(256) void k_combine(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
-  if ((uint64_t)blockIdx.x * blockDim.x >= p.nreg) return;   // a batched grid sized for a longer file
+  if ((uint64_t)blockIdx.x * blockDim.x >= p.nreg || scan_done(p)) return;   // (a batched grid sized for a longer file)
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ uint64_t s_sum[256];
   uint64_t cnt = 0;
@@ -1439,9 +1511,14 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p0, int only_on_overflow, co
 // counts (k_combine), its regions are scanned in LDS, and tuples are copied flat (thread j of
 // the block's output range finds its region by binary search). The block holding the terminal
 // region writes the ldb_scan_result.
+__device__ __forceinline__ void compact_body(const Pipe& p);
 template <bool kB>
 __global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
+  compact_body(p);
+}
+__device__ __forceinline__ void compact_body(const Pipe& p) {
+  if (scan_done(p)) return;   // uni_finish wrote the result
   if (p.ctr[1]) {   // a region overflowed its tuple slots (k_combine): the serial walker redoes the scan
     if (blockIdx.x == 0 && threadIdx.x == 0) serial_walk(p);
     return;
@@ -1678,7 +1755,7 @@ WsLayout layout(uint64_t len) {
   // tpos (2 x u64, set by k_scan_main's first workgroup); take() rounds each field to 256 B
   L.o_ctr = take(32);
   L.o_tpos = take(16);
-  L.o_dyn = take(32);   // run prefix: K, entry size, setup-published flag (k_uniform)
+  L.o_dyn = take(64);   // run prefix: K, entry size, setup-published flag, done flag, done counter (k_uniform)
   L.o_uni = take(kUniSetupBytes + 4 * kUniTabWords);   // run prefix: the published setup
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
@@ -1729,23 +1806,29 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.out = out;
   p.cap = cap;
   p.kind = kind;
-  p.fill_main = 0;
   p.result = res;
   return p;
 }
 
-// Note the stream of the pipeline just enqueued (see ldb_ctx::ws_ev). The event itself is recorded
-// only when a pipeline on another stream wants the workspace (ws_wait): everything enqueued on the
-// old stream by then includes that pipeline, and a scan stream used alone pays no marker packet per
-// pipeline (one was ~10 us between the config-4 pipelines).
+// Note the stream of the pipeline just enqueued (see ldb_ctx::ws_ev). No marker is recorded per
+// pipeline (one was ~10 us between the config-4 pipelines): a scan stream used alone pays nothing.
 int fence_ws(ldb_ctx* c, hipStream_t s) {
   c->ws_stream = s;
   c->ws_ev_live = true;
   return LDB_OK;
 }
-// the workspace is free for stream s once the last pipeline enqueued on another stream has finished
+// The workspace is free for stream s once the last pipeline enqueued on another stream has finished.
+// An event is recorded on the old stream only when the context owns it (h_stream lives as long as the
+// context); a caller's stream may have been destroyed since its last call (the C ABI allows that), and
+// recording on a dead handle is undefined, so a switch away from one drains the device instead. A
+// context used from one stream never switches; the merge's scan contexts keep to their own streams.
 int ws_wait(ldb_ctx* c, hipStream_t s) {
   if (!c->ws_ev_live || c->ws_stream == s) return LDB_OK;
+  if (c->ws_stream != c->h_stream || !c->h_stream) {
+    LDB_HIP(hipDeviceSynchronize());
+    c->ws_ev_live = false;
+    return LDB_OK;
+  }
   if (!c->ws_ev && hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess) return LDB_ERR_HIP;
   LDB_HIP(hipEventRecord(c->ws_ev, c->ws_stream));
   LDB_HIP(hipStreamWaitEvent(s, c->ws_ev, 0));
@@ -1778,9 +1861,12 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
 }
 
 // the control words every region pipeline starts from (enqueue_scan)
+// dyn: [0] K (dyn_val: ~0 = no failure seen, 0 = no run), [1] entry size, [2] setup flag, [3] done
+// flag (uni_finish), [4] k_uniform's done counter
 __global__ __launch_bounds__(64) void k_init(uint32_t* ctr, uint64_t* dyn, uint64_t dyn_val) {
   if (threadIdx.x < 8) ctr[threadIdx.x] = 0u;
-  if (threadIdx.x < 4) dyn[threadIdx.x] = dyn_val;
+  if (threadIdx.x < 3) dyn[threadIdx.x] = dyn_val;
+  if (threadIdx.x == 3 || threadIdx.x == 4) dyn[threadIdx.x] = 0;
 }
 
 // persistent k_scan_main workgroups: exactly those resident at once (LDS-limited), so no second
@@ -1880,14 +1966,8 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     } else {
-      launch(0, len);
+      launch(0, len);   // its workgroups also write the run's INDEX tuples (uni_post_fill)
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-      // the run's INDEX tuples are written by k_scan_main's grid before its regions (p.fill_main);
-      // timed (ldb_kernel_timing), by k_uniform_fill in series, for the split
-      if (kind == LDB_TUPLE_INDEX && !p.hash_out) {
-        if (ev) hipLaunchKernelGGL(k_uniform_fill<false>, dim3(fill_grid(c, len)), dim3(kFillThreads), 0, s, p, 0, len);
-        else p.fill_main = 1;
-      }
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
   } else if (ev) {
@@ -2238,9 +2318,11 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
   const size_t tsz = tuple_kind == LDB_TUPLE_ENTRY ? sizeof(ldb_entry) : sizeof(ldb_index_tuple);
   // context-owned staging (grow-only): image, tuples, result; one stream per context
   if (!c->h_stream && hipStreamCreateWithFlags(&c->h_stream, hipStreamNonBlocking) != hipSuccess) return LDB_ERR_HIP;
-  // A page-locked image (ldb_host_register, or a pinned allocation) is scanned in place, below
+  // An image this context page-locked (ldb_host_register) for all len bytes is scanned in place, below
   // (opt-in, LDB_DIRECT_IMAGE=1: measured slower than the staged copy, 23.7 vs 21.0 ms at config 2 --
-  // the CUs' PCIe reads reach 52 GB/s against the DMA engines' 57.6)
+  // the CUs' PCIe reads reach 52 GB/s against the DMA engines' 57.6). Memory pinned any other way
+  // (hipHostMalloc, torch pin_memory, another context's registration) is staged like pageable memory.
+  if (cap > UINT64_MAX / tsz) return LDB_ERR_ARG;
   void* mapped = nullptr;
   if (len && getenv("LDB_DIRECT_IMAGE") != nullptr && c->registered(h_image, len) &&
       (hipHostGetDevicePointer(&mapped, const_cast<uint8_t*>(h_image), 0) != hipSuccess || ((uintptr_t)mapped & 15))) {

@@ -40,23 +40,52 @@ def sum_over_ranks(xs, device):
     return [float(v) for v in t.tolist()]
 
 
+def gather_floats(xs, device):
+    """Every rank's list of floats (same length on every rank), rank order, on every rank."""
+    device = coll_device(device)
+    t = torch.tensor([float(x) for x in xs], dtype=torch.float64, device=device)
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [[float(v) for v in t.tolist()]]
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(v) for v in o.tolist()] for o in out]
+
+
+def agree(ok: bool, what: str, device) -> None:
+    """Every rank learns whether every rank's local check passed (one all_reduce MIN of a flag) and all
+    of them raise together: a rank that raised alone before a collective would leave the others blocked
+    in it (under RCCL until the process-group timeout), so checks on a rank's own inputs go through here
+    before the collective they guard."""
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=coll_device(device))
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if int(t.item()) == 0:
+        raise RuntimeError(f"{what}: refused on every rank (a rank's own check failed"
+                           f"{'' if not ok else ', not this one'})")
+
+
 def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0):
     """Gather every rank's tuple byte buffer (uint8, 1-D, on the rank's device) to `dst`: a gatherv.
 
     One all_gather of the byte counts, then point-to-point transfers of exactly those bytes (one
     batched group of isend / irecv: over RCCL the receives run concurrently on dst's xGMI links), so
     unequal files ship no padding. Returns the list of per-rank buffers (rank order) on `dst`, None
-    elsewhere; gather_tuples.last_bytes is the byte total that crossed to dst.
+    elsewhere; gather_tuples.last_bytes is the byte total that crossed to dst. A rank whose buffer is
+    not a 1-D uint8 tensor makes every rank raise (agree) instead of leaving the others blocked.
     """
-    assert tuple_bytes.dtype == torch.uint8 and tuple_bytes.dim() == 1
     world = dist.get_world_size()
     rank = dist.get_rank()
-    tuple_bytes = tuple_bytes.to(coll_device(tuple_bytes.device)).contiguous()
-    dev = tuple_bytes.device
+    ok = isinstance(tuple_bytes, torch.Tensor) and tuple_bytes.dtype == torch.uint8 and tuple_bytes.dim() == 1 \
+        and 0 <= dst < world
+    dev = coll_device(tuple_bytes.device if isinstance(tuple_bytes, torch.Tensor) else torch.device("cpu"))
+    agree(ok, "gather_tuples", dev)
+    tuple_bytes = tuple_bytes.to(dev).contiguous()
     n = torch.tensor([tuple_bytes.numel()], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
+    if counts[rank] != tuple_bytes.numel():   # every rank sees the same list; this would be a transport fault
+        raise RuntimeError(f"gather_tuples: rank {rank} counted {counts[rank]} B, holds {tuple_bytes.numel()}")
     gather_tuples.last_bytes = sum(c for r, c in enumerate(counts) if r != dst)
     if rank == dst:
         bufs = [tuple_bytes if r == dst else torch.empty(counts[r], dtype=torch.uint8, device=dev)

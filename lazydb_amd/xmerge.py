@@ -281,22 +281,29 @@ def _all_gather_varlen(x, dist):
     return [b[:k].to(x.device) for b, k in zip(bufs, ns)]
 
 
-def check_fid_blocks(files, dist):
+def check_fid_blocks(files, dist, device=None):
     """Both cross-GPU merges take last-writer-wins order from the rank order (rank r's block below rank
     r+1's): a round-robin or misordered split would give wrong liveness silently, so it is refused.
-    One all-gather of each rank's (min fid, max fid); an empty block is skipped."""
+    One all-gather of each rank's (fids ascending?, min fid, max fid); an empty block is skipped.
+    Every rank raises on the same gathered values, so a bad block on one rank never leaves the others
+    blocked in a later collective. `device`: where the collective buffer lives (the engine's GPU under
+    RCCL; host memory under gloo), never taken from the files, which an empty block has none of."""
     import torch
-    cpu = dist.get_backend() == "gloo"
-    dev = "cpu" if cpu else files[0][0].device if files else "cpu"
+    from .multi import coll_device
+    dev = coll_device(device if device is not None else
+                      (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"))
     fids = [int(f) for _, f, _ in files]
-    if fids != sorted(fids) or len(set(fids)) != len(fids):
-        raise ValueError(f"rank {dist.get_rank()}: fids not strictly ascending: {fids}")
-    mine = torch.tensor([min(fids), max(fids)] if fids else [-1, -1], dtype=torch.int64, device=dev)
+    ok = fids == sorted(fids) and len(set(fids)) == len(fids)
+    mine = torch.tensor([1 if ok else 0] + ([min(fids), max(fids)] if fids else [-1, -1]), dtype=torch.int64,
+                        device=dev)
     allb = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
     dist.all_gather(allb, mine)
+    allb = [[int(v) for v in b.cpu()] for b in allb]
+    bad = [r for r, b in enumerate(allb) if b[0] == 0]
+    if bad:
+        raise ValueError(f"rank(s) {bad}: fids not strictly ascending" + ("" if ok else f" (here: {fids})"))
     prev = None
-    for r, b in enumerate(allb):
-        lo, hi = int(b[0]), int(b[1])
+    for r, (_, lo, hi) in enumerate(allb):
         if lo < 0:
             continue
         if prev is not None and lo <= prev:
@@ -314,7 +321,7 @@ def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
-    check_fid_blocks(files, dist)
+    check_fid_blocks(files, dist, torch.device("cuda", eng.device))
     if world == 1:
         allsum = []
     else:   # rank r reads the summaries of ranks r+1..: nobody reads rank 0's
@@ -332,11 +339,16 @@ def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int
 
 def _all_to_all_varlen(chunks, dist):
     """chunks[o] (1-D uint8 device tensors) to rank o; returns what every rank sent here, rank order.
-    RCCL: all_to_all_single with the splits; gloo (CPU tests): an all-gather of everything, host copies."""
+    RCCL: all_to_all_single with the splits; gloo (CPU tests): an all-gather of everything, host copies.
+    A rank with the wrong number of chunks makes every rank raise (multi.agree) before any byte moves;
+    after the size exchange, the bytes all ranks will send and receive are summed and must agree."""
     import torch
+    from .multi import agree, coll_device
     world = dist.get_world_size()
     rank = dist.get_rank()
-    dev = chunks[0].device
+    ok = len(chunks) == world and all(c.dtype == torch.uint8 and c.dim() == 1 for c in chunks)
+    dev = chunks[0].device if chunks else torch.device("cpu")
+    agree(ok, "all-to-all exchange", dev)
     sizes = torch.tensor([int(c.numel()) for c in chunks], dtype=torch.int64)
     if dist.get_backend() == "gloo":
         flat = torch.cat(chunks).cpu() if chunks else torch.zeros(0, dtype=torch.uint8)
@@ -351,6 +363,12 @@ def _all_to_all_varlen(chunks, dist):
     sizes_d = sizes.to(dev)
     recv_sz = torch.empty_like(sizes_d)
     dist.all_to_all_single(recv_sz, sizes_d)
+    # the sizes every rank will send must equal what every rank expects to receive (a transport or
+    # caller fault otherwise: all_to_all_single with mismatched splits would fail or hang mid-transfer)
+    bal = torch.stack([sizes_d.sum(), recv_sz.sum()]).to(coll_device(dev))
+    dist.all_reduce(bal)
+    if int(bal[0]) != int(bal[1]):
+        raise RuntimeError(f"all-to-all exchange: ranks send {int(bal[0])} B in all but expect {int(bal[1])} B")
     recv_sz = [int(x) for x in recv_sz.cpu()]
     send = torch.cat(chunks) if chunks else torch.zeros(0, dtype=torch.uint8, device=dev)
     recv = torch.empty(sum(recv_sz), dtype=torch.uint8, device=dev)
@@ -370,7 +388,7 @@ def merge_hashed_distributed(eng, files, active_fid: int, active_off: int, max_f
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
-    check_fid_blocks(files, dist)
+    check_fid_blocks(files, dist, torch.device("cuda", eng.device))
     ro = route_phase(eng, files, world, io_type)
     rc = [ro["recs"][sum(ro["rec_splits"][:o]): sum(ro["rec_splits"][:o + 1])] for o in range(world)]
     kc = [ro["keys"][sum(ro["key_splits"][:o]): sum(ro["key_splits"][:o + 1])] for o in range(world)]

@@ -111,3 +111,37 @@ def test_three_rank_gatherv_unequal_sizes():
     for r, g in enumerate(got):
         assert g == (torch.arange(sizes[r], dtype=torch.int64).to(torch.uint8) ^ r).numpy().tobytes()
     assert moved == sizes[1] + sizes[2]   # exactly the other ranks' bytes crossed to rank 0
+
+
+def _gather_bad_worker(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lazydb_amd import multi
+        # rank 1 hands in int32 tuples instead of bytes: every rank raises, none waits in the gather
+        mine = torch.zeros(64, dtype=torch.uint8 if rank != 1 else torch.int32)
+        try:
+            multi.gather_tuples(mine)
+            q.put((rank, "ok"))
+        except RuntimeError as e:
+            q.put((rank, "refused: " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gatherv_refuses_on_every_rank():
+    """the gather fails loudly on every rank, not with one rank raising and the others
+    hanging in the collective."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_bad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(v.startswith("refused") for v in got.values()), got

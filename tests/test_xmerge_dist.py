@@ -171,6 +171,8 @@ def _fid_block_worker(rank, world, port, q, blocks):
     ([[0, 1], []], True),                      # an empty block is skipped
     ([[0, 2], [1, 3]], False),                 # round-robin split: refused, not silently wrong
     ([[2, 3], [0, 1]], False),                 # blocks descending in rank order
+    ([[1, 0], [2, 3]], False),                 # one rank's own fids descending: every rank raises (no hang)
+    ([[0, 0], [2, 3]], False),                 # a duplicate fid on one rank
 ])
 def test_fid_blocks_checked_gloo(blocks, ok):
     """Both cross-GPU merges take last-writer-wins order from rank order: a split whose
@@ -188,3 +190,37 @@ def test_fid_blocks_checked_gloo(blocks, ok):
         assert p.exitcode == 0
     for r in range(world):
         assert (got[r] == "ok") == ok, got
+
+
+def _a2a_bad_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        import torch
+        from lazydb_amd.xmerge import _all_to_all_varlen
+        # rank 1 hands in one chunk too few: every rank must raise before any byte moves
+        n = world if rank != 1 else world - 1
+        chunks = [torch.full((3 + o,), rank, dtype=torch.uint8) for o in range(n)]
+        try:
+            _all_to_all_varlen(chunks, dist)
+            q.put((rank, "ok"))
+        except RuntimeError as e:
+            q.put((rank, "refused: " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_all_to_all_refuses_on_every_rank_gloo():
+    """A rank with a malformed exchange raises on EVERY rank (multi.agree) instead of leaving the
+    others blocked in the collective (fail loudly, not hang)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_a2a_bad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(v.startswith("refused") for v in got.values()), got

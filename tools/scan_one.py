@@ -22,6 +22,8 @@ def main():
     d = torch.from_numpy(img).to("cuda:0")
     eng.reserve(img.size)
     res, _ = eng.scan_dev(d, io_type=io, cap=n + 1024)
+    out, rb = eng.alloc_out(n + 1024, 0), eng.alloc_result()
+    bench.settle(lambda: eng.scan_dev_async(d, io_type=io, out=out, cap=n + 1024, result=rb), 150.0)   # clocks (DVFS)
     torch.cuda.synchronize()
     eng.timing_split(1)
     t0 = time.perf_counter()
