@@ -53,7 +53,7 @@ namespace ldb { extern uint64_t g_chain_why[16]; }
 namespace ldb {
 
 constexpr uint32_t kOwnerOk = 8u;     // sflag: owner of the region's first start CRC-verified in-wave
-constexpr uint32_t kMinFast = kS + 4; // fast path: every entry >= 84 B (one start per slice, one check per lane)
+constexpr uint32_t kMinFast = kS + 4; // memo (predicted starts) entries: one start per slice
 
 // Chain state carried from one region to the next within a wavefront's run.
 //
@@ -335,16 +335,46 @@ LDB_HD uint32_t crc_slice_raw2(const uint32_t* tab, const SliceRows& rows) {
 
 // Per-lane registers of the chained path.
 struct ChainPriv {
-  uint32_t s;       // region-relative entry start in this slice, or kNone32
-  uint32_t X;       // its exit
-  uint32_t crc, k, vv, w1, hs, stat;
-  uint32_t wo;      // ~crc of its owner (injected at [s, s+4))
+  uint32_t s;       // region-relative FIRST entry start in this slice, or kNone32
+  uint32_t X;       // the exit of the slice's LAST entry (the lane's link to the next start lane)
+  uint32_t crc, k, vv, w1, hs, stat;   // the last entry's header (its owner role, the summary, the memo)
+  uint32_t sl;      // the last entry's start (= s when the slice holds one start)
+  uint32_t cnt;     // entries starting in the slice (round 4: several, when entries end inside it)
+  uint32_t pre;     // exclusive prefix of cnt over the lanes (tuple slots)
+  uint32_t wo;      // ~crc of the first start's owner (injected at [s, s+4))
   uint32_t kb;      // check: capture step (or 0), chk: 1 if this lane checks an owner
   uint32_t chk;
+  uint32_t chkB;    // 1: this lane also checks the previous lane's single start in that lane's last 4
+                    // bytes (at its step 0); 2: a local CRC of an inner entry failed (the region declines)
   uint64_t mlo;     // bytes of the capture step's word that precede the checked entry's CRC span
   uint64_t wc;      // that word
-  uint32_t y, ya, cap, O;
+  uint64_t wB;      // chkB: the slice's first 8 bytes, those at or past that start's CRC span masked
+  uint32_t y, ya, cap, O, yB;
 };
+
+// Round 4: a slice may hold several entry starts. From the lane's first start p (decode_lean in e), an
+// entry that ends inside the slice is followed by the next at its exit, and so on; the lane keeps its
+// first start, the last entry's fields and the count. Returns false when such an exit does not decode as
+// a lean header (a terminal, a non-canonical or long-varint header, or a false speculative start): the
+// lane then has no start (region_process decides a region the true chain cannot cross that way).
+// Rounds 1-3 declined any region with an entry < kMinFast = 84 B (two starts in one slice); LazyDB's
+// writers emit many (a Delete is 21 B): 98 % of a writer-realistic log's regions went to region_process.
+template <class CP>
+LDB_HD bool lean_walk(const View& v, int l, uint32_t p, const Lean& e, CP& c) {
+  const uint32_t E = (uint32_t)(l * kS + kS);
+  Lean cur = e;
+  uint32_t q = p, n = 1;
+  while (cur.X < E) {
+    Lean nx;
+    if (!decode_lean(v, (int)cur.X, &nx)) return false;
+    q = cur.X;
+    cur = nx;
+    ++n;
+  }
+  c.s = p; c.sl = q; c.cnt = n;
+  c.X = cur.X; c.crc = cur.crc; c.k = cur.k; c.vv = cur.vv; c.w1 = cur.w1; c.hs = cur.hs; c.stat = cur.stat;
+  return true;
+}
 
 // Rewrite (inject = true) or restore the 8 bytes [s, s+8) of a start in the staging buffer.
 LDB_HD void rewrite8(uint8_t* wbuf, const ChainPriv& c, bool inject) {
@@ -462,6 +492,7 @@ LDB_HD bool predict_starts(WP& wp, const View& v, WaveSh& sh, const ChainState& 
       p = p < B + (uint32_t)kS ? p : kNone32;
     }
     c.s = kNone32;
+    c.cnt = 0;
     if (p == kNone32) return false;
     const int a = (int)p + kPre;
     const int qd = a & ~3;
@@ -478,11 +509,12 @@ LDB_HD bool predict_starts(WP& wp, const View& v, WaveSh& sh, const ChainState& 
                     !read_eof(v.len, v.io, (int64_t)(off + hs), kv);               // log_file.go:130-139
     if (ok) {
       c.s = p; c.X = p + sz; c.crc = w0; c.k = st.m_k; c.vv = st.m_vv; c.w1 = w1; c.hs = hs; c.stat = stat;
+      c.sl = p; c.cnt = 1;   // memo entries are >= kMinFast: one start per slice
     }
     return !ok;
   });
   if (bad) {
-    wp.each([&](int l) { cpriv(l).s = kNone32; });
+    wp.each([&](int l) { cpriv(l).s = kNone32; cpriv(l).cnt = 0; });
     return false;
   }
   wp.each([&](int l) { sh.s[l] = cpriv(l).s; });
@@ -582,6 +614,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   wp.each([&](int l) {
     ChainPriv& c = cpriv(l);
     c.s = kNone32;
+    c.cnt = 0;
     c.chk = 0;
     c.X = l == lt ? xr : (l > lt ? first_cand(v, l * kS) : kNone32);   // candidate (X reused)
   });
@@ -591,9 +624,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       const uint32_t p = c.s == kNone32 ? c.X : kNone32;
       if (p == kNone32) return;
       Lean e;
-      if (decode_lean(v, (int)p, &e)) {
-        c.s = p; c.X = e.X; c.crc = e.crc; c.k = e.k; c.vv = e.vv; c.w1 = e.w1; c.hs = e.hs; c.stat = e.stat;
-      } else {
+      if (!(decode_lean(v, (int)p, &e) && lean_walk(v, l, p, e, c))) {
         const uint32_t nxt = p + 1 - (uint32_t)(l * kS);
         c.X = (!known && nxt < (uint32_t)kS) ? first_cand(v, l * kS, nxt) : kNone32;
       }
@@ -609,7 +640,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     tstat = lean_terminal(v, xr);
     if (tstat == kCont) return LDB_DECLINE(2);
     tpos = xr;   // the chain enters on its terminal: nothing in the region is on it
-    wp.each([&](int l) { cpriv(l).s = kNone32; sh.s[l] = kNone32; });
+    wp.each([&](int l) { cpriv(l).s = kNone32; cpriv(l).cnt = 0; sh.s[l] = kNone32; });
   }
   if (tpos == kNone32) {
   // ---- pointer round: a lane without a plausible first candidate that the nearest start below
@@ -630,9 +661,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
         const uint32_t X = target(l);
         if (X != kNone32) {
           Lean e;
-          if (decode_lean(v, (int)X, &e)) {
-            c.s = X; c.X = e.X; c.crc = e.crc; c.k = e.k; c.vv = e.vv; c.w1 = e.w1; c.hs = e.hs; c.stat = e.stat;
-          }
+          if (decode_lean(v, (int)X, &e)) lean_walk(v, l, X, e, c);
         }
       });
       wp.each([&](int l) { sh.s[l] = cpriv(l).s; });
@@ -642,8 +671,6 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   for (int it = 0;; ++it) {
     starts = wp.ballot([&](int l) { return cpriv(l).s != kNone32; });
     const uint64_t sts = starts;
-    const int irr = wp.first([&](int l) { const ChainPriv& c = cpriv(l); return c.s != kNone32 && c.X - c.s < kMinFast; });
-    if (irr >= 0) return LDB_DECLINE(3);
     const int j = wp.first([&](int l) {
       const ChainPriv& c = cpriv(l);
       if (c.s == kNone32) return false;
@@ -661,9 +688,8 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       if (l == m) {
         Lean e;
         c.s = kNone32;
-        if (decode_lean(v, (int)Xj, &e)) {
-          c.s = Xj; c.X = e.X; c.crc = e.crc; c.k = e.k; c.vv = e.vv; c.w1 = e.w1; c.hs = e.hs; c.stat = e.stat;
-        }
+        c.cnt = 0;
+        if (decode_lean(v, (int)Xj, &e)) lean_walk(v, l, Xj, e, c);
       }
       sh.s[l] = c.s;
     });
@@ -673,7 +699,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       if (tstat == kCont) return LDB_DECLINE(6);
       tpos = Xj;
       wp.each([&](int l) {
-        if (l > j) cpriv(l).s = kNone32;
+        if (l > j) { cpriv(l).s = kNone32; cpriv(l).cnt = 0; }
         sh.s[l] = cpriv(l).s;
       });
       starts = wp.ballot([&](int l) { return cpriv(l).s != kNone32; });
@@ -691,14 +717,14 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     const int mt = (int)(tpos / kS);
     wp.each([&](int l) {
       ChainPriv& c = cpriv(l);
-      if (l == mt) { c.s = tpos; c.X = tpos; c.crc = 0; c.w1 = 0; }
+      if (l == mt) { c.s = tpos; c.sl = tpos; c.X = tpos; c.crc = 0; c.w1 = 0; c.cnt = 0; }
       sh.s[l] = c.s;
     });
   }
   const int L0 = known ? lt : (int)__builtin_ctzll(starts);
   const uint32_t sL0 = wp.from(L0, [&](int l) { return cpriv(l).s; });
   const int z = starts ? 63 - (int)__builtin_clzll(starts) : L0;
-  const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).s; });
+  const uint32_t sz = wp.from(z, [&](int l) { return cpriv(l).sl; });   // the region's last entry start
   // the next regions' memo: the region's last entry (the owner of the next x), read while the
   // staging buffer still holds this region (a predicted region keeps the memo it verified against)
   // Only a region whose first and last entries look alike (same size and leading header bytes) sets
@@ -714,7 +740,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       const uint32_t w1z = wp.from(z, [&](int l) { return cpriv(l).w1; });
       const bool alike = wp.from(L0, [&](int l) {
         const ChainPriv& c = cpriv(l);
-        return (uint32_t)(c.X - c.s == esz && c.hs == hsz && c.k == kz && c.vv == vz && c.w1 == w1z);
+        return (uint32_t)(c.cnt == 1 && c.X - c.s == esz && c.hs == hsz && c.k == kz && c.vv == vz && c.w1 == w1z);
       }) != 0u;
       if (alike && esz >= kMinFast && hsz <= 16u) {
         nm.m_meta = uniform(1u | (hsz << 1) | (wp.from(z, [&](int l) { return cpriv(l).stat; }) << 8));
@@ -725,15 +751,36 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
       }
     }
   }
-  // ---- tuples (see emit above)
+  // ---- tuples (see emit above). A lane with several starts walks them again (decode_lean on the
+  // staging buffer, unmodified until the rewrite below), emits each, and CRC-checks every entry that
+  // ends inside its slice right here (crc_segment, init ~0 against ~stored crc): such an entry's owner
+  // check needs no G-chain capture. A failure declines the region before any byte is rewritten.
+  auto cnt_of = [&](int l) { return ((starts >> l) & 1u) ? cpriv(l).cnt : 0u; };
+  const bool multi = wp.ballot([&](int l) { return cnt_of(l) > 1u; }) != 0;
+  if (multi) wp.excl_prefix(cnt_of, [&](int l, uint32_t x) { cpriv(l).pre = x; });
+  auto pos_of = [&](uint32_t s0, uint32_t hs0, uint32_t st0) {
+    return ((v.R0 + s0) & 0xFFFFFFFFFFull) | ((uint64_t)(hs0 & 0x3F) << 40) | ((uint64_t)(hs0 & 0x3F) << 46) |
+           ((uint64_t)(st0 & 0xFF) << 52);
+  };
   wp.each([&](int l) {
-    const ChainPriv& c = cpriv(l);
+    ChainPriv& c = cpriv(l);
     const bool valid = ((starts >> l) & 1u) && !(LDB_ABLATE & 4);   // an entry (not the pseudo start)
-    const uint32_t slot = (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
-    const uint64_t pos = ((v.R0 + c.s) & 0xFFFFFFFFFFull) | ((uint64_t)(c.hs & 0x3F) << 40) |
-                         ((uint64_t)(c.hs & 0x3F) << 46) | ((uint64_t)(c.stat & 0xFF) << 52);
-    emit(valid, slot, pos, c.k, c.vv);
+    c.chkB = 0;
+    if (!multi || c.cnt <= 1) {
+      const uint32_t slot = multi ? c.pre : (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
+      emit(valid, slot, pos_of(c.s, c.hs, c.stat), c.k, c.vv);
+      return;
+    }
+    uint32_t q = c.s;
+    for (uint32_t i = 0; i < c.cnt; ++i) {
+      Lean e;
+      decode_lean(v, (int)q, &e);   // (decoded before: a start of the lane's walk)
+      emit(valid, c.pre + i, pos_of(q, e.hs, e.stat), e.k, e.vv);
+      if (i + 1 < c.cnt && crc_segment(v, (int)q + 4, (int)e.X, 0xFFFFFFFFu) != ~e.crc) c.chkB = 2;   // ErrInvalidCrc
+      q = e.X;
+    }
   });
+  if (multi && wp.ballot([&](int l) { return cpriv(l).chkB == 2u; })) return LDB_DECLINE(9);
   // The last start's 8-byte rewrite may run past the region end (into the staged halo):
   //   kW - sz in (4, 8): its CRC-init bytes straddle the end; the true init-based register at the
   //     region end is the G-chain's ^ (~0 >> 8 * (bytes of the init inside the region));
@@ -741,7 +788,13 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   //     k_combine finishes it); its owner is checked in lane 63 over the halo (capture step 10).
   const uint32_t tail = (uint32_t)kW - sz;
   // ---- owners, check assignment, buffer rewrite
-  wp.each([&](int l) { sh.want[l] = ~cpriv(l).crc; });
+  // sh.want: ~crc of each lane's LAST start (the owner of the next start above); sh.fl: a lane's start
+  // when it holds exactly one (or the pseudo start), whose owner check may fall in the next lane
+  wp.each([&](int l) {
+    const ChainPriv& c = cpriv(l);
+    sh.want[l] = ~c.crc;
+    sh.fl[l] = c.s != kNone32 && c.cnt <= 1 ? c.s : kNone32;
+  });
   const uint32_t want_x = spec ? 0u : ~st.owner;   // speculative: the entry's stored crc field becomes 0
   wp.each([&](int l) {
     ChainPriv& c = cpriv(l);
@@ -750,14 +803,37 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     const uint32_t B = (uint32_t)(l * kS);
     uint32_t cs = kNone32;
     if (c.s != kNone32 && (c.s + 4 < B + kS || l == kLanes - 1)) cs = c.s;   // lane 63: P may be past E (halo)
-    else if (l > 0 && sh.s[l - 1] != kNone32 && sh.s[l - 1] + 4 >= B) cs = sh.s[l - 1];
     // speculative: L0's owner is checked by k_combine (rpre); its capture only yields the prefix
     c.chk = cs != kNone32 && !(spec && cs == sL0);
     const uint32_t rel = cs != kNone32 ? cs + 4 - B : 0u;   // [0, kS + 4): kb == 10 only in lane 63
     c.kb = rel >> 3;
     const uint32_t nb = rel & 7u;
     c.mlo = nb ? (~0ull >> (64 - 8 * nb)) : 0ull;
-    if (c.s != kNone32) rewrite8(wbuf, c, true);
+    // the previous lane's single start in that lane's last 4 bytes: its owner's check point lies in this
+    // slice, at step 0 (the register before it is 0); kept apart from this lane's own capture
+    const uint32_t sb = l > 0 ? sh.fl[l - 1] : kNone32;
+    const uint32_t nbB = sb != kNone32 && sb + 4 >= B ? sb + 4 - B : 8u;   // 0..3, or 8: none
+    c.chkB = nbB < 8u && !(spec && sb == sL0) ? 1u : 0u;
+    c.wB = c.chkB && nbB ? (~0ull >> (64 - 8 * nbB)) : 0ull;   // the mask until the rows are read
+    if (c.s == kNone32) return;
+    if (c.cnt <= 1) {
+      rewrite8(wbuf, c, true);
+      return;
+    }
+    uint32_t q = c.s, own = c.wo;   // every start of the slice: [s, s+4) := ~crc(owner), [s+4, s+8) ^= ~0
+    for (uint32_t i = 0; i < c.cnt; ++i) {
+      Lean e;
+      decode_lean(v, (int)q, &e);
+      uint8_t* b = wbuf + kPre + q;
+      const uint32_t hi = ~e.w1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        b[k] = (uint8_t)(own >> (8 * k));
+        b[4 + k] = (uint8_t)(hi >> (8 * k));
+      }
+      own = ~e.crc;
+      q = e.X;
+    }
   });
   wp.stamp(12);
   // ---- one CRC chain per lane, lane scan, owner checks
@@ -766,6 +842,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     const SliceRows rows = load_rows(v, l * kS);   // the (rewritten) slice, the buffer's last read
     const uint64_t w10 = (l == kLanes - 1 && c.kb == (uint32_t)(kS / 8))
                              ? (((uint64_t)vword(v, kW + 4) << 32) | vword(v, kW)) : 0ull;   // halo
+    c.wB &= ((uint64_t)rows.q[0].w[1] << 32) | rows.q[0].w[0];
 #ifndef LDB_LATE_RELEASE
     release();
 #endif
@@ -795,8 +872,10 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   const uint32_t Iin = st.I;
   wp.template shfl_up<1>([&](int l) { return cpriv(l).O; }, [&](int l, uint32_t t, bool valid) {
     ChainPriv& c = cpriv(l);
-    if (!c.chk) return;   // lanes without a check stay off the LDS (fewer bank conflicts)
+    if (!c.chk && !c.chkB) return;   // lanes without a check stay off the LDS (fewer bank conflicts)
     const uint32_t g = valid ? t : Iin;   // G at the slice start
+    if (c.chkB) c.yB = shift_tab(v.tab, kVSOff, g) ^ crc_step8(v.tab, 0u, (uint32_t)c.wB, (uint32_t)(c.wB >> 32));
+    if (!c.chk) return;
     const uint64_t w = c.wc & c.mlo;
     // G at P = slice start + 8 (kb + 1) = shift(G at the chain start, P - chain start) ^ the chain's
     // register at P; the second chain starts at byte 48, where G = shift48(G) ^ (first chain)
@@ -805,7 +884,10 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     const uint32_t n = second ? c.kb + 1 - kSplit : c.kb + 1;
     c.y = shift_8n(v.tab, base, n) ^ crc_step8(v.tab, c.cap, (uint32_t)w, (uint32_t)(w >> 32));
   });
-  const int bad = LDB_ABLATE ? -1 : wp.first([&](int l) { const ChainPriv& c = cpriv(l); return c.chk && c.y != 0u; });
+  const int bad = LDB_ABLATE ? -1 : wp.first([&](int l) {
+    const ChainPriv& c = cpriv(l);
+    return (c.chk && c.y != 0u) || (c.chkB && c.yB != 0u);
+  });
 #ifdef LDB_LATE_RELEASE
   if (bad < 0) release();
 #endif
@@ -815,11 +897,12 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   }
   wp.stamp(14);
   // ---- summary
+  const uint32_t nstarts = multi ? wp.sum(cnt_of) : (uint32_t)__builtin_popcountll(starts);
   RegionSum r;
   r.start = v.R0 + sL0;
   if (tpos != kNone32) {   // the chain ends here (status at tpos, as region_process reports it)
     r.status = tstat;
-    r.count = (uint32_t)__builtin_popcountll(starts);
+    r.count = nstarts;
     r.exitp = v.R0 + tpos;
     r.soff = 0; r.scrc = 0; r.rout = 0;
     r.rpre = rpre;
@@ -831,7 +914,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     return true;
   }
   r.status = kCont;
-  r.count = (uint32_t)__builtin_popcountll(starts);
+  r.count = nstarts;
   r.exitp = v.R0 + wp.from(z, [&](int l) { return cpriv(l).X; });
   r.soff = v.R0 + sz;
   r.scrc = wp.from(z, [&](int l) { return cpriv(l).crc; });

@@ -33,7 +33,8 @@ struct Pipe {
   uint64_t* blk;              // per kBlkRegions-region block: count sum (k_combine)
   uint64_t* dyn;              // [0] K: entries of the equal-sized run k_uniform verified, [1] their size,
                               // [2] kUniReady once a k_uniform launch published its setup to `uni`,
-                              // [3] kUniDone once the run prefix ended the scan (uni_finish), [4] its counter
+                              // [3] kUniDone once the run prefix ended the scan (uni_finish), [4] its counter,
+                              // [5] x0 (uni_finish) or ~0
   uint8_t* uni;               // the run prefix's published setup (memo, slicing, combine tables)
   uint64_t* hash_out;         // merge mode (nullable): ldb::key_hash_w of the key of run entry k at [k]
   void* out;
@@ -51,7 +52,10 @@ constexpr int kBlkRegions = 256;   // regions per k_combine / k_compact workgrou
 // region before x0's region, takes x0 as the chain's entry point (where it used to take offset 0),
 // and emits its tuples after the K the run wrote. K = 0 (no run) is the plain pipeline.
 LDB_HD uint64_t run_k(const Pipe& p) { return p.dyn[0] == ~0ull ? 0ull : p.dyn[0]; }
-LDB_HD uint64_t chain_x0(const Pipe& p) { return run_k(p) * p.dyn[1]; }
+// dyn[5]: x0 as the run prefix's last workgroup computed it over its runs (a log of several runs of
+// equal-sized entries, k_uniform uni_finish); ~0 where no such finish ran (a batched scan: one run, x0 =
+// K sz)
+LDB_HD uint64_t chain_x0(const Pipe& p) { return p.dyn[5] != ~0ull ? p.dyn[5] : run_k(p) * p.dyn[1]; }
 // first region of the replay; nreg when the header window at x0 is already unreadable (the replay
 // stops there with io.EOF, log_file.go:117-122, and no region has work)
 LDB_HD uint64_t first_region(const Pipe& p) {
@@ -169,11 +173,12 @@ LDB_HD uint32_t uni_lead(const UniGeo& g, uint32_t j) {
   return g.t > o ? (g.t - o < g.P ? g.t - o : g.P) : 0u;
 }
 
+// fetch(i) = image byte off + i (i in [0, 38)); off = the entry's image offset (the IOController bounds)
 template <class Fetch>
-LDB_HD UniMemo uni_memo(Fetch fetch, uint64_t len, int io) {
+LDB_HD UniMemo uni_memo(Fetch fetch, uint64_t len, int io, uint64_t off = 0) {
   UniMemo m;
   m.ok = 0;
-  const EntryInfo e = classify_entry(fetch, len, io, 0);
+  const EntryInfo e = classify_entry(fetch, len, io, off);
   if (e.status != kCont || !e.h.canonical || e.h.size < 10 || e.h.size > kMaxHeader) return m;
   if (e.size > kUniMaxSize || e.size < 16) return m;
   m.hs = (uint32_t)e.h.size;

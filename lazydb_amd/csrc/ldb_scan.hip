@@ -300,6 +300,25 @@ struct UniSetup {
   UniMemo m;
   UniGeo g;
 };
+// Round 4: a log may be several runs of equal-sized entries one after another (the reference bench's
+// log: keys bench_test_key_<i> grow a digit at entries 10, 100, ..., 100000, so its entry size steps up
+// five times, bench/db_bench_test.go:17-36; any fixed-schema writer whose key or value width steps).
+// uni_prepare finds where each run's headers stop matching its memo and speculates the next run there;
+// k_uniform verifies every run's candidates in one launch, and K counts entries along the chain across
+// the runs (run r's entry e is chain entry gbase + e). A boundary that is not the chain's (an entry of
+// run r failing its CRC before it) only costs the later runs' work: K stops at that first failure.
+constexpr int kUniMaxRuns = 8;
+struct UniRun {
+  UniMemo m;
+  UniGeo g;
+  uint64_t y;       // image offset of the run's entry 0
+  uint64_t gbase;   // its chain index (entries of the earlier runs)
+  uint64_t nc;      // candidates: entries e in [0, nc) at y + e sz
+};
+struct UniRuns {
+  UniRun r[kUniMaxRuns];
+  int n;
+};
 // Combine tables in LDS (4 byte-indexed 256-word tables each = 1024 words): G <= kUniDirectG uses the
 // direct form, G - 1 tables "shift by d P bytes" (d = 1 .. G - 1); larger G the tree, lg tables
 // "shift by 2^i P bytes".
@@ -371,7 +390,7 @@ __device__ __forceinline__ uint32_t ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 constexpr uint64_t kUniReady = 0x5E7A11ED5E7A11EDull;   // dyn[2]: the setup in p.uni is complete
 constexpr uint64_t kUniSetupBytes = 1024;                // UniSetup, then the combine tables
 constexpr uint32_t kUniWin = 8192;                       // image bytes uni_prepare stages (entries 0 and 1)
-static_assert(kUniMaxSize + 48 <= kUniWin, "entry 1's header lies in the staged window");
+static_assert(kUniMaxSize + 48 + 3 <= kUniWin, "entry 1's header lies in the staged window");
 static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // The first k_uniform launch of a pipeline derives the run's parameters in every workgroup (no
 // separate setup launch) and its workgroup 0 publishes them to p.uni, so the later launches of a
@@ -386,55 +405,119 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // scan: grid.y = file, its Pipe from the device array pb (enqueue_scan_batch).
 #define LDB_PIPE_SELECT const Pipe p = kB ? pb[blockIdx.y] : p0
 
-// Header probes (the unpublished path only): threads 0..63 each compare one candidate's header bytes
-// with the memo (uni_header_ok), at entries 2^(t+2) for t < 24 and evenly over the candidates in [0,
-// probe_hi) for the rest. A candidate whose header differs fails, so K <= the smallest such e: *bound
-// (~0 when none) is that e, and workgroup 0 lowers K to it, so the waves stop below it from their
-// first batch instead of verifying the whole file before a run that breaks early is seen (the
-// reference bench's log breaks at entry 10, where its keys grow a digit: config 1, 0.19 ms -> ).
+// Header probes (the unpublished path only). The first header mismatch of a run past its entry 1: the
+// smallest e in (1, nc - 1) whose header bytes or IOController bounds differ from the memo
+// (uni_header_ok), where candidate nc - 1 lies past the file's last whole entry and always fails. Rounds
+// of one probe per thread: the smallest failing probe bounds it from above, the largest passing probe
+// below that from below, so the interval shrinks ~1000-fold per round; the first round probes powers of
+// two, then evenly, so a break near the run's start (the reference bench's log: entry 10) or anywhere
+// else is bracketed at once. A run is a contiguous block of equal headers, so the search is exact; where
+// it is not (a header equal to the memo again after a different one) it returns a later mismatch, which
+// costs speed only: the verification's K stops at the first real failure. Returns nc - 1 when no probe of
+// the first round fails (the run reaches the end of the file as far as sampled, and no refinement round
+// is paid: a file one run covers, configs 2, 4, 5). Probes whose bytes lie at or past probe_hi (a chunked
+// scan's bytes still in flight) are not taken. All threads of the workgroup call it.
 #ifndef LDB_UNI_NOPROBE
 #define LDB_UNI_NOPROBE 0   // A/B: no header probes
 #endif
-__device__ __forceinline__ uint64_t uni_probe(const Pipe& p, const UniMemo& m, uint64_t probe_hi) {
-  __shared__ unsigned long long pb;
-  if (threadIdx.x == 0) pb = ~0ull;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const uint32_t t = threadIdx.x;
-    const uint64_t sz = m.sz, need = sz > 48 ? sz : 48;
-    const uint64_t ncand = p.len / sz + 1;
-    const uint64_t e = t < 24 ? (4ull << t) : (ncand * (uint64_t)(t - 23)) / 41;
-    const uint64_t x = e * sz;
-    if (e >= 2 && e < ncand && x + need <= probe_hi) {
+__device__ uint64_t uni_boundary(const Pipe& p, const UniMemo& m, uint64_t y, uint64_t nc, uint64_t probe_hi) {
+  __shared__ unsigned long long s_fail, s_pass;
+  const uint64_t sz = m.sz, need = sz > 48 ? sz : 48;
+  uint64_t lo = 1, hi = nc - 1;
+  for (int round = 0; hi > lo + 1; ++round) {
+    if (threadIdx.x == 0) {
+      s_fail = hi;
+      s_pass = lo;
+    }
+    __syncthreads();
+    const uint64_t w = hi - lo - 1, t = threadIdx.x, nt = blockDim.x;
+    uint64_t e;
+    if (round == 0) e = t < 40 ? lo + (2ull << t) : lo + 1 + (w * (t - 40)) / (nt - 40);
+    else e = lo + 1 + (w * t) / nt;
+    const uint64_t x = y + e * sz;
+    bool pass = false;
+    if (e > lo && e < hi && x + need <= probe_hi) {
       auto word = [&](int i) -> uint32_t {
-        uint32_t w = 0;
+        uint32_t v = 0;
         for (int b = 0; b < 4; ++b) {
           const uint64_t a = x + 4 * (uint64_t)i + b;
-          w |= (a < p.len ? (uint32_t)p.img[a] : 0u) << (8 * b);
+          v |= (a < p.len ? (uint32_t)p.img[a] : 0u) << (8 * b);
         }
-        return w;
+        return v;
       };
-      if (!uni_header_ok(m, word, x, p.len, p.io)) atomicMin(&pb, (unsigned long long)e);
+      pass = uni_header_ok(m, word, x, p.len, p.io);
+      if (!pass) atomicMin(&s_fail, (unsigned long long)e);
     }
+    __syncthreads();
+    const uint64_t f = s_fail;
+    if (round == 0 && f == hi) return hi;
+    if (pass && e < f) atomicMax(&s_pass, (unsigned long long)e);
+    __syncthreads();
+    lo = s_pass;
+    hi = f;
+    __syncthreads();
   }
-  __syncthreads();
-  return pb;
+  return hi;
 }
 
-__device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_t* T, uint64_t probe_hi,
-                                            uint64_t& bound) {
+// The combine tables for geometry g: T[t][q][b] = shift(b << 8q, n_t bytes) are linear in b: 32 basis
+// registers per table (one multmodp each, one thread each), then every entry an xor of its bits' basis
+// values. (Round 2: one 32-step multmodp per entry, 3 x 1024 of them per workgroup: most of the setup.)
+// gT: also written there (workgroup 0's publication), or null. All threads call it.
+__device__ __forceinline__ void uni_build_comb(const Pipe& p, const UniGeo& g, uint32_t* T, uint32_t* gT) {
+  __shared__ uint32_t basis[kUniTabWords / 1024][32];
+  const uint32_t nt = uni_ntab(g);
+  const uint32_t t = threadIdx.x >> 5, bit = threadIdx.x & 31u;
+  if (t < nt) {
+    const uint32_t xt = g.G <= kUniDirectG ? p.xw[(t + 1) * g.P] : p.xw[g.P << t];   // d P <= 7 * 96 < kW
+    basis[t][bit] = multmodp(xt, 1u << bit);
+  }
+  if (LDB_UNI_CH2 && threadIdx.x >= 1024 - 32) {   // the second chain's length (kUniHalfTab)
+    basis[kUniHalfTab][bit] = multmodp(p.xw[8 * (g.S - g.S / 2)], 1u << bit);
+  }
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) {
+    if (e >= nt * 1024u && e < kUniHalfTab * 1024u) continue;
+    const uint32_t tt = e >> 10, q = (e >> 8) & 3u, b = e & 255u;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) v ^= ((b >> i) & 1u) ? basis[tt][8 * q + i] : 0u;
+    T[e] = v;
+    if (gT) gT[e] = v;
+  }
+  __syncthreads();
+}
+
+// kMulti (the device path's whole-image launch): after run 0 (entry 0's memo, as below), each run's
+// header boundary (uni_boundary) becomes the next run's entry 0 when that entry is a run start too (a
+// memo, a slicing, and an entry 1 with the same header), up to kUniMaxRuns runs. Otherwise (and always
+// for a chunked or batched scan) there is one run, and a boundary inside it is a failure: *bound = its
+// chain index, and workgroup 0 lowers K to it.
+template <bool kMulti>
+__device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns& ru, uint32_t* T,
+                                            uint64_t probe_hi, uint64_t& bound) {
   bound = ~0ull;
   __shared__ int published;
   UniSetup* gsu = reinterpret_cast<UniSetup*>(p.uni);
-  const uint32_t* gT = reinterpret_cast<const uint32_t*>(p.uni + kUniSetupBytes);
+  uint32_t* gT = reinterpret_cast<uint32_t*>(p.uni + kUniSetupBytes);
   if (threadIdx.x == 0) {
     published = __hip_atomic_load(&p.dyn[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == kUniReady;
     if (published) su = *gsu;
   }
   __syncthreads();
+  auto run0 = [&] {   // thread 0
+    ru.r[0].m = su.m;
+    ru.r[0].g = su.g;
+    ru.r[0].y = 0;
+    ru.r[0].gbase = 0;
+    ru.r[0].nc = p.len / su.m.sz + 1;
+    ru.n = 1;
+  };
   if (published) {
     if (!su.g.ok) return false;
+    if (threadIdx.x == 0) run0();
     for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) T[e] = gT[e];
+    __syncthreads();
     return true;
   }
   // bytes [0, kUniWin) of the image, zero past len, staged once: entry 0's header and entry 1's (sz <=
@@ -465,47 +548,76 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, uint32_
     }
     if (su.g.ok) {
       if (blockIdx.x == 0) p.dyn[1] = su.m.sz;
+      run0();
     } else if (blockIdx.x == 0) {
       p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
     }
   }
   __syncthreads();
-  if (su.g.ok && !LDB_UNI_NOPROBE) {
-    bound = uni_probe(p, su.m, probe_hi);
-    if (bound != ~0ull && blockIdx.x == 0 && threadIdx.x == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)bound);
-  }
-  if (su.g.ok) {
-    // The combine tables T[t][q][b] = shift(b << 8q, n_t bytes) are linear in b: 32 basis registers per
-    // table (one multmodp each, one thread each), then every entry an xor of its bits' basis values.
-    // (Round 2: one 32-step multmodp per entry, 3 x 1024 of them per workgroup: most of the setup.)
-    __shared__ uint32_t basis[kUniTabWords / 1024][32];
-    const uint32_t nt = uni_ntab(su.g);
-    const uint32_t t = threadIdx.x >> 5, bit = threadIdx.x & 31u;
-    if (t < nt) {
-      const uint32_t xt = su.g.G <= kUniDirectG ? p.xw[(t + 1) * su.g.P] : p.xw[su.g.P << t];   // d P <= 7 * 96 < kW
-      basis[t][bit] = multmodp(xt, 1u << bit);
-    }
-    if (LDB_UNI_CH2 && threadIdx.x >= 1024 - 32) {   // the second chain's length (kUniHalfTab)
-      basis[kUniHalfTab][bit] = multmodp(p.xw[8 * (su.g.S - su.g.S / 2)], 1u << bit);
-    }
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) {
-      if (e >= nt * 1024u && e < kUniHalfTab * 1024u) continue;
-      const uint32_t tt = e >> 10, q = (e >> 8) & 3u, b = e & 255u;
-      uint32_t v = 0;
-#pragma unroll
-      for (uint32_t i = 0; i < 8; ++i) v ^= ((b >> i) & 1u) ? basis[tt][8 * q + i] : 0u;
-      T[e] = v;
-      if (blockIdx.x == 0) const_cast<uint32_t*>(gT)[e] = v;
-    }
-  }
-  if (blockIdx.x == 0) {   // publish: the tables and the setup, then the flag (release)
+  if (su.g.ok) uni_build_comb(p, su.g, T, blockIdx.x == 0 ? gT : nullptr);
+  if (blockIdx.x == 0) {   // publish run 0 (a chunked scan's later launches): the tables, the setup, the flag
     if (threadIdx.x == 0) *gsu = su;
     __threadfence();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&p.dyn[2], kUniReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
-  return su.g.ok != 0;
+  if (!su.g.ok) return false;
+  if (LDB_UNI_NOPROBE) return true;
+  __shared__ int s_next;
+  for (;;) {
+    UniRun& r = ru.r[ru.n - 1];
+    const uint64_t M = uni_boundary(p, r.m, r.y, r.nc, probe_hi);
+    if (M >= r.nc - 1) break;   // no boundary inside: the run reaches the end of the file
+    const uint64_t yn = r.y + M * r.m.sz, ya = yn & ~3ull;
+    const bool more = kMulti && ru.n < kUniMaxRuns;
+    if (more) {   // the next run's entries 0 and 1, staged as run 0's were (one round trip, decoded from LDS)
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < kUniWin / 4; i += blockDim.x) {
+        const uint64_t a0 = ya + 4ull * i;
+        uint32_t w = 0;
+        if (a0 + 4 <= p.len) {
+          w = *reinterpret_cast<const uint32_t*>(p.img + a0);
+        } else {
+          for (uint32_t k = 0; k < 4; ++k) w |= (a0 + k < p.len ? (uint32_t)p.img[a0 + k] : 0u) << (8 * k);
+        }
+        win[i] = w;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      s_next = 0;
+      if (more) {
+        UniRun& q = ru.r[ru.n];
+        q.y = yn;
+        const uint32_t o = (uint32_t)(yn - ya);   // 0..3
+        q.m = uni_memo([&](int i) -> uint32_t { return wb[o + i]; }, p.len, p.io, q.y);
+        q.g = q.m.ok ? uni_geometry(p.xw, (uint32_t)(q.m.sz - 4)) : UniGeo{};
+        if (q.g.ok) {
+          const uint64_t x1 = q.y + q.m.sz;
+          const uint8_t* h = wb + o + q.m.sz;   // o + sz + 40 < kUniWin
+          auto word = [&](int i) -> uint32_t {
+            return (uint32_t)h[4 * i] | ((uint32_t)h[4 * i + 1] << 8) | ((uint32_t)h[4 * i + 2] << 16) |
+                   ((uint32_t)h[4 * i + 3] << 24);
+          };
+          if (uni_header_ok(q.m, word, x1, p.len, p.io)) {
+            q.gbase = r.gbase + M;
+            q.nc = (p.len - q.y) / q.m.sz + 1;
+            r.nc = M;   // entry M of run r is the next run's entry 0
+            ru.n += 1;
+            s_next = 1;
+          }
+        }
+      }
+      if (!s_next && blockIdx.x == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(r.gbase + M));
+    }
+    __syncthreads();
+    if (!s_next) {
+      bound = r.gbase + M;   // a failure of the last run: K <= bound
+      break;
+    }
+  }
+  __syncthreads();
+  return true;
 }
 
 // Combine level D of the group's tree: lanes j = 2D - 1 (mod 2D) take lane j - D's register shifted
@@ -530,8 +642,9 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 // hashes are still stored in the loop.
 // kAl: every window and header starts on a dword (sz and t multiples of 4, as for LazyDB's 332-B
 // config 2/4/5 entries): no funnel shifts (22 v_alignbyte per batch at S = 11).
+// One run (ru): its entry e at ru.y + e sz is chain entry ru.gbase + e; candidates e < ru.nc.
 template <int S, bool kChunk, bool kHash, bool kFill, bool kAl>
-__device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, const uint8_t* lp2, const uint32_t* T,
+__device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, const uint8_t* lp2, const uint32_t* T,
                                           int lane, int wave, uint64_t a_lo, uint64_t a_hi, uint64_t bound) {
   if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
     a_lo = 0;
@@ -567,7 +680,8 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     lm1[k] = n >= 8 ? 0u : (n > 4 ? 0xFFFFFFFFu << (8 * (n - 4)) : 0xFFFFFFFFu);
   }
   GpuWave wp{lane};
-  const uint64_t nbatch = kChunk ? ~0ull : (p.len / sz + E) / E;   // !kChunk: ceil(ncand / E), ncand = len / sz + 1
+  const uint64_t nbatch = kChunk ? ~0ull : (su.nc + E - 1) / E;   // !kChunk: ceil(nc / E)
+  const uint64_t y0 = su.y, gb = su.gbase;   // (kChunk: one run, y0 = gb = 0)
   // K as last seen: the load issued in one batch is tested at the top of the next, so its latency hides
   // behind the batch (a batch past K only costs its own time: the run's tuples stop at K anyway)
   v2u32 kv = {(uint32_t)bound, (uint32_t)(bound >> 32)};   // K as loaded during the previous batch (vector value:
@@ -578,16 +692,16 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     // uniform by construction (one address), but a load's result is divergent to the compiler: the
     // loop exit on it would make b, and every descriptor built from b, divergent (waterfall loops)
     const uint64_t kseen = ((uint64_t)__builtin_amdgcn_readfirstlane(kv[1]) << 32) | __builtin_amdgcn_readfirstlane(kv[0]);
-    if (b * E >= kseen) break;
+    if (gb + b * E >= kseen) break;
 
     // Opaque per-batch copies: the uniform step / level conditions and the lane masks derived from
     // them are evaluated inside the batch, not hoisted out of the loop as a bank of held SGPR masks.
     uint32_t GG = __builtin_amdgcn_readfirstlane(G), c = ~j & (j + 1);
     asm volatile("" : "+s"(GG), "+v"(c));
     const uint64_t e = b * E + ((uint32_t)lane >> lg);
-    const uint64_t x = e * sz;
+    const uint64_t x = y0 + e * sz;
     if (kChunk && (b + 1) * Esz + need <= a_lo) continue;   // wave-uniform: below the launch's range (b_first's slack)
-    const uint64_t b0 = b * E * sz;
+    const uint64_t b0 = y0 + b * E * sz;
     const uint64_t base = b0 >= 512 ? (b0 - 512) & ~15ull : 0;   // wave-uniform; the lead t < 8 G <= 512
     const uint64_t nrec = (p.len - base + 3) & ~3ull;
     const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)min(nrec, (uint64_t)0xFFFFFFFFu));
@@ -695,7 +809,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
     // an opaque offset, so its words stay per-batch VGPR loads instead of SGPRs held across the loop.
     bool ok = false;
     uint32_t crc = 0;
-    bool mine = x <= p.len;
+    bool mine = e < su.nc && x <= p.len;
     if (kChunk) {
       uint64_t lo_ = a_lo, hi_ = all_hi ? ~0ull : a_hi;   // opaque per batch: not held across the loop
       lo_ = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo_ >> 32)) << 32) |
@@ -726,8 +840,8 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
 #endif
     const uint64_t bad = __ballot((last && mine && !ok) ? 1 : 0);
     if (bad && lane == 0)
-      atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
-    if (ok && e < p.cap && (!fill || kHash)) {
+      atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(gb + b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
+    if (ok && gb + e < p.cap && (!fill || kHash)) {
       uint32_t z = 0;
       asm volatile("" : "+v"(z));
       const UniMemo& m = *(&su.m + z);
@@ -745,13 +859,13 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
         en.enc_hdr_size = (uint8_t)m.enc;
         en.pad_[0] = en.pad_[1] = en.pad_[2] = 0;
         en.fid = p.fid;
-        reinterpret_cast<ldb_entry*>(p.out)[e] = en;
+        reinterpret_cast<ldb_entry*>(p.out)[gb + e] = en;
       } else {
-        store_tuple(reinterpret_cast<ldb_index_tuple*>(p.out) + e, uni_pos(m, x), m.k, m.v);
+        store_tuple(reinterpret_cast<ldb_index_tuple*>(p.out) + gb + e, uni_pos(m, x), m.k, m.v);
       }
       if (kHash) {   // merge mode: the key's hash, from the lines this wave just loaded
         const uint32_t kx = hx + m.hs;
-        p.hash_out[e] = key_hash_w(
+        p.hash_out[gb + e] = key_hash_w(
             [&](uint32_t i, uint64_t* w) {
               const uint32_t a0 = kx + i, al = a0 & ~3u, s0 = a0 & 3u;
               const uint4 q = ld16(rs, al);
@@ -773,26 +887,33 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniSetup& su, con
 // may still drop) lies beyond n_entries, where the region pipeline writes its own tuples from K on.
 // (Round 4: per-wave stores of each wave's own batches, 4 scattered 256-B pieces per instruction, cost
 // 61 us at config 4 against 33 for the separate dense sweep.)
-__device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniMemo& m) {
+__device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniRuns& ru) {
   __syncthreads();
-  const uint64_t sz = m.sz, ncand = p.len / sz + 1;
+  const UniRun& rl = ru.r[ru.n - 1];
+  const uint64_t ntot = rl.gbase + rl.nc;   // chain entries over every run
   const uint64_t K = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t n = K < ncand ? K : ncand;
+  uint64_t n = K < ntot ? K : ntot;
   n = n < p.cap ? n : p.cap;
-  const uint64_t per = (ncand + gridDim.x - 1) / gridDim.x;
+  const uint64_t per = (ntot + gridDim.x - 1) / gridDim.x;
   const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
   ldb_index_tuple* out = reinterpret_cast<ldb_index_tuple*>(p.out);
-  for (uint64_t e = lo + threadIdx.x; e < hi; e += blockDim.x) store_tuple(out + e, uni_pos(m, e * sz), m.k, m.v);
+  for (int r = 0; r < ru.n; ++r) {   // this workgroup's slice, run by run
+    const UniRun& q = ru.r[r];
+    const uint64_t a = lo > q.gbase ? lo : q.gbase, z = q.gbase + q.nc < hi ? q.gbase + q.nc : hi;
+    const uint64_t sz = q.m.sz, ya = q.y - q.gbase * sz;   // x of chain entry g in run r: ya + g sz (mod 2^64)
+    for (uint64_t g = a + threadIdx.x; g < z; g += blockDim.x) store_tuple(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
+  }
 }
 
 // The device path's run prefix, finished (the last k_uniform workgroup to be done, after every
-// workgroup's K update): when the chain stops right at x0 = K sz -- the header window there is
-// unreadable (io.EOF), or it decodes as the zero sentinel (ErrLogEndOfFile), a key/value read past the
-// bound (io.EOF) or a malformed header (log_file.go:116-139) -- the scan is complete: this writes the
-// ldb_scan_result and sets dyn[3] = kUniDone, and the region pipeline's kernels leave at once. A file
-// the run covers to its terminal (BASELINE configs 2, 4, 5) then pays no region kernel work.
+// workgroup's K update): x0 = the position of chain entry K over the runs (dyn[5], chain_x0). When the
+// chain stops right there -- the header window there is unreadable (io.EOF), or it decodes as the zero
+// sentinel (ErrLogEndOfFile), a key/value read past the bound (io.EOF) or a malformed header
+// (log_file.go:116-139) -- the scan is complete: this writes the ldb_scan_result and sets dyn[3] =
+// kUniDone, and the region pipeline's kernels leave at once. A file the runs cover to its terminal
+// (BASELINE configs 1, 2, 4, 5) then pays no region kernel work.
 constexpr uint64_t kUniDone = 0xD0E5CA11D0E5CA11ull;
-__device__ __forceinline__ void uni_finish(const Pipe& p, uint64_t sz) {
+__device__ __forceinline__ void uni_finish(const Pipe& p, const UniRuns& ru) {
   __shared__ int s_last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -805,7 +926,10 @@ __device__ __forceinline__ void uni_finish(const Pipe& p, uint64_t sz) {
   p.dyn[4] = 0;
   const uint64_t K = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (K == ~0ull) return;   // (unreachable: the candidate at or past len always fails)
-  const uint64_t x0 = K * sz;
+  int r = ru.n - 1;
+  while (r > 0 && ru.r[r].gbase > K) --r;
+  const uint64_t x0 = ru.r[r].y + (K - ru.r[r].gbase) * ru.r[r].m.sz;
+  p.dyn[5] = x0;
   int32_t st;
   if (read_eof(p.len, p.io, (int64_t)x0, kMaxHeader)) {
     st = LDB_EOF_WINDOW;
@@ -837,11 +961,38 @@ __device__ __forceinline__ bool scan_done(const Pipe& p) { return p.dyn[3] == kU
 // with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
 // LDS: the 64 KiB LP2 block, the combine tables and the setup (~90 KiB): one workgroup of 16 waves per
 // CU, 4 waves per SIMD, up to 128 VGPRs.
+// One run's verification: uni_waves instantiated for its slicing S and alignment (a switch over S on
+// a wave-uniform value).
+template <bool kChunk, bool kHash, bool kFill>
+__device__ __forceinline__ void uni_run(const Pipe& p, const UniRun& q, const uint8_t* lp2, const uint32_t* comb,
+                                        int lane, int wave, uint64_t a_lo, uint64_t a_hi, uint64_t bound) {
+  const bool al = (q.m.sz & 3u) == 0 && (q.g.t & 3u) == 0 && (q.y & 3u) == 0;   // every window and header dword-aligned
+  switch (q.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
+#define LDB_UNI_CASE(n)                                                                             \
+  case n:                                                                                           \
+    if (al) uni_waves<n, kChunk, kHash, kFill, true>(p, q, lp2, comb, lane, wave, a_lo, a_hi, bound);  \
+    else uni_waves<n, kChunk, kHash, kFill, false>(p, q, lp2, comb, lane, wave, a_lo, a_hi, bound);    \
+    break;
+    LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
+    LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
+#undef LDB_UNI_CASE
+    default: break;
+  }
+}
+
+// kChunk: a_lo, a_hi: image bytes [0, a_hi) are in place; candidates not already taken by a launch
+// with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
+// LDS: the 64 KiB LP2 block, the combine tables and the setup (~90 KiB): one workgroup of 16 waves per
+// CU, 4 waves per SIMD, up to 128 VGPRs. The device path (!kChunk, !kHash) verifies every run of the
+// log (UniRuns) and writes the INDEX tuples itself; a chunked scan (the image still arriving over
+// PCIe) and the merge's hashed scans take the first run only.
 template <bool kChunk, bool kHash>
 __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_lo, uint64_t a_hi) {
   __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
   __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];   // combine tables (shift by 2^i P bytes)
   __shared__ UniSetup su;
+  __shared__ UniRuns ru;
+  constexpr bool kMulti = !kChunk && !kHash;
 #ifdef LDB_STAMPS   // setup cost: slot 9 the LP2 block, slot 17 uni_prepare (thread 0 of every workgroup)
   uint64_t t0_, t1_, t2_;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_) :: "memory");
@@ -852,7 +1003,7 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_) :: "memory");
 #endif
   uint64_t bound;
-  if (!uni_prepare(p, su, comb, kChunk ? a_hi : p.len, bound)) return;   // (its __syncthreads also publish the LP2 block)
+  if (!uni_prepare<kMulti>(p, su, ru, comb, kChunk ? a_hi : p.len, bound)) return;   // (its __syncthreads also publish the LP2 block)
   __syncthreads();
 #ifdef LDB_STAMPS
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2_) :: "memory");
@@ -863,21 +1014,16 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
 #endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool al = (su.m.sz & 3u) == 0 && (su.g.t & 3u) == 0;   // every window and header dword-aligned
-  constexpr bool kPost = !kChunk && !kHash;
-  switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n)                                                                    \
-  case n:                                                                                  \
-    if (al) uni_waves<n, kChunk, kHash, !kHash, true>(p, su, lp2, comb, lane, wave, a_lo, a_hi, bound); \
-    else uni_waves<n, kChunk, kHash, !kHash, false>(p, su, lp2, comb, lane, wave, a_lo, a_hi, bound); \
-    break;
-    LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
-    LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
-#undef LDB_UNI_CASE
-    default: break;
+  for (int r = 0; r < ru.n; ++r) {
+    const UniRun& q = ru.r[r];
+    if (r > 0 && (q.g.G != ru.r[r - 1].g.G || q.g.P != ru.r[r - 1].g.P)) {
+      __syncthreads();   // every wave is done with the previous run's combine tables
+      uni_build_comb(p, q.g, comb, nullptr);
+    }
+    uni_run<kChunk, kHash, !kHash>(p, q, lp2, comb, lane, wave, a_lo, a_hi, bound);
   }
-  if (kPost && p.kind == LDB_TUPLE_INDEX) uni_post_fill(p, su.m);
-  if (!kChunk || a_hi >= p.len) uni_finish(p, su.m.sz);
+  if (kMulti && p.kind == LDB_TUPLE_INDEX) uni_post_fill(p, ru);
+  if (!kChunk || a_hi >= p.len) uni_finish(p, ru);
 }
 static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
 
@@ -954,24 +1100,14 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
   __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];
   __shared__ UniSetup su;
+  __shared__ UniRuns ru;
   lp2_build(lp2, p.gtab);
   uint64_t bound;
-  if (!uni_prepare(p, su, comb, p.len, bound)) return;
+  if (!uni_prepare<false>(p, su, ru, comb, p.len, bound)) return;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool al = (su.m.sz & 3u) == 0 && (su.g.t & 3u) == 0;   // every window and header dword-aligned
-  switch (su.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n)                                                                         \
-  case n:                                                                                       \
-    if (al) uni_waves<n, false, false, true, true>(p, su, lp2, comb, lane, wave, 0, p.len, bound);  \
-    else uni_waves<n, false, false, true, false>(p, su, lp2, comb, lane, wave, 0, p.len, bound);    \
-    break;
-    LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
-    LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
-#undef LDB_UNI_CASE
-    default: break;
-  }
+  uni_run<false, false, true>(p, ru.r[0], lp2, comb, lane, wave, 0, p.len, bound);
 }
 // ---------------------------------------------------------------- k_scan_main
 template <bool kB>
@@ -1862,11 +1998,12 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
 
 // the control words every region pipeline starts from (enqueue_scan)
 // dyn: [0] K (dyn_val: ~0 = no failure seen, 0 = no run), [1] entry size, [2] setup flag, [3] done
-// flag (uni_finish), [4] k_uniform's done counter
+// flag (uni_finish), [4] k_uniform's done counter, [5] x0 (uni_finish)
 __global__ __launch_bounds__(64) void k_init(uint32_t* ctr, uint64_t* dyn, uint64_t dyn_val) {
   if (threadIdx.x < 8) ctr[threadIdx.x] = 0u;
   if (threadIdx.x < 3) dyn[threadIdx.x] = dyn_val;
   if (threadIdx.x == 3 || threadIdx.x == 4) dyn[threadIdx.x] = 0;
+  if (threadIdx.x == 5) dyn[5] = ~0ull;   // x0 not finished: K sz (no run: 0)
 }
 
 // persistent k_scan_main workgroups: exactly those resident at once (LDS-limited), so no second
@@ -1931,7 +2068,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   if (serial || len < (uint64_t)kMaxHeader) {
     LDB_HIP(hipMemsetAsync(c->ws + L.o_ctr, 0, 32, s));
     LDB_HIP(hipMemsetAsync(c->ws + L.o_tpos, 0xFF, 16, s));
-    LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0, 32, s));   // no run prefix: the walk starts at 0
+    LDB_HIP(hipMemsetAsync(c->ws + L.o_dyn, 0, 64, s));   // no run prefix: the walk starts at 0 (dyn[5] = x0 = 0)
     hipLaunchKernelGGL(k_serial<false>, dim3(1), dim3(64), 0, s, p, 0, nullptr);
     LDB_HIP(hipGetLastError());
     return fence_ws(c, s);
@@ -2013,7 +2150,8 @@ bool batch_eligible(const uint8_t* img, uint64_t len) {
 __global__ __launch_bounds__(64) void k_batch_init(const Pipe* __restrict__ pb) {
   const Pipe& p = pb[blockIdx.x];
   if (threadIdx.x < 8) p.ctr[threadIdx.x] = 0u;
-  if (threadIdx.x < 4) p.dyn[threadIdx.x] = ~0ull;
+  if (threadIdx.x < 4 || threadIdx.x == 5) p.dyn[threadIdx.x] = ~0ull;   // [3]: not done; [5]: x0 = K sz
+  if (threadIdx.x == 4) p.dyn[4] = 0;
 }
 
 int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s) {

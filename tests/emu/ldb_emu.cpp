@@ -250,7 +250,8 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
   Emu emu;
   const uint64_t nreg = std::max<uint64_t>(1, (len + kW - 1) / kW);
   const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
-  std::vector<uint64_t> blk(nblk, 0), tpos(2, ~0ull), dyn(2, 0);
+  std::vector<uint64_t> blk(nblk, 0), tpos(2, ~0ull), dyn(8, 0);
+  dyn[5] = ~0ull;   // x0 = K sz (one run; the GPU's uni_finish writes x0 over several runs)
   std::vector<RegionSum> rs(nreg);
   std::vector<uint32_t> ctr(8, 0);
   std::vector<ldb_index_tuple> scratch(nreg * (uint64_t)kRegionCap);

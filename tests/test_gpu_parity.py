@@ -5,6 +5,7 @@ sizes, EncodeEntry sizes, stat, key/value sizes; ENTRY kind adds crc, expiredAt,
 txid, txstat, fid).
 """
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -235,6 +236,62 @@ def test_run_prefix_capacity(eng):
     assert np.array_equal(tup["pos"], rt["pos"][:1000])
 
 
+def _runs_log(spec, seed):
+    """Runs of equal-sized entries one after another: spec = [(n, klen, vlen, expired_at), ...]."""
+    return b"".join(_fixed_log(n, k, v, seed + 31 * i, expired_at=e) for i, (n, k, v, e) in enumerate(spec))
+
+
+@pytest.mark.parametrize("case", ["steps", "aligned", "many", "single_between", "repeat", "cut"])
+def test_piecewise_runs(eng, case):
+    """Round 4: a log that is several runs of equal-sized entries (the reference bench's keys grow a
+    digit at entries 10, 100, ...; fixed-schema writers whose key or value width steps) is verified run
+    by run in k_uniform: K counts entries along the chain over the runs, x0 follows the runs, and a file
+    the runs cover to its terminal needs no region kernel. Runs of every slicing (entries 29 B .. 5 KB,
+    starts not dword-aligned), more runs than k_uniform keeps (8; the rest go to the region pipeline), a
+    lone entry between runs, a run shape that recurs after another one (the boundary search is then only
+    an upper bound), corruption at a run's first, middle and last entry, a 240 KiB zero tail and a cut
+    end; both IOController rules, both tuple kinds, bit-exact."""
+    rng = random.Random(zlib.crc32(case.encode()))
+    if case == "steps":       # the reference bench's shape, small: key widths 16..21
+        spec = [(10, 16, 512, 0), (90, 17, 512, 0), (900, 18, 512, 0), (2000, 19, 512, 0), (500, 20, 512, 0)]
+    elif case == "aligned":   # 332-B and 100-B entries: dword-aligned runs, and runs whose start is not
+        spec = [(700, 64, 256, 0), (333, 13, 75, 0), (701, 64, 256, 0), (50, 9, 9, 0), (300, 40, 1000, 0)]
+    elif case == "many":      # 11 runs: k_uniform takes 8
+        spec = [(40 + 7 * i, 10 + i, 30 + 13 * i, 0) for i in range(11)]
+    elif case == "single_between":   # run, one entry, run (the lone entry is not a run start)
+        spec = [(500, 16, 100, 0), (1, 16, 37, 0), (600, 16, 100, 0), (400, 20, 5000, 0)]
+    elif case == "repeat":    # A, B, A, B with A and B of equal size (expiry differs): non-monotone headers
+        spec = [(300, 16, 100, 0), (200, 16, 100, 1700000000), (300, 16, 100, 0), (200, 16, 100, 1700000001)]
+    else:                     # cut inside the last run
+        spec = [(100, 16, 200, 0), (1000, 18, 200, 0)]
+    log = _runs_log(spec, rng.randrange(1 << 30))
+    n_all = sum(x[0] for x in spec)
+    bounds = [0]
+    for (nn, k, v, e) in spec:
+        bounds.append(bounds[-1] + len(_fixed_log(1, k, v, 1, expired_at=e)) * nn)
+    imgs = [np.frombuffer(log + bytes(240 << 10), np.uint8).copy()]
+    if case == "cut":
+        imgs = [np.frombuffer(log[: len(log) - 150], np.uint8).copy()]
+    base = imgs[0]
+    # corrupt a byte of run 2's (or the last run's) first, middle and last entry
+    r = min(2, len(spec) - 1)
+    esz = (bounds[r + 1] - bounds[r]) // spec[r][0]
+    for k in (0, spec[r][0] // 2, spec[r][0] - 1):
+        im = base.copy()
+        im[bounds[r] + k * esz + rng.choice([0, 6, esz - 1])] ^= 0x20
+        imgs.append(im)
+    for i, im in enumerate(imgs):
+        d = to_dev(im)
+        for io in (0, 1):
+            for kind in (0, 1):
+                res, tup = eng.scan_dev(d, io_type=io, kind=kind, cap=n_all + 64)
+                ref, rt = coracle.scan(im, io, tuple_kind=kind, cap=n_all + 64)
+                assert_same(res, tup, ref, rt, kind=kind)
+                if i == 0 and case in ("steps", "aligned") and kind == 0:
+                    # every run went through k_uniform and it ended the scan (no region kernel)
+                    assert res.n_run == n_all and res.n_regions == 0, (res.n_run, n_all, res.n_regions)
+
+
 @pytest.mark.parametrize("io_type", [1, 0])
 def test_config1_reference_bench_log(eng, io_type):
     """BASELINE config 1 at its stated size, in the reference benchmark's own shape
@@ -249,6 +306,9 @@ def test_config1_reference_bench_log(eng, io_type):
     assert ref.status == 2 and ref.end_off == end and ref.n_entries == n
     res, tup = eng.scan_dev(d, io_type=io_type, cap=n + 16)
     assert_same(res, tup, ref, rt)
+    # round 4: its six runs (key widths 16..21) all go through k_uniform, which ends the scan at the
+    # sentinel, so the 240 MiB zero tail is never staged
+    assert res.n_run == n and res.n_regions == 0, (res.n_run, res.n_regions)
     res1, tup1 = eng.scan_dev(d, io_type=io_type, cap=n + 16, kind=1)
     ref1, rt1 = coracle.scan(img, io_type, tuple_kind=1)
     assert_same(res1, tup1, ref1, rt1, kind=1)
