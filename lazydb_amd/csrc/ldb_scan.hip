@@ -270,6 +270,22 @@ __device__ __forceinline__ void copy_tables(uint32_t* tab, const uint32_t* gtab)
 
 #ifdef LDB_STAMPS
 __device__ uint64_t g_stamps[kStampSlots];
+// k_uniform's phases (tools/uni_stamps.py), thread 0 of every workgroup: 0 run 0's window, 1 its decode +
+// combine tables + publication, 2 header probes, 3 later runs' windows, 4 their decodes, 5 combine
+// rebuilds between runs, 6 the verify loops, 7 the INDEX fill, 8 uni_finish
+constexpr int kUniStampSlots = 16;
+__device__ uint64_t g_ustamps[kUniStampSlots];
+__device__ __forceinline__ uint64_t uni_now() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  return t;
+}
+#define UNI_T(v) const uint64_t v = uni_now()
+#define UNI_ADD(slot, a, b) \
+  do { if (threadIdx.x == 0) atomicAdd((unsigned long long*)&g_ustamps[slot], (unsigned long long)((b) - (a))); } while (0)
+#else
+#define UNI_T(v)
+#define UNI_ADD(slot, a, b)
 #endif
 
 // ---------------------------------------------------------------- k_uniform
@@ -420,32 +436,50 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 #ifndef LDB_UNI_NOPROBE
 #define LDB_UNI_NOPROBE 0   // A/B: no header probes
 #endif
-__device__ uint64_t uni_boundary(const Pipe& p, const UniMemo& m, uint64_t y, uint64_t nc, uint64_t probe_hi) {
+// One probe: run r's candidate at x matches the memo (uni_header_ok) -- the header words by aligned
+// dword loads (<= 12 of them, one round trip) instead of byte loads.
+__device__ __forceinline__ bool uni_probe_ok(const Pipe& p, const UniMemo& m, uint64_t x) {
+  const uint64_t xa = x & ~3ull;
+  const uint32_t sh = (uint32_t)(x & 3u);
+  uint32_t d[11];
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    const uint64_t a = xa + 4ull * i;
+    uint32_t v = 0;
+    if (i <= (int)m.nw + 1) {
+      if (a + 4 <= p.len) {
+        v = *reinterpret_cast<const uint32_t*>(p.img + a);
+      } else {
+        for (uint32_t k = 0; k < 4; ++k) v |= (a + k < p.len ? (uint32_t)p.img[a + k] : 0u) << (8 * k);
+      }
+    }
+    d[i] = v;
+  }
+  auto word = [&](int i) -> uint32_t { return funnel(d[i + 1], d[i], sh); };
+  return uni_header_ok(m, word, x, p.len, p.io);
+}
+
+__device__ uint64_t uni_boundary(const Pipe& p, const UniMemo& m, uint64_t y, uint64_t nc, uint64_t probe_hi,
+                             uint32_t nt0) {
   __shared__ unsigned long long s_fail, s_pass;
   const uint64_t sz = m.sz, need = sz > 48 ? sz : 48;
   uint64_t lo = 1, hi = nc - 1;
   for (int round = 0; hi > lo + 1; ++round) {
-    if (threadIdx.x == 0) {
+    // round 0: threads 0..nt0-1 (entries lo + 2^(t+1) for t < 24, then evenly); later rounds: every
+    // thread evenly over (lo, hi), so the interval shrinks ~blockDim-fold per round
+    const uint32_t nt = round == 0 ? nt0 : blockDim.x, t = threadIdx.x;
+    if (t == 0) {
       s_fail = hi;
       s_pass = lo;
     }
     __syncthreads();
-    const uint64_t w = hi - lo - 1, t = threadIdx.x, nt = blockDim.x;
-    uint64_t e;
-    if (round == 0) e = t < 40 ? lo + (2ull << t) : lo + 1 + (w * (t - 40)) / (nt - 40);
-    else e = lo + 1 + (w * t) / nt;
+    const uint64_t w = hi - lo - 1;
+    uint64_t e = 0;
+    if (t < nt) e = round == 0 ? (t < 24 ? lo + (2ull << t) : lo + 1 + (w * (t - 23)) / (nt - 23)) : lo + 1 + (w * t) / nt;
     const uint64_t x = y + e * sz;
     bool pass = false;
-    if (e > lo && e < hi && x + need <= probe_hi) {
-      auto word = [&](int i) -> uint32_t {
-        uint32_t v = 0;
-        for (int b = 0; b < 4; ++b) {
-          const uint64_t a = x + 4 * (uint64_t)i + b;
-          v |= (a < p.len ? (uint32_t)p.img[a] : 0u) << (8 * b);
-        }
-        return v;
-      };
-      pass = uni_header_ok(m, word, x, p.len, p.io);
+    if (t < nt && e > lo && e < hi && x + need <= probe_hi) {
+      pass = uni_probe_ok(p, m, x);
       if (!pass) atomicMin(&s_fail, (unsigned long long)e);
     }
     __syncthreads();
@@ -488,11 +522,266 @@ __device__ __forceinline__ void uni_build_comb(const Pipe& p, const UniGeo& g, u
   __syncthreads();
 }
 
-// kMulti (the device path's whole-image launch): after run 0 (entry 0's memo, as below), each run's
-// header boundary (uni_boundary) becomes the next run's entry 0 when that entry is a run start too (a
-// memo, a slicing, and an entry 1 with the same header), up to kUniMaxRuns runs. Otherwise (and always
-// for a chunked or batched scan) there is one run, and a boundary inside it is a failure: *bound = its
-// chain index, and workgroup 0 lowers K to it.
+// kMulti (the device path's whole-image launch): a log of several runs one after another. Workgroup 0
+// finds them (uni_discover) while the others stage their tables; the list is published once complete
+// (dyn[6] = the number of runs | kUniFinal, UniRun records at p.uni + kUniRunsOff), and every workgroup
+// then verifies the runs in order. Each run r has its own first-failure word F_r (run 0: dyn[0], then
+// p.uni + kUniFOff), the smallest candidate index within the run known to fail: workgroup 0 starts it
+// at the run's end M_r (its header boundary; the next run's entry 0 lies there), and the verification
+// lowers it at a failing entry. K is then the first run's gbase + F_r with F_r < M_r (a failure inside
+// the run), or the last run's gbase + F_r (uni_finish).
+// Otherwise (a chunked, batched or hashed scan) there is one run, and a boundary inside it is a failure:
+// *bound = its chain index, and workgroup 0 lowers K (dyn[0]) to it.
+// Round 4 history (config 1, the reference bench's log of six runs, k_uniform): every workgroup finding
+// the runs itself, 0.287 ms (256 workgroups probing the same lines: ~5 us a probe round); workgroup 0
+// publishing each run as soon as a probe round bracketed it, so the others verified while it searched,
+// 0.196 ms; the list published once complete, 0.184 ms -- the search is a chain of dependent loads,
+// and the verification's traffic only lengthens it. The chain: per run 1-3 probe rounds (a load round
+// trip, ~1 us, plus three barriers), the next run's header from a probe's own loads (no extra load),
+// decoded through readlane by one wave; the slicing (uni_geometry: a table load and two multmodp) is
+// left to the verifying workgroups, one wave per run.
+#ifndef LDB_UNI_SPIN
+#define LDB_UNI_SPIN 4   // s_sleep between polls of dyn[6] (x 64 cycles)
+#endif
+constexpr uint64_t kUniRunsOff = kUniSetupBytes + 4 * kUniTabWords;
+constexpr uint64_t kUniFOff = kUniRunsOff + 256 * kUniMaxRuns;
+constexpr uint64_t kUniFinal = 1ull << 32;
+constexpr uint64_t kUniBlockBytes = kUniFOff + 8 * kUniMaxRuns;   // the workspace's p.uni block
+static_assert(sizeof(UniRun) <= 256, "run records are 256 B apart");
+__device__ __forceinline__ UniRun* uni_recs(const Pipe& p) { return reinterpret_cast<UniRun*>(p.uni + kUniRunsOff); }
+__device__ __forceinline__ uint64_t* uni_fword(const Pipe& p, int r) {
+  return r == 0 ? p.dyn : reinterpret_cast<uint64_t*>(p.uni + kUniFOff) + r;
+}
+__device__ __forceinline__ uint64_t uni_fload(const uint64_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bytes [a, a + kUniWin) of the image into win (zero past len), one coalesced load per thread and dword
+__device__ __forceinline__ void uni_stage_win(const Pipe& p, uint32_t* win, uint64_t a) {
+  for (uint32_t i = threadIdx.x; i < kUniWin / 4; i += blockDim.x) {
+    const uint64_t a0 = a + 4ull * i;
+    uint32_t w = 0;
+    if (a0 + 4 <= p.len) {
+      w = *reinterpret_cast<const uint32_t*>(p.img + a0);
+    } else {
+      for (uint32_t k = 0; k < 4; ++k) w |= (a0 + k < p.len ? (uint32_t)p.img[a0 + k] : 0u) << (8 * k);
+    }
+    win[i] = w;
+  }
+}
+
+// the slicing exists for entries of L = sz - 4 CRC'd bytes (uni_geometry's shapes, without its KL)
+__device__ __forceinline__ bool uni_sliceable(uint32_t L) {
+  for (uint32_t lg = 0; lg < kUniLevels + 1; ++lg) {
+    const uint32_t G = 1u << lg;
+    if ((((L + G - 1) / G + 7) & ~7u) <= 8 * kUniSteps) return true;
+  }
+  return false;
+}
+
+// Wave 0 of the workgroup, all 64 lanes (wave-uniform control): run q's memo from the entry at image
+// offset y, lane i holding byte y + i (zero past len), decoded through readlane, not by one lane's
+// dependent byte reads (each an LDS or memory round trip: ~5 us per run). kGeo: its slicing too (a
+// table load and two multmodp); otherwise only whether it has one. Lane 0 writes q.m (q.g), q.y.
+template <bool kGeo>
+__device__ __forceinline__ bool uni_decode_wave(const Pipe& p, uint64_t y, uint32_t b, UniRun& q) {
+  auto fetch = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)b, i); };
+  UNI_T(d0);
+  const UniMemo m = uni_memo(fetch, p.len, p.io, y);
+  UNI_T(d1);
+  if (blockIdx.x == 0) UNI_ADD(4, d0, d1);
+  UniGeo g{};
+  bool ok = m.ok;
+  if (kGeo) {
+    if (ok) g = uni_geometry(p.xw, (uint32_t)(m.sz - 4));
+    ok = g.ok;
+  } else {
+    ok = ok && uni_sliceable((uint32_t)(m.sz - 4));
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    q.m = m;
+    if (kGeo) q.g = g;
+    q.y = y;
+  }
+  return ok;
+}
+
+// One discovery probe: candidate x of a run matches its memo (uni_header_ok). The header's dwords from
+// x rounded down, as three 16-B loads (x + 48 <= len, so they stay inside the image); kept in d for the
+// stash (uni_search).
+__device__ __forceinline__ bool uni_probe16(const Pipe& p, const UniMemo& m, uint64_t x, uint32_t* d) {
+  const uint64_t xa = x & ~3ull;
+  const uint32_t sh = (uint32_t)(x & 3u);
+  const uint4* q = reinterpret_cast<const uint4*>(p.img + xa);
+  const uint4 r0 = q[0], r1 = q[1], r2 = q[2];
+  d[0] = r0.x; d[1] = r0.y; d[2] = r0.z; d[3] = r0.w;
+  d[4] = r1.x; d[5] = r1.y; d[6] = r1.z; d[7] = r1.w;
+  d[8] = r2.x; d[9] = r2.y; d[10] = r2.z; d[11] = r2.w;
+  auto word = [&](int i) -> uint32_t { return funnel(d[i + 1], d[i], sh); };
+  return uni_header_ok(m, word, x, p.len, p.io);
+}
+
+// Run q's end M: the smallest candidate in (lo, nc - 1) whose header mismatches (as uni_boundary), by
+// rounds of probes over the whole workgroup. Round 0: 128 probes at lo + 1 .. lo + 128, then 128 spaced
+// geometrically to nc - 1, so a short run ends exactly in one round and a long one is bracketed to ~7 %;
+// later rounds probe every candidate of the bracket (<= blockDim of them) or spread evenly over it. The
+// probes of a wave are in increasing order, so its smallest failing and largest passing probe are one
+// ballot each (one LDS atomic per wave, not per lane). The probe that sets the final M leaves its 48
+// header bytes in stash[0..12) (stash[12] = x & 3): the next run's entry 0 without another load.
+// Returns nc - 1 when round 0 finds no mismatch.
+__device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint32_t* stash) {
+  __shared__ unsigned long long s_fail, s_pass;
+  const UniMemo& m = q.m;
+  const uint64_t sz = m.sz, need = sz > 48 ? sz : 48;
+  const uint32_t t = threadIdx.x, nt = blockDim.x, lane = t & 63u;
+  uint64_t hi = q.nc - 1;
+  for (int round = 0; hi > lo + 1; ++round) {
+    UNI_T(r0);
+    if (t == 0) {
+      s_fail = hi;
+      s_pass = lo;
+    }
+    __syncthreads();
+    const uint64_t w = hi - lo - 1;   // candidates strictly between
+    uint64_t e = 0;
+    if (round == 0) {
+      if (t < 128) {
+        e = lo + 1 + t;
+      } else if (t < 256) {
+        const float a = fmaxf(0.0f, __logf((float)w / 128.0f) * (1.0f / 128.0f));
+        e = lo + (uint64_t)(128.0f * __expf(a * (float)(t - 127)));
+      }
+    } else {
+      e = w <= nt ? lo + 1 + t : lo + 1 + (w * t) / nt;
+    }
+    const uint64_t x = q.y + e * sz;
+    const bool act = e > lo && e < hi && x + need <= p.len;
+    bool pass = false;
+    uint32_t d[12];
+    UNI_T(ra);
+    if (act) pass = uni_probe16(p, m, x, d);
+    const uint64_t fm = __ballot(act && !pass);
+    if (fm && lane == (uint32_t)__builtin_ctzll(fm)) atomicMin(&s_fail, (unsigned long long)e);
+    UNI_T(rb);
+    UNI_ADD(14, ra, rb);
+    __syncthreads();
+    UNI_T(rc);
+    UNI_ADD(15, rb, rc);
+    const uint64_t f = s_fail;
+    if (act && !pass && e == f) {   // the header at the (so far) end: the next run's entry 0
+#pragma unroll
+      for (int i = 0; i < 12; ++i) stash[i] = d[i];
+      stash[12] = (uint32_t)(x & 3u);
+    }
+    if (round == 0 && f == hi) return hi;
+    const uint64_t pm = __ballot(act && pass && e < f);
+    if (pm && lane == 63u - (uint32_t)__builtin_clzll(pm)) atomicMax(&s_pass, (unsigned long long)e);
+    __syncthreads();
+    lo = s_pass;
+    hi = f;
+    __syncthreads();
+    UNI_T(r1);
+    UNI_ADD(10, 0, 1);
+    UNI_ADD(11, r0, r1);
+  }
+  return hi;
+}
+
+// Workgroup 0 of a kMulti launch, run 0's memo in ru: for each run, its end M (uni_search), then the
+// entry at M as the next run's entry 0 when it decodes as a run start (a memo and a slicing; its entry 1
+// is the next search's first probe), up to kUniMaxRuns runs. Then the list is published: the records,
+// each run's F (its M, or "none" when no boundary was found), dyn[6] = the count | kUniFinal.
+__device__ void uni_discover(const Pipe& p, UniRuns& ru) {
+  __shared__ int s_next;
+  __shared__ uint32_t stash[13];
+  __shared__ unsigned long long s_f[kUniMaxRuns];
+  for (;;) {
+    const int r = ru.n - 1;
+    UniRun& q = ru.r[r];
+    UNI_T(b0);
+    const uint64_t M = uni_search(p, q, r == 0 ? 1 : 0, stash);
+    UNI_T(b1);
+    UNI_ADD(2, b0, b1);
+    const bool brk = M < q.nc - 1;   // (uniform)
+    if (threadIdx.x == 0) {
+      s_f[r] = brk ? M : ~0ull;
+      if (brk) q.nc = M;
+      s_next = brk && r + 1 < kUniMaxRuns;
+    }
+    __syncthreads();
+    if (s_next && threadIdx.x < 64) {   // the entry at M from the stash, one byte per lane of wave 0
+      const uint32_t lane = threadIdx.x, i = lane + stash[12];
+      const uint32_t b = i < 48 ? (stash[i >> 2] >> (8 * (i & 3u))) & 0xFFu : 0u;
+      const uint64_t yn = q.y + M * q.m.sz;
+      UniRun& n = ru.r[r + 1];
+      const bool ok = uni_decode_wave<false>(p, yn, b, n);
+      if (lane == 0) {
+        s_next = ok;
+        if (ok) {
+          n.gbase = q.gbase + M;
+          n.nc = (p.len - yn) / n.m.sz + 1;
+          ru.n = r + 2;
+        }
+      }
+    }
+    __syncthreads();
+    UNI_T(b2);
+    UNI_ADD(3, b1, b2);
+    if (!s_next) break;
+  }
+  UNI_T(p0);
+  for (int r = 0; r < ru.n; ++r) {   // the list, then the flag
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&ru.r[r]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(uni_recs(p) + r);
+    for (uint32_t i = threadIdx.x; i < sizeof(UniRun) / 4; i += blockDim.x) dst[i] = src[i];
+  }
+  if (threadIdx.x < (uint32_t)ru.n) *uni_fword(p, threadIdx.x) = s_f[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&p.dyn[6], (uint64_t)ru.n | kUniFinal, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  UNI_T(p1);
+  UNI_ADD(12, p0, p1);
+}
+
+// Every workgroup of a kMulti launch: the run list once workgroup 0 has published it (spinning on
+// dyn[6]; workgroup 0 is dispatched first), then each run's slicing (uni_geometry, wave i for run i;
+// run 0's too unless `have0`).
+__device__ __forceinline__ void uni_take_runs(const Pipe& p, UniRuns& ru, bool have0) {
+  __shared__ int s_n;
+  UNI_T(w0);
+  if (threadIdx.x == 0) {
+    uint64_t w;
+    for (;;) {
+      w = __hip_atomic_load(&p.dyn[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w & kUniFinal) break;
+      __builtin_amdgcn_s_sleep(LDB_UNI_SPIN);   // (every workgroup's thread 0 polls one word)
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_n = (int)(uint32_t)w;
+  }
+  __syncthreads();
+  const int n = s_n;
+  if (blockIdx.x != 0) {   // (workgroup 0: its own list; the others have run 0 but for its nc)
+    for (int r = 1; r < n; ++r) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(uni_recs(p) + r);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&ru.r[r]);
+      for (uint32_t i = threadIdx.x; i < sizeof(UniRun) / 4; i += blockDim.x) dst[i] = src[i];
+    }
+    if (threadIdx.x == 0) ru.r[0].nc = uni_recs(p)[0].nc;
+  }
+  __syncthreads();
+  const int wv = (int)(threadIdx.x >> 6);
+  if (wv < n && (wv > 0 || !have0)) {
+    UniRun& q = ru.r[wv];
+    const UniGeo g = uni_geometry(p.xw, (uint32_t)(q.m.sz - 4));
+    if ((threadIdx.x & 63u) == 0) q.g = g;
+  }
+  if (threadIdx.x == 0) ru.n = n;
+  __syncthreads();
+  UNI_T(w1);
+  UNI_ADD(9, w0, w1);
+}
+
 template <bool kMulti>
 __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns& ru, uint32_t* T,
                                             uint64_t probe_hi, uint64_t& bound) {
@@ -500,8 +789,8 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
   __shared__ int published;
   UniSetup* gsu = reinterpret_cast<UniSetup*>(p.uni);
   uint32_t* gT = reinterpret_cast<uint32_t*>(p.uni + kUniSetupBytes);
-  if (threadIdx.x == 0) {
-    published = __hip_atomic_load(&p.dyn[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == kUniReady;
+  if (threadIdx.x == 0) {   // (kMulti: one launch, nothing published before it)
+    published = !kMulti && __hip_atomic_load(&p.dyn[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == kUniReady;
     if (published) su = *gsu;
   }
   __syncthreads();
@@ -523,37 +812,52 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
   // bytes [0, kUniWin) of the image, zero past len, staged once: entry 0's header and entry 1's (sz <=
   // kUniMaxSize) come from the same round trip (round 2 staged them in two dependent rounds)
   __shared__ uint32_t win[kUniWin / 4];
-  for (uint32_t i = threadIdx.x; i < kUniWin / 4; i += blockDim.x) {
-    const uint64_t a0 = 4ull * i;
-    uint32_t w = 0;
-    if (a0 + 4 <= p.len) {
-      w = *reinterpret_cast<const uint32_t*>(p.img + a0);
-    } else {
-      for (uint32_t k = 0; k < 4; ++k) w |= (a0 + k < p.len ? (uint32_t)p.img[a0 + k] : 0u) << (8 * k);
-    }
-    win[i] = w;
-  }
+  UNI_T(s0);
+  uni_stage_win(p, win, 0);
   __syncthreads();
+  UNI_T(s1);
+  UNI_ADD(0, s0, s1);
   const uint8_t* wb = reinterpret_cast<const uint8_t*>(win);
-  if (threadIdx.x == 0) {
-    su.m = uni_memo([&](int i) -> uint32_t { return i < (int)kUniWin ? wb[i] : 0u; }, p.len, p.io);
-    su.g = su.m.ok ? uni_geometry(p.xw, (uint32_t)(su.m.sz - 4)) : UniGeo{};
-    if (su.g.ok) {
-      const uint8_t* h = wb + su.m.sz;   // sz + 40 < kUniWin
-      auto word = [&](int i) -> uint32_t {
-        return (uint32_t)h[4 * i] | ((uint32_t)h[4 * i + 1] << 8) | ((uint32_t)h[4 * i + 2] << 16) |
-               ((uint32_t)h[4 * i + 3] << 24);
-      };
-      if (!uni_header_ok(su.m, word, su.m.sz, p.len, p.io)) su.g.ok = 0;
-    }
-    if (su.g.ok) {
-      if (blockIdx.x == 0) p.dyn[1] = su.m.sz;
-      run0();
-    } else if (blockIdx.x == 0) {
-      p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
+  if (threadIdx.x < 64) {   // entry 0 decoded by wave 0 (readlane), entry 1's header from the window
+    UniRun& q = ru.r[0];
+    // (workgroup 0 of a kMulti launch leaves the slicing for later: it finds the runs first)
+    bool ok = kMulti && blockIdx.x == 0 ? uni_decode_wave<false>(p, 0, wb[threadIdx.x], q)
+                                        : uni_decode_wave<true>(p, 0, wb[threadIdx.x], q);
+    if (threadIdx.x == 0) {
+      if (ok) {
+        const uint8_t* h = wb + q.m.sz;   // sz + 40 < kUniWin
+        auto word = [&](int i) -> uint32_t {
+          return (uint32_t)h[4 * i] | ((uint32_t)h[4 * i + 1] << 8) | ((uint32_t)h[4 * i + 2] << 16) |
+                 ((uint32_t)h[4 * i + 3] << 24);
+        };
+        ok = uni_header_ok(q.m, word, q.m.sz, p.len, p.io);
+      }
+      su.m = q.m;
+      su.g = q.g;
+      su.g.ok = ok;
+      if (ok) {
+        if (blockIdx.x == 0) p.dyn[1] = su.m.sz;
+        run0();
+      } else if (blockIdx.x == 0) {
+        p.dyn[0] = 0;   // no run: the pipeline starts at offset 0
+      }
     }
   }
   __syncthreads();
+  if (kMulti) {
+    if (!su.g.ok) return false;
+    if (blockIdx.x != 0) {
+      uni_build_comb(p, su.g, T, nullptr);   // while workgroup 0 finds the runs
+    } else if (!LDB_UNI_NOPROBE) {
+      uni_discover(p, ru);
+    } else if (threadIdx.x == 0) {
+      uni_recs(p)[0] = ru.r[0];
+      __hip_atomic_store(&p.dyn[6], 1ull | kUniFinal, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    UNI_T(s2);
+    UNI_ADD(1, s1, s2);
+    return true;
+  }
   if (su.g.ok) uni_build_comb(p, su.g, T, blockIdx.x == 0 ? gT : nullptr);
   if (blockIdx.x == 0) {   // publish run 0 (a chunked scan's later launches): the tables, the setup, the flag
     if (threadIdx.x == 0) *gsu = su;
@@ -561,60 +865,15 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&p.dyn[2], kUniReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
+  UNI_T(s2);
+  UNI_ADD(1, s1, s2);
   if (!su.g.ok) return false;
   if (LDB_UNI_NOPROBE) return true;
-  __shared__ int s_next;
-  for (;;) {
-    UniRun& r = ru.r[ru.n - 1];
-    const uint64_t M = uni_boundary(p, r.m, r.y, r.nc, probe_hi);
-    if (M >= r.nc - 1) break;   // no boundary inside: the run reaches the end of the file
-    const uint64_t yn = r.y + M * r.m.sz, ya = yn & ~3ull;
-    const bool more = kMulti && ru.n < kUniMaxRuns;
-    if (more) {   // the next run's entries 0 and 1, staged as run 0's were (one round trip, decoded from LDS)
-      __syncthreads();
-      for (uint32_t i = threadIdx.x; i < kUniWin / 4; i += blockDim.x) {
-        const uint64_t a0 = ya + 4ull * i;
-        uint32_t w = 0;
-        if (a0 + 4 <= p.len) {
-          w = *reinterpret_cast<const uint32_t*>(p.img + a0);
-        } else {
-          for (uint32_t k = 0; k < 4; ++k) w |= (a0 + k < p.len ? (uint32_t)p.img[a0 + k] : 0u) << (8 * k);
-        }
-        win[i] = w;
-      }
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      s_next = 0;
-      if (more) {
-        UniRun& q = ru.r[ru.n];
-        q.y = yn;
-        const uint32_t o = (uint32_t)(yn - ya);   // 0..3
-        q.m = uni_memo([&](int i) -> uint32_t { return wb[o + i]; }, p.len, p.io, q.y);
-        q.g = q.m.ok ? uni_geometry(p.xw, (uint32_t)(q.m.sz - 4)) : UniGeo{};
-        if (q.g.ok) {
-          const uint64_t x1 = q.y + q.m.sz;
-          const uint8_t* h = wb + o + q.m.sz;   // o + sz + 40 < kUniWin
-          auto word = [&](int i) -> uint32_t {
-            return (uint32_t)h[4 * i] | ((uint32_t)h[4 * i + 1] << 8) | ((uint32_t)h[4 * i + 2] << 16) |
-                   ((uint32_t)h[4 * i + 3] << 24);
-          };
-          if (uni_header_ok(q.m, word, x1, p.len, p.io)) {
-            q.gbase = r.gbase + M;
-            q.nc = (p.len - q.y) / q.m.sz + 1;
-            r.nc = M;   // entry M of run r is the next run's entry 0
-            ru.n += 1;
-            s_next = 1;
-          }
-        }
-      }
-      if (!s_next && blockIdx.x == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(r.gbase + M));
-    }
-    __syncthreads();
-    if (!s_next) {
-      bound = r.gbase + M;   // a failure of the last run: K <= bound
-      break;
-    }
+  const UniRun& r = ru.r[0];
+  const uint64_t M = uni_boundary(p, r.m, r.y, r.nc, probe_hi, 64u);   // every workgroup probes: few probes
+  if (M < r.nc - 1) {   // a failure of the run: K <= bound
+    bound = M;
+    if (threadIdx.x == 0 && blockIdx.x == 0) atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)M);
   }
   __syncthreads();
   return true;
@@ -643,9 +902,11 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 // kAl: every window and header starts on a dword (sz and t multiples of 4, as for LazyDB's 332-B
 // config 2/4/5 entries): no funnel shifts (22 v_alignbyte per batch at S = 11).
 // One run (ru): its entry e at ru.y + e sz is chain entry ru.gbase + e; candidates e < ru.nc.
-template <int S, bool kChunk, bool kHash, bool kFill, bool kAl>
-__device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, const uint8_t* lp2, const uint32_t* T,
-                                          int lane, int wave, uint64_t a_lo, uint64_t a_hi, uint64_t bound) {
+// NW: the workgroup's verifying waves (waves 0 .. NW-1; kUniWaves, or one fewer beside a fill wave).
+template <int S, bool kChunk, bool kHash, bool kFill, bool kAl, int NW>
+__device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint64_t* F, const uint8_t* lp2,
+                                          const uint32_t* T, int lane, int wave, uint64_t a_lo, uint64_t a_hi,
+                                          uint64_t bound) {
   if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
     a_lo = 0;
     a_hi = p.len;
@@ -684,15 +945,16 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, const
   const uint64_t y0 = su.y, gb = su.gbase;   // (kChunk: one run, y0 = gb = 0)
   // K as last seen: the load issued in one batch is tested at the top of the next, so its latency hides
   // behind the batch (a batch past K only costs its own time: the run's tuples stop at K anyway)
-  v2u32 kv = {(uint32_t)bound, (uint32_t)(bound >> 32)};   // K as loaded during the previous batch (vector value:
+  // (F: the run's first-failure word, candidate indices within the run; K itself for a one-run scan)
+  v2u32 kv = {(uint32_t)bound, (uint32_t)(bound >> 32)};   // F as loaded during the previous batch (vector value:
                                                            // read at the next top); first the probes' bound
-  const __amdgpu_buffer_rsrc_t krs = rsrc_of(p.dyn, 8);
-  for (uint64_t b = b_first + (uint64_t)blockIdx.x * kUniWaves + wave; b < nbatch; b += (uint64_t)gridDim.x * kUniWaves) {
+  const __amdgpu_buffer_rsrc_t krs = rsrc_of(F, 8);
+  for (uint64_t b = b_first + (uint64_t)blockIdx.x * NW + wave; b < nbatch; b += (uint64_t)gridDim.x * NW) {
     if (kChunk && b * Esz > (all_hi ? p.len : a_hi)) break;   // wave-uniform: no candidate of this launch from here on
     // uniform by construction (one address), but a load's result is divergent to the compiler: the
     // loop exit on it would make b, and every descriptor built from b, divergent (waterfall loops)
     const uint64_t kseen = ((uint64_t)__builtin_amdgcn_readfirstlane(kv[1]) << 32) | __builtin_amdgcn_readfirstlane(kv[0]);
-    if (gb + b * E >= kseen) break;
+    if (b * E >= kseen) break;
 
     // Opaque per-batch copies: the uniform step / level conditions and the lane masks derived from
     // them are evaluated inside the batch, not hoisted out of the loop as a bank of held SGPR masks.
@@ -840,7 +1102,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, const
 #endif
     const uint64_t bad = __ballot((last && mine && !ok) ? 1 : 0);
     if (bad && lane == 0)
-      atomicMin((unsigned long long*)&p.dyn[0], (unsigned long long)(gb + b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
+      atomicMin((unsigned long long*)F, (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
     if (ok && gb + e < p.cap && (!fill || kHash)) {
       uint32_t z = 0;
       asm volatile("" : "+v"(z));
@@ -879,40 +1141,51 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, const
   }
 }
 
-// kPost: the run's INDEX tuples, written by each workgroup once its waves' verify loops are done, as a
-// dense sweep of its own slice of the tuple array (so the stores of early workgroups overlap the loads
-// of the others, and no fill launch follows). A tuple's bytes depend only on its index (uni_pos of
-// e sz and the memo's sizes), not on who verified the entry, so the slice covers every e below K as
-// visible now and below cap: every e below the final K is written, and one at or past the final K (K
-// may still drop) lies beyond n_entries, where the region pipeline writes its own tuples from K on.
+// The runs' INDEX tuples, written by each workgroup once its waves' verify loops are done, as a dense
+// sweep of its own slice of the chain's tuples (so the stores of early workgroups overlap the loads of
+// the others, and no fill launch follows). A tuple's bytes depend only on its index (uni_pos of its x and
+// the run's memo), not on who verified the entry, so the slice covers every entry of run r below F_r
+// as visible now (and below cap): every one below the final K is written, and one at or past the final
+// K (F may still drop) lies beyond n_entries, where the region pipeline writes its own tuples from K on.
+// F_r <= M_r (uni_discover), so no run writes into the next run's tuples. The slices come from the runs'
+// nc (the same in every workgroup; F as seen here is not).
 // (Round 4: per-wave stores of each wave's own batches, 4 scattered 256-B pieces per instruction, cost
-// 61 us at config 4 against 33 for the separate dense sweep.)
+// 61 us at config 4 against 33 for the separate dense sweep; a fill per run, after each run's verify
+// loop, 20 us at config 1 against 8 for this one sweep -- a barrier per run. A fill wave writing the
+// slice while the other 15 verify -- K re-read every 4096 tuples -- was measured and rejected: config 4
+// k_uniform 0.897 ms against 0.84, 15 verifying waves per CU lose more than the overlap gains.)
 __device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniRuns& ru) {
   __syncthreads();
   const UniRun& rl = ru.r[ru.n - 1];
-  const uint64_t ntot = rl.gbase + rl.nc;   // chain entries over every run
-  const uint64_t K = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t n = K < ntot ? K : ntot;
-  n = n < p.cap ? n : p.cap;
-  const uint64_t per = (ntot + gridDim.x - 1) / gridDim.x;
-  const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  const uint64_t ntot = rl.gbase + rl.nc;   // chain entries over every run's candidates
+  const uint64_t per = ((ntot + gridDim.x - 1) / gridDim.x + 63) & ~63ull;   // whole KiB of tuples each
+  const uint64_t lo = (uint64_t)blockIdx.x * per;
+  uint64_t hi = lo + per < ntot ? lo + per : ntot;
+  hi = hi < p.cap ? hi : p.cap;
   ldb_index_tuple* out = reinterpret_cast<ldb_index_tuple*>(p.out);
-  for (int r = 0; r < ru.n; ++r) {   // this workgroup's slice, run by run
+  for (int r = 0; r < ru.n; ++r) {
     const UniRun& q = ru.r[r];
-    const uint64_t a = lo > q.gbase ? lo : q.gbase, z = q.gbase + q.nc < hi ? q.gbase + q.nc : hi;
-    const uint64_t sz = q.m.sz, ya = q.y - q.gbase * sz;   // x of chain entry g in run r: ya + g sz (mod 2^64)
+    if (q.gbase >= hi || q.gbase + q.nc <= lo) continue;
+    const uint64_t f = uni_fload(uni_fword(p, r));
+    const uint64_t a = lo > q.gbase ? lo : q.gbase;
+    uint64_t z = q.gbase + (q.nc < f ? q.nc : f);
+    z = z < hi ? z : hi;
+    const uint64_t sz = q.m.sz, ya = q.y - q.gbase * sz;   // x of chain entry g: ya + g sz (mod 2^64)
     for (uint64_t g = a + threadIdx.x; g < z; g += blockDim.x) store_tuple(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
   }
 }
 
 // The device path's run prefix, finished (the last k_uniform workgroup to be done, after every
-// workgroup's K update): x0 = the position of chain entry K over the runs (dyn[5], chain_x0). When the
-// chain stops right there -- the header window there is unreadable (io.EOF), or it decodes as the zero
-// sentinel (ErrLogEndOfFile), a key/value read past the bound (io.EOF) or a malformed header
-// (log_file.go:116-139) -- the scan is complete: this writes the ldb_scan_result and sets dyn[3] =
-// kUniDone, and the region pipeline's kernels leave at once. A file the runs cover to its terminal
-// (BASELINE configs 1, 2, 4, 5) then pays no region kernel work.
+// workgroup's F updates). kMulti: K = gbase + F of the first run whose F lies below its end M (a failure
+// inside it; M = the next run's gbase - this one's), or of the last run; x0 = the position of chain entry
+// K (dyn[0] = K, dyn[5] = x0, chain_x0). When the chain stops right there -- the header window there is
+// unreadable (io.EOF), or it decodes as the zero sentinel (ErrLogEndOfFile), a key/value read past the
+// bound (io.EOF) or a malformed header (log_file.go:116-139) -- the scan is complete: this writes the
+// ldb_scan_result and sets dyn[3] = kUniDone, and the region pipeline's kernels leave at once. A file the
+// runs cover to its terminal (BASELINE configs 1, 2, 4, 5) then pays no region kernel work. Wave 0 of the
+// last workgroup: the entry at x0 is decoded through readlane, one byte per lane.
 constexpr uint64_t kUniDone = 0xD0E5CA11D0E5CA11ull;
+template <bool kMulti>
 __device__ __forceinline__ void uni_finish(const Pipe& p, const UniRuns& ru) {
   __shared__ int s_last;
   __syncthreads();
@@ -921,26 +1194,43 @@ __device__ __forceinline__ void uni_finish(const Pipe& p, const UniRuns& ru) {
     s_last = atomicAdd((unsigned long long*)&p.dyn[4], 1ull) == (unsigned long long)gridDim.x - 1;
   }
   __syncthreads();
-  if (!s_last || threadIdx.x != 0) return;
+  if (!s_last || threadIdx.x >= 64) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  p.dyn[4] = 0;
-  const uint64_t K = __hip_atomic_load(&p.dyn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t lane = threadIdx.x;
+  uint64_t K = ~0ull, x0 = 0;
+  if (kMulti) {
+    for (int r = 0; r < ru.n; ++r) {
+      const uint64_t f = uni_fload(uni_fword(p, r));
+      const bool last = r == ru.n - 1;
+      if (last || f < ru.r[r + 1].gbase - ru.r[r].gbase) {
+        if (f == ~0ull) break;
+        K = ru.r[r].gbase + f;
+        x0 = ru.r[r].y + f * ru.r[r].m.sz;
+        break;
+      }
+    }
+  } else {
+    K = uni_fload(p.dyn);
+    if (K != ~0ull) x0 = K * ru.r[0].m.sz;
+  }
+  if (lane == 0) {
+    p.dyn[4] = 0;
+    if (K != ~0ull) {
+      p.dyn[0] = K;
+      p.dyn[5] = x0;
+    }
+  }
   if (K == ~0ull) return;   // (unreachable: the candidate at or past len always fails)
-  int r = ru.n - 1;
-  while (r > 0 && ru.r[r].gbase > K) --r;
-  const uint64_t x0 = ru.r[r].y + (K - ru.r[r].gbase) * ru.r[r].m.sz;
-  p.dyn[5] = x0;
   int32_t st;
   if (read_eof(p.len, p.io, (int64_t)x0, kMaxHeader)) {
     st = LDB_EOF_WINDOW;
   } else {
-    struct G {
-      const uint8_t* q;
-      __device__ uint32_t operator()(int i) const { return q[i]; }
-    };
-    st = classify_entry(G{p.img + x0}, p.len, p.io, x0).status;
+    const uint32_t b = x0 + lane < p.len ? (uint32_t)p.img[x0 + lane] : 0u;
+    auto fetch = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)b, i); };
+    st = classify_entry(fetch, p.len, p.io, x0).status;
   }
   if (st != LDB_EOF_WINDOW && st != LDB_EOF_SENTINEL && st != LDB_EOF_KV && st != LDB_ERR_MALFORMED) return;
+  if (lane != 0) return;
   ldb_scan_result res;
   res.status = K > p.cap ? LDB_ERR_CAPACITY : st;
   res.fid = p.fid;
@@ -957,21 +1247,18 @@ __device__ __forceinline__ void uni_finish(const Pipe& p, const UniRuns& ru) {
 // the region pipeline's kernels: nothing to do once the run prefix finished the scan
 __device__ __forceinline__ bool scan_done(const Pipe& p) { return p.dyn[3] == kUniDone; }
 
-// kChunk: a_lo, a_hi: image bytes [0, a_hi) are in place; candidates not already taken by a launch
-// with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
-// LDS: the 64 KiB LP2 block, the combine tables and the setup (~90 KiB): one workgroup of 16 waves per
-// CU, 4 waves per SIMD, up to 128 VGPRs.
 // One run's verification: uni_waves instantiated for its slicing S and alignment (a switch over S on
 // a wave-uniform value).
-template <bool kChunk, bool kHash, bool kFill>
-__device__ __forceinline__ void uni_run(const Pipe& p, const UniRun& q, const uint8_t* lp2, const uint32_t* comb,
-                                        int lane, int wave, uint64_t a_lo, uint64_t a_hi, uint64_t bound) {
+template <bool kChunk, bool kHash, bool kFill, int NW>
+__device__ __forceinline__ void uni_run(const Pipe& p, const UniRun& q, uint64_t* F, const uint8_t* lp2,
+                                        const uint32_t* comb, int lane, int wave, uint64_t a_lo, uint64_t a_hi,
+                                        uint64_t bound) {
   const bool al = (q.m.sz & 3u) == 0 && (q.g.t & 3u) == 0 && (q.y & 3u) == 0;   // every window and header dword-aligned
   switch (q.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
-#define LDB_UNI_CASE(n)                                                                             \
-  case n:                                                                                           \
-    if (al) uni_waves<n, kChunk, kHash, kFill, true>(p, q, lp2, comb, lane, wave, a_lo, a_hi, bound);  \
-    else uni_waves<n, kChunk, kHash, kFill, false>(p, q, lp2, comb, lane, wave, a_lo, a_hi, bound);    \
+#define LDB_UNI_CASE(n)                                                                                 \
+  case n:                                                                                               \
+    if (al) uni_waves<n, kChunk, kHash, kFill, true, NW>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, bound);  \
+    else uni_waves<n, kChunk, kHash, kFill, false, NW>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, bound);    \
     break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
@@ -1014,16 +1301,39 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
 #endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int r = 0; r < ru.n; ++r) {
-    const UniRun& q = ru.r[r];
-    if (r > 0 && (q.g.G != ru.r[r - 1].g.G || q.g.P != ru.r[r - 1].g.P)) {
-      __syncthreads();   // every wave is done with the previous run's combine tables
-      uni_build_comb(p, q.g, comb, nullptr);
+  if (!kMulti) {
+    UNI_T(v0);
+    uni_run<kChunk, kHash, !kHash, kUniWaves>(p, ru.r[0], p.dyn, lp2, comb, lane, wave, a_lo, a_hi, bound);
+    UNI_T(v1);
+    UNI_ADD(6, v0, v1);
+    if (!kChunk || a_hi >= p.len) uni_finish<false>(p, ru);
+  } else {
+    // the run list (uni_discover), each run verified up to its F, then the INDEX tuples written
+    uni_take_runs(p, ru, blockIdx.x != 0);
+    if (blockIdx.x == 0) uni_build_comb(p, ru.r[0].g, comb, nullptr);
+    for (int r = 0; r < ru.n; ++r) {
+      const UniRun& q = ru.r[r];
+      uint64_t* F = uni_fword(p, r);
+      if (r > 0 && (q.g.G != ru.r[r - 1].g.G || q.g.P != ru.r[r - 1].g.P)) {
+        UNI_T(c0);
+        __syncthreads();   // every wave is done with the old tables
+        uni_build_comb(p, q.g, comb, nullptr);
+        UNI_T(c1);
+        UNI_ADD(5, c0, c1);
+      }
+      UNI_T(v0);
+      uni_run<kChunk, kHash, !kHash, kUniWaves>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, ~0ull);
+      UNI_T(v1);
+      UNI_ADD(6, v0, v1);
     }
-    uni_run<kChunk, kHash, !kHash>(p, q, lp2, comb, lane, wave, a_lo, a_hi, bound);
+    UNI_T(f0);
+    if (p.kind == LDB_TUPLE_INDEX) uni_post_fill(p, ru);
+    UNI_T(f1);
+    UNI_ADD(7, f0, f1);
+    uni_finish<true>(p, ru);
+    UNI_T(f2);
+    UNI_ADD(8, f1, f2);
   }
-  if (kMulti && p.kind == LDB_TUPLE_INDEX) uni_post_fill(p, ru);
-  if (!kChunk || a_hi >= p.len) uni_finish(p, ru);
 }
 static_assert(kUniSteps == 12, "k_uniform's switch covers S = 1..12");
 
@@ -1107,7 +1417,7 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uni_run<false, false, true>(p, ru.r[0], lp2, comb, lane, wave, 0, p.len, bound);
+  uni_run<false, false, true, kUniWaves>(p, ru.r[0], p.dyn, lp2, comb, lane, wave, 0, p.len, bound);
 }
 // ---------------------------------------------------------------- k_scan_main
 template <bool kB>
@@ -1892,7 +2202,7 @@ WsLayout layout(uint64_t len) {
   L.o_ctr = take(32);
   L.o_tpos = take(16);
   L.o_dyn = take(64);   // run prefix: K, entry size, setup-published flag, done flag, done counter (k_uniform)
-  L.o_uni = take(kUniSetupBytes + 4 * kUniTabWords);   // run prefix: the published setup
+  L.o_uni = take(kUniBlockBytes);   // run prefix: the published setup, the run list, the runs' F words
   L.o_blk = take(8 * L.nblk);
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1) + 64);   // fail flags + walker claims (ldb_pipeline.h fail_flags)
@@ -1998,11 +2308,11 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
 
 // the control words every region pipeline starts from (enqueue_scan)
 // dyn: [0] K (dyn_val: ~0 = no failure seen, 0 = no run), [1] entry size, [2] setup flag, [3] done
-// flag (uni_finish), [4] k_uniform's done counter, [5] x0 (uni_finish)
+// flag (uni_finish), [4] k_uniform's done counter, [5] x0 (uni_finish), [6] runs published (uni_discover)
 __global__ __launch_bounds__(64) void k_init(uint32_t* ctr, uint64_t* dyn, uint64_t dyn_val) {
   if (threadIdx.x < 8) ctr[threadIdx.x] = 0u;
   if (threadIdx.x < 3) dyn[threadIdx.x] = dyn_val;
-  if (threadIdx.x == 3 || threadIdx.x == 4) dyn[threadIdx.x] = 0;
+  if (threadIdx.x == 3 || threadIdx.x == 4 || threadIdx.x == 6 || threadIdx.x == 7) dyn[threadIdx.x] = 0;
   if (threadIdx.x == 5) dyn[5] = ~0ull;   // x0 not finished: K sz (no run: 0)
 }
 
@@ -2103,7 +2413,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     } else {
-      launch(0, len);   // its workgroups also write the run's INDEX tuples (uni_post_fill)
+      launch(0, len);   // its workgroups also write the runs' INDEX tuples (uni_post_fill)
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
@@ -2151,7 +2461,7 @@ __global__ __launch_bounds__(64) void k_batch_init(const Pipe* __restrict__ pb) 
   const Pipe& p = pb[blockIdx.x];
   if (threadIdx.x < 8) p.ctr[threadIdx.x] = 0u;
   if (threadIdx.x < 4 || threadIdx.x == 5) p.dyn[threadIdx.x] = ~0ull;   // [3]: not done; [5]: x0 = K sz
-  if (threadIdx.x == 4) p.dyn[4] = 0;
+  if (threadIdx.x == 4 || threadIdx.x == 6 || threadIdx.x == 7) p.dyn[threadIdx.x] = 0;
 }
 
 int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s) {
@@ -2567,6 +2877,14 @@ int ldb_debug_stamps(uint64_t* out, int reset) {
   if (reset) {
     uint64_t z[kStampSlots] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 8 * kStampSlots) != hipSuccess) return LDB_ERR_HIP;
+  }
+  return LDB_OK;
+}
+int ldb_debug_ustamps(uint64_t* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ustamps), 8 * kUniStampSlots) != hipSuccess) return LDB_ERR_HIP;
+  if (reset) {
+    uint64_t z[kUniStampSlots] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ustamps), z, 8 * kUniStampSlots) != hipSuccess) return LDB_ERR_HIP;
   }
   return LDB_OK;
 }
