@@ -200,6 +200,13 @@ __device__ __forceinline__ void store_tuple(ldb_index_tuple* dst, uint64_t pos, 
   t.w = v;
   *reinterpret_cast<uint4*>(dst) = t;
 }
+// the same as a streaming store (not kept in L2: the INDEX sweep's tuples are read by the host or the
+// next kernel, and a release fence after the sweep would otherwise write them back from L2)
+__device__ __forceinline__ void store_tuple_nt(ldb_index_tuple* dst, uint64_t pos, uint32_t k, uint32_t v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 t = {(uint32_t)pos, (uint32_t)(pos >> 32), k, v};
+  __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(dst));
+}
 
 // Region summary record (48 B) from its LDS copy: lanes 0-11 move one dword each -- one LDS read
 // and one coalesced global_store_dword (global, in-order on vmcnt: k_scan_main counts it).
@@ -227,10 +234,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint
   return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
+#ifndef LDB_ST_NT
+#define LDB_ST_NT 0   // A/B: the region pipeline's tuple stores streaming (nt): measured and rejected, config 3 k_scan_main 2.77 vs 2.75 ms, w 1.246 vs 1.245
+#endif
+constexpr int kNt = 2;   // buffer cache-policy bit: nt (streaming)
+template <int kAux = 0>
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t x, uint32_t y, uint32_t z,
                                         uint32_t w) {
   const v4u32 d = {x, y, z, w};
-  __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, 0, kAux);
 }
 // A 48-B region summary from wave-uniform values: lanes 0-2 store 16 B each (one instruction).
 // drop: the instruction still issues (k_scan_main's counted vmcnt waits) but writes nothing
@@ -630,18 +642,21 @@ __device__ __forceinline__ bool uni_probe16(const Pipe& p, const UniMemo& m, uin
 // header bytes in stash[0..12) (stash[12] = x & 3): the next run's entry 0 without another load.
 // Returns nc - 1 when round 0 finds no mismatch.
 __device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint32_t* stash) {
-  __shared__ unsigned long long s_fail, s_pass;
+  // a round's smallest failing and largest passing probe: two slots, alternating by round, so the next
+  // round's pair is set up before this round's last barrier (two barriers a round)
+  __shared__ unsigned long long s_fail[2], s_pass[2];
   const UniMemo& m = q.m;
   const uint64_t sz = m.sz, need = sz > 48 ? sz : 48;
   const uint32_t t = threadIdx.x, nt = blockDim.x, lane = t & 63u;
   uint64_t hi = q.nc - 1;
+  if (t == 0) {
+    s_fail[0] = hi;
+    s_pass[0] = 0;
+  }
+  __syncthreads();
   for (int round = 0; hi > lo + 1; ++round) {
     UNI_T(r0);
-    if (t == 0) {
-      s_fail = hi;
-      s_pass = lo;
-    }
-    __syncthreads();
+    const int cur = round & 1;
     const uint64_t w = hi - lo - 1;   // candidates strictly between
     uint64_t e = 0;
     if (round == 0) {
@@ -661,13 +676,13 @@ __device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint
     UNI_T(ra);
     if (act) pass = uni_probe16(p, m, x, d);
     const uint64_t fm = __ballot(act && !pass);
-    if (fm && lane == (uint32_t)__builtin_ctzll(fm)) atomicMin(&s_fail, (unsigned long long)e);
+    if (fm && lane == (uint32_t)__builtin_ctzll(fm)) atomicMin(&s_fail[cur], (unsigned long long)e);
     UNI_T(rb);
     UNI_ADD(14, ra, rb);
     __syncthreads();
     UNI_T(rc);
     UNI_ADD(15, rb, rc);
-    const uint64_t f = s_fail;
+    const uint64_t f = s_fail[cur];
     if (act && !pass && e == f) {   // the header at the (so far) end: the next run's entry 0
 #pragma unroll
       for (int i = 0; i < 12; ++i) stash[i] = d[i];
@@ -675,11 +690,15 @@ __device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint
     }
     if (round == 0 && f == hi) return hi;
     const uint64_t pm = __ballot(act && pass && e < f);
-    if (pm && lane == 63u - (uint32_t)__builtin_clzll(pm)) atomicMax(&s_pass, (unsigned long long)e);
+    if (pm && lane == 63u - (uint32_t)__builtin_clzll(pm)) atomicMax(&s_pass[cur], (unsigned long long)e);
+    if (t == 0) {   // the next round's pair (last read before this round's first barrier)
+      s_fail[cur ^ 1] = f;
+      s_pass[cur ^ 1] = 0;
+    }
     __syncthreads();
-    lo = s_pass;
+    const uint64_t sp = s_pass[cur];   // 0, or a passing probe > lo
+    lo = sp > lo ? sp : lo;
     hi = f;
-    __syncthreads();
     UNI_T(r1);
     UNI_ADD(10, 0, 1);
     UNI_ADD(11, r0, r1);
@@ -1151,9 +1170,14 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
 // nc (the same in every workgroup; F as seen here is not).
 // (Round 4: per-wave stores of each wave's own batches, 4 scattered 256-B pieces per instruction, cost
 // 61 us at config 4 against 33 for the separate dense sweep; a fill per run, after each run's verify
-// loop, 20 us at config 1 against 8 for this one sweep -- a barrier per run. A fill wave writing the
+// loop, 20 us at config 1 against 8 for this one sweep -- a barrier per run. Streaming stores (nt):
+// config 4 k_uniform 0.808 -> 0.768 ms on one box -- with plain stores the tuples sat dirty in L2, and
+// uni_finish's agent-scope release wrote them back before the last workgroup could go on. A fill wave writing the
 // slice while the other 15 verify -- K re-read every 4096 tuples -- was measured and rejected: config 4
 // k_uniform 0.897 ms against 0.84, 15 verifying waves per CU lose more than the overlap gains.)
+#ifndef LDB_UNI_NTFILL
+#define LDB_UNI_NTFILL 1   // the sweep's tuples as streaming stores (0: plain stores, A/B)
+#endif
 __device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniRuns& ru) {
   __syncthreads();
   const UniRun& rl = ru.r[ru.n - 1];
@@ -1171,7 +1195,10 @@ __device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniRuns& ru) 
     uint64_t z = q.gbase + (q.nc < f ? q.nc : f);
     z = z < hi ? z : hi;
     const uint64_t sz = q.m.sz, ya = q.y - q.gbase * sz;   // x of chain entry g: ya + g sz (mod 2^64)
-    for (uint64_t g = a + threadIdx.x; g < z; g += blockDim.x) store_tuple(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
+    for (uint64_t g = a + threadIdx.x; g < z; g += blockDim.x) {
+      if (LDB_UNI_NTFILL) store_tuple_nt(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
+      else store_tuple(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
+    }
   }
 }
 
@@ -1284,13 +1311,15 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   uint64_t t0_, t1_, t2_;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_) :: "memory");
 #endif
-  lp2_build(lp2, p.gtab);
+  // (workgroup 0 of a kMulti launch finds the runs first: its LP2 block afterwards, off that chain)
+  if (!kMulti || blockIdx.x != 0) lp2_build(lp2, p.gtab);
 #ifdef LDB_STAMPS
   __syncthreads();
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_) :: "memory");
 #endif
   uint64_t bound;
   if (!uni_prepare<kMulti>(p, su, ru, comb, kChunk ? a_hi : p.len, bound)) return;   // (its __syncthreads also publish the LP2 block)
+  if (kMulti && blockIdx.x == 0) lp2_build(lp2, p.gtab);   // (published by uni_take_runs' barriers)
   __syncthreads();
 #ifdef LDB_STAMPS
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2_) :: "memory");
@@ -1554,7 +1583,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     const bool fast = !skip && region_chained(
         wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },
         [&](bool valid, uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
-          store16(sc_rs, valid && !dry ? slot_ * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
+          store16<LDB_ST_NT ? kNt : 0>(sc_rs, valid && !dry ? slot_ * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
         },
         [&] {   // the buffer's last read is behind us: stage the run's region i + kNB into it
           const uint64_t nx = i + kNB;
@@ -1592,7 +1621,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
       region_process(
           wp, v, wl->sh, enter, &wl->rs, [&](int) -> LanePriv& { return q; },
           [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
-            store16(sc_rs, dry ? kDrop : slot_ * 16u, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
+            store16<LDB_ST_NT ? kNt : 0>(sc_rs, dry ? kDrop : slot_ * 16u, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
           },
           [] {});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2065,6 +2094,7 @@ __device__ __forceinline__ void compact_body(const Pipe& p) {
     if (dst >= p.cap) break;
     const ldb_index_tuple t = p.scratch[(r0 + lo) * (uint64_t)kRegionCap + (j - s_off[lo])];
     if (p.kind == LDB_TUPLE_ENTRY) decode_entry_global(p, t.pos & 0xFFFFFFFFFFull, reinterpret_cast<ldb_entry*>(p.out) + dst);
+    else if (LDB_ST_NT) store_tuple_nt(reinterpret_cast<ldb_index_tuple*>(p.out) + dst, t.pos, t.k_size, t.v_size);
     else reinterpret_cast<ldb_index_tuple*>(p.out)[dst] = t;
   }
   __syncthreads();   // s_off / s_wsum / s_part are reused by the next block
