@@ -144,6 +144,9 @@ struct UniMemo {
 constexpr int kUniSteps = 12;                            // 8-byte steps per lane at most
 constexpr int kUniLevels = 6;                            // combine levels (G <= 64)
 constexpr uint64_t kUniMaxSize = 4 + 64ull * 8 * kUniSteps;   // larger entries never form a run
+// the smallest entry a run may have: a 10-byte header (crc, stat, five one-byte varints) and no key or
+// value (round 3: 16, so logs of 11-B entries -- adversarial "tiny" -- went through the region pipeline)
+constexpr uint64_t kUniMinSize = 10;
 static_assert(kUniMaxSize - 4 < 2ull * kW && 8ull * kUniSteps << (kUniLevels - 1) <= (uint64_t)kW,
               "uni_geometry reads its shifts from the x^(8n) table");
 
@@ -180,7 +183,7 @@ LDB_HD UniMemo uni_memo(Fetch fetch, uint64_t len, int io, uint64_t off = 0) {
   m.ok = 0;
   const EntryInfo e = classify_entry(fetch, len, io, off);
   if (e.status != kCont || !e.h.canonical || e.h.size < 10 || e.h.size > kMaxHeader) return m;
-  if (e.size > kUniMaxSize || e.size < 16) return m;
+  if (e.size > kUniMaxSize || e.size < kUniMinSize) return m;
   m.hs = (uint32_t)e.h.size;
   m.enc = (uint32_t)e.h.enc_size;
   m.stat = e.h.stat;

@@ -722,6 +722,11 @@ __device__ void uni_discover(const Pipe& p, UniRuns& ru) {
     UNI_T(b1);
     UNI_ADD(2, b0, b1);
     const bool brk = M < q.nc - 1;   // (uniform)
+    if (r > 0 && M < 2) {   // a later "run" of one entry (entry 1 differs): no run; the chain goes on from
+      if (threadIdx.x == 0) ru.n = r;   // its entry 0 in the region pipeline (K = its gbase)
+      __syncthreads();
+      break;
+    }
     if (threadIdx.x == 0) {
       s_f[r] = brk ? M : ~0ull;
       if (brk) q.nc = M;
@@ -1495,6 +1500,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
   const uint64_t r00 = rb - warm, total = count + warm;
   uint32_t n_fast = 0;
   uint32_t declines = 0;        // consecutive lean declines (give-up mode, below)
+  uint32_t backoff = 0;         // give-up windows in a row that ended in another decline
   // LDS-DMA ring of kNB buffers: region i+kNB is staged into region i's buffer as soon as region i
   // has read it for the last time (buffer_free), so the DMA overlaps the summary, its stores and
   // the next region's wait.
@@ -1577,9 +1583,13 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     if (i == warm && warm && st.on && st.x >= v.R0 + (uint64_t)kW) chain_reset(st);
     bool released = false;
     const bool spec_entry = !st.on;   // this region's entry is speculated (run start, warm-up, after a terminal)
-    // after 2 declines in a row the next 8 regions go straight to region_process (one lean attempt
-    // after each 8: a log of short entries stops paying for attempts that cannot succeed)
-    const bool skip = declines >= 2 && declines < 10;
+    // after 2 declines in a row the next 8 regions go straight to region_process, then one lean
+    // attempt; each attempt that declines again doubles the window (up to 256 regions): a log whose
+    // regions cannot go lean (11-B entries, adversarial "tiny": 1.45 ms of k_scan_main with a fixed
+    // window of 8 against 0.96 before the lean path took several starts per slice) stops paying for
+    // attempts, and one success returns to attempting every region
+    const uint32_t win = 8u << (backoff < 5 ? backoff : 5);
+    const bool skip = declines >= 2 && declines < 2 + win;
     const bool fast = !skip && region_chained(
         wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },
         [&](bool valid, uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
@@ -1597,6 +1607,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     if (fast) {
       n_fast += dry ? 0u : 1u;
       declines = 0;
+      backoff = 0;
     } else {
       // The exact general routine, inline (run_region, ldb_chain.h): entered at the chain's position
       // when the chain is on, else speculating; its exit carries the chain into the next region. A
@@ -1631,7 +1642,10 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
       if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
       store_summary(p, r, o, lane, dry);
       chain_after_general(st, o, v, enter);
-      if (++declines >= 11) declines = 2;
+      if (++declines >= 3 + win) {   // the attempt after a window declined too
+        declines = 2;
+        backoff += 1;
+      }
     }
     // A speculated entry that leaves the chain inside an entry reaching more than kWarmSwallow past
     // this region: most likely a false header (random value bytes decode to random varint sizes),
@@ -2361,7 +2375,7 @@ int repair_grid(const ldb_ctx* c, uint64_t nreg) {
 }
 
 int uniform_grid(const ldb_ctx* c, uint64_t bytes) {
-  const uint64_t batches = bytes / 16 / 64 + 1;   // entries are >= 16 B in a run, <= 64 per wave
+  const uint64_t batches = bytes / kUniMinSize / 64 + 1;   // entries are >= kUniMinSize B in a run, <= 64 per wave
   return std::max(1, (int)std::min<uint64_t>((batches + kUniWaves - 1) / kUniWaves, (uint64_t)c->n_cu));
 }
 // k_uniform_fill: a dense sweep, 2 workgroups of 1024 threads per CU (tools/microbench/mb_uni.hip wr_W0:

@@ -288,7 +288,7 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
       chain_reset(st);
       if (r0 == rf) { st.on = 2; st.x = x0; }   // as k_scan_main: the replay's entry point
       const uint64_t warm = r0 > rf ? std::min<uint64_t>(kWarm, r0 - rf) : 0;   // dry warm-up regions
-      uint32_t declines = 0;
+      uint32_t declines = 0, backoff = 0;
       std::vector<RegionSum> keep;
       for (uint64_t r = r0 - warm; r < nreg && r < r0 + run_len; ++r) {
         const bool dry = r < r0;
@@ -298,7 +298,8 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
         const RegionSum saved = rs[r];   // a dry region's summary and tuples belong to the previous run
         std::vector<ldb_index_tuple> saved_sc;
         if (dry) saved_sc.assign(scratch.begin() + r * (uint64_t)kRegionCap, scratch.begin() + (r + 1) * (uint64_t)kRegionCap);
-        const bool skip = declines >= 2 && declines < 10;   // give-up mode
+        const uint32_t win = 8u << (backoff < 5 ? backoff : 5);   // give-up mode (as k_scan_main)
+        const bool skip = declines >= 2 && declines < 2 + win;
         static const long dbg_r = getenv("LDB_EMU_DBG_R") ? atol(getenv("LDB_EMU_DBG_R")) : -1;
         if ((long)r == dbg_r || (long)r + 1 == dbg_r)
           fprintf(stderr, "region %llu dry=%d st.on=%u st.x=%llu declines=%u skip=%d\n", (unsigned long long)r, (int)dry,
@@ -306,6 +307,7 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
         if (!skip && emu.run_chained(p, r, st)) {
           n_fast += dry ? 0u : 1u;
           declines = 0;
+          backoff = 0;
         } else {
           // the general routine inline (run_region, ldb_chain.h)
           uint32_t enter = kForceSpec;
@@ -313,7 +315,10 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
             enter = st.x - r * (uint64_t)kW < (uint64_t)region_len(p, r) ? (uint32_t)(st.x - r * (uint64_t)kW) : kForceNone;
           const RegionSum o = emu.run(p, r, enter);
           chain_after_general(st, o, emu.view(p, r), enter);
-          if (++declines >= 11) declines = 2;
+          if (++declines >= 3 + win) {
+            declines = 2;
+            backoff += 1;
+          }
         }
         if (spec_entry && st.on && st.x > r * (uint64_t)kW + kWarmSwallow) chain_reset(st);   // as k_scan_main
         if ((long)r == dbg_r)

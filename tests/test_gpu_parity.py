@@ -198,9 +198,11 @@ def _fixed_log(n, klen, vlen, seed, expired_at=0, tx_id=0):
 
 @pytest.mark.parametrize("shape", [(64, 256, 0, 0), (16, 100, 0, 0), (13, 70, 0, 0), (20, 33, 1700000000, 7),
                                    (9, 9, 0, 0), (64, 256, 0, 1 << 40), (16, 361, 0, 0), (40, 1000, 0, 0),
-                                   (16, 3041, 0, 0), (64, 5000, 0, 0), (16, 362, 0, 0)])
+                                   (16, 3041, 0, 0), (64, 5000, 0, 0), (16, 362, 0, 0),
+                                   (1, 0, 0, 0), (0, 0, 0, 0), (0, 1, 0, 0), (2, 3, 0, 0), (1, 4, 0, 0)])
 def test_run_prefix_shapes(eng, shape):
-    """The run prefix (k_uniform): equal-sized entries at the file start, one per lane, then the
+    """The run prefix (k_uniform): equal-sized entries at the file start (10-B entries up: a header and
+    no key or value), then the
     region pipeline from the first entry outside the run. Every span length mod 8, long headers,
     clean and cut ends, corrupted entries at the run's start / middle / end, a run followed by
     other entries; both IOController rules and both tuple kinds (k_uniform writes ldb_entry too)."""

@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4o_gputests.log 2>&1; rc=$?; tail -2 gpurun_out/r4o_gputests.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/r4o_gputests.log | head -30; exit $rc; }
+timeout -k 10 400 python tools/adversarial.py > gpurun_out/r04_adv.jsonl 2>gpurun_out/r04_adv.err || exit 1
+cat gpurun_out/r04_adv.jsonl
+VARIANTS="liblazydb_gpu" CASES="1 w" ROUNDS=1 bash tools/scan_ab.sh || exit 1
+T=r4o NOTEST=1 VARIANTS="var_git_9d49948 liblazydb_gpu" ROUNDS=1 bash tools/gpu_session.sh
