@@ -936,6 +936,11 @@ def main():
                 "run_entries": int(r.n_run),
                 "avg_pipeline_ms": round(total_ms, 4),
                 "algorithmic_bytes_per_launch": kbytes,
+                # k_uniform also writes the run's tuples (16 or 48 B per entry, uni_post_fill / the verify
+                # loop): read + written bytes over the same launch time, beside the read-only figure
+                "achieved_incl_tuple_writes": (round((kbytes + int(r.n_run) * (16 if args.kind == 0 else 48))
+                                                     / (kms * 1e-3) / 1e9, 1)
+                                               if kname == "k_uniform" and kms > 0 else None),
                 "practical_ceiling": {"kernel": "read-only reduction over the image (ldb_read_ceiling)",
                                       "GB_per_s": round(ceiling, 1) if ceiling else None,
                                       "frac": round(achieved / ceiling, 4) if achieved and ceiling else None},

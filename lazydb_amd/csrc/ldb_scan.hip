@@ -1590,6 +1590,9 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     // attempts, and one success returns to attempting every region
     const uint32_t win = 8u << (backoff < 5 ? backoff : 5);
     const bool skip = declines >= 2 && declines < 2 + win;
+    // (round 4: a single-start form of region_chained until a wave's first decline was measured and
+    // rejected -- config 3 2.73 -> 2.84 ms, and the writer mix's speculation then took false starts
+    // where a lane's true first start has a second one behind it: 1 ms of k_repair)
     const bool fast = !skip && region_chained(
         wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },
         [&](bool valid, uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {

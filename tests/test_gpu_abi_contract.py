@@ -206,8 +206,9 @@ def test_five_contexts_five_threads():
             start.wait()
             for i, d in enumerate(dev[t]):
                 cap = d.numel() // 10 + 16
-                out = eng.alloc_out(cap)
-                res = eng.alloc_result()
+                with torch.cuda.stream(s):   # the result's zero fill ordered before the scan on s
+                    out = eng.alloc_out(cap)
+                    res = eng.alloc_result()
                 rc = N.lib().ldb_scan_file_dev(eng.ctx, C.c_void_p(d.data_ptr()), d.numel(), i + 1, N.FILEIO,
                                                N.TUPLE_INDEX, C.c_void_p(out.data_ptr()), cap,
                                                C.c_void_p(res.data_ptr()), C.c_void_p(s.cuda_stream))
