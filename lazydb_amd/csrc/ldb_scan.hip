@@ -641,14 +641,18 @@ __device__ __forceinline__ bool uni_probe16(const Pipe& p, const UniMemo& m, uin
 // ballot each (one LDS atomic per wave, not per lane). The probe that sets the final M leaves its 48
 // header bytes in stash[0..12) (stash[12] = x & 3): the next run's entry 0 without another load.
 // Returns nc - 1 when round 0 finds no mismatch.
-__device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint32_t* stash) {
+// Runs the search from bracket (lo, hi) (lo: a passing candidate or the start, hi: a failing one or nc - 1)
+// and returns true with hi = M, or, when `stop_wide` and round 0 left a bracket of more than blockDim
+// candidates (two rounds more), false after round 0 with the bracket in (lo, hi). `first`: round 0 is the
+// dense + geometric one (a continuation probes the bracket only).
+__device__ bool uni_search(const Pipe& p, const UniRun& q, uint64_t& lo, uint64_t& hi, uint32_t* stash, bool first,
+                           bool stop_wide) {
   // a round's smallest failing and largest passing probe: two slots, alternating by round, so the next
   // round's pair is set up before this round's last barrier (two barriers a round)
   __shared__ unsigned long long s_fail[2], s_pass[2];
   const UniMemo& m = q.m;
   const uint64_t sz = m.sz, need = sz > 48 ? sz : 48;
   const uint32_t t = threadIdx.x, nt = blockDim.x, lane = t & 63u;
-  uint64_t hi = q.nc - 1;
   if (t == 0) {
     s_fail[0] = hi;
     s_pass[0] = 0;
@@ -657,9 +661,10 @@ __device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint
   for (int round = 0; hi > lo + 1; ++round) {
     UNI_T(r0);
     const int cur = round & 1;
+    const bool rz = first && round == 0;
     const uint64_t w = hi - lo - 1;   // candidates strictly between
     uint64_t e = 0;
-    if (round == 0) {
+    if (rz) {
       if (t < 128) {
         e = lo + 1 + t;
       } else if (t < 256) {
@@ -688,7 +693,7 @@ __device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint
       for (int i = 0; i < 12; ++i) stash[i] = d[i];
       stash[12] = (uint32_t)(x & 3u);
     }
-    if (round == 0 && f == hi) return hi;
+    if (rz && f == hi) return true;   // no mismatch: the run reaches the file's end
     const uint64_t pm = __ballot(act && pass && e < f);
     if (pm && lane == 63u - (uint32_t)__builtin_clzll(pm)) atomicMax(&s_pass[cur], (unsigned long long)e);
     if (t == 0) {   // the next round's pair (last read before this round's first barrier)
@@ -702,26 +707,63 @@ __device__ uint64_t uni_search(const Pipe& p, const UniRun& q, uint64_t lo, uint
     UNI_T(r1);
     UNI_ADD(10, 0, 1);
     UNI_ADD(11, r0, r1);
+    if (rz && stop_wide && hi - lo - 1 > nt) return false;
   }
-  return hi;
+  return true;
+}
+
+// Publishes runs [from, to) of ru (records, F words: a run's M, or its probe bound hi for the run still
+// being searched, or "none"), then dyn[6] = to (| kUniFinal). Every thread of workgroup 0.
+__device__ void uni_publish_runs(const Pipe& p, const UniRuns& ru, int from, int to, const unsigned long long* s_f,
+                                 bool fin) {
+  UNI_T(p0);
+  for (int r = from; r < to; ++r) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&ru.r[r]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(uni_recs(p) + r);
+    for (uint32_t i = threadIdx.x; i < sizeof(UniRun) / 4; i += blockDim.x) dst[i] = src[i];
+  }
+  if ((int)threadIdx.x >= from && (int)threadIdx.x < to) *uni_fword(p, threadIdx.x) = s_f[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&p.dyn[6], (uint64_t)to | (fin ? kUniFinal : 0ull), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  UNI_T(p1);
+  UNI_ADD(12, p0, p1);
 }
 
 // Workgroup 0 of a kMulti launch, run 0's memo in ru: for each run, its end M (uni_search), then the
 // entry at M as the next run's entry 0 when it decodes as a run start (a memo and a slicing; its entry 1
-// is the next search's first probe), up to kUniMaxRuns runs. Then the list is published: the records,
-// each run's F (its M, or "none" when no boundary was found), dyn[6] = the count | kUniFinal.
+// is the next search's first probe), up to kUniMaxRuns runs. A run whose first probe round leaves a wide
+// bracket (a long run: two rounds more) is published right then, with the runs before it, its F = the
+// bracket's failing end (INDEX-kind scans: no candidate's verification stores anything); the others
+// verify them while this workgroup narrows the bracket, and its M then lowers F. The rest of the list
+// is published at the end, with kUniFinal.
 __device__ void uni_discover(const Pipe& p, UniRuns& ru) {
   __shared__ int s_next;
   __shared__ uint32_t stash[13];
   __shared__ unsigned long long s_f[kUniMaxRuns];
+  const bool early = p.kind == LDB_TUPLE_INDEX;
+  int published = 0;
   for (;;) {
     const int r = ru.n - 1;
     UniRun& q = ru.r[r];
     UNI_T(b0);
-    const uint64_t M = uni_search(p, q, r == 0 ? 1 : 0, stash);
+    uint64_t lo = r == 0 ? 1 : 0, hi = q.nc - 1;
+    bool wide = false;
+    if (!uni_search(p, q, lo, hi, stash, true, early)) {   // published now, narrowed below
+      wide = true;
+      if (threadIdx.x == 0) {
+        s_f[r] = hi;
+        ru.r[r].nc = hi + 1;
+      }
+      __syncthreads();
+      uni_publish_runs(p, ru, published, r + 1, s_f, false);
+      published = r + 1;
+      uni_search(p, q, lo, hi, stash, false, false);
+    }
+    const uint64_t M = hi;
     UNI_T(b1);
     UNI_ADD(2, b0, b1);
-    const bool brk = M < q.nc - 1;   // (uniform)
+    const bool brk = M < (p.len - q.y) / q.m.sz;   // (uniform) M below the first candidate past the file
     if (r > 0 && M < 2) {   // a later "run" of one entry (entry 1 differs): no run; the chain goes on from
       if (threadIdx.x == 0) ru.n = r;   // its entry 0 in the region pipeline (K = its gbase)
       __syncthreads();
@@ -730,6 +772,10 @@ __device__ void uni_discover(const Pipe& p, UniRuns& ru) {
     if (threadIdx.x == 0) {
       s_f[r] = brk ? M : ~0ull;
       if (brk) q.nc = M;
+      if (wide) {   // already published: its F may be lower by now (a verified failure)
+        atomicMin((unsigned long long*)uni_fword(p, r), (unsigned long long)M);
+        uni_recs(p)[r].nc = q.nc;
+      }
       s_next = brk && r + 1 < kUniMaxRuns;
     }
     __syncthreads();
@@ -753,48 +799,38 @@ __device__ void uni_discover(const Pipe& p, UniRuns& ru) {
     UNI_ADD(3, b1, b2);
     if (!s_next) break;
   }
-  UNI_T(p0);
-  for (int r = 0; r < ru.n; ++r) {   // the list, then the flag
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&ru.r[r]);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(uni_recs(p) + r);
-    for (uint32_t i = threadIdx.x; i < sizeof(UniRun) / 4; i += blockDim.x) dst[i] = src[i];
-  }
-  if (threadIdx.x < (uint32_t)ru.n) *uni_fword(p, threadIdx.x) = s_f[threadIdx.x];
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&p.dyn[6], (uint64_t)ru.n | kUniFinal, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  UNI_T(p1);
-  UNI_ADD(12, p0, p1);
+  uni_publish_runs(p, ru, published, ru.n, s_f, true);
 }
 
-// Every workgroup of a kMulti launch: the run list once workgroup 0 has published it (spinning on
-// dyn[6]; workgroup 0 is dispatched first), then each run's slicing (uni_geometry, wave i for run i;
-// run 0's too unless `have0`).
-__device__ __forceinline__ void uni_take_runs(const Pipe& p, UniRuns& ru, bool have0) {
-  __shared__ int s_n;
+// Every workgroup of a kMulti launch: the runs published beyond the first `have` (spinning on dyn[6];
+// workgroup 0 is dispatched first), copied in, each new run's slicing computed (uni_geometry, one wave
+// per run; run 0's only unless `have0`). Returns the published word (count | kUniFinal).
+__device__ __forceinline__ uint64_t uni_take_runs(const Pipe& p, UniRuns& ru, int have, bool have0) {
+  __shared__ unsigned long long s_w;
   UNI_T(w0);
   if (threadIdx.x == 0) {
     uint64_t w;
     for (;;) {
       w = __hip_atomic_load(&p.dyn[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (w & kUniFinal) break;
+      if ((int)(uint32_t)w > have || (w & kUniFinal)) break;
       __builtin_amdgcn_s_sleep(LDB_UNI_SPIN);   // (every workgroup's thread 0 polls one word)
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    s_n = (int)(uint32_t)w;
+    s_w = w;
   }
   __syncthreads();
-  const int n = s_n;
+  const uint64_t w = s_w;
+  const int n = (int)(uint32_t)w;
   if (blockIdx.x != 0) {   // (workgroup 0: its own list; the others have run 0 but for its nc)
-    for (int r = 1; r < n; ++r) {
+    for (int r = have > 1 ? have : 1; r < n; ++r) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(uni_recs(p) + r);
       uint32_t* dst = reinterpret_cast<uint32_t*>(&ru.r[r]);
       for (uint32_t i = threadIdx.x; i < sizeof(UniRun) / 4; i += blockDim.x) dst[i] = src[i];
     }
-    if (threadIdx.x == 0) ru.r[0].nc = uni_recs(p)[0].nc;
+    if (threadIdx.x == 0 && have == 0 && n > 0) ru.r[0].nc = uni_recs(p)[0].nc;
   }
   __syncthreads();
-  const int wv = (int)(threadIdx.x >> 6);
+  const int wv = have + (int)(threadIdx.x >> 6);
   if (wv < n && (wv > 0 || !have0)) {
     UniRun& q = ru.r[wv];
     const UniGeo g = uni_geometry(p.xw, (uint32_t)(q.m.sz - 4));
@@ -804,6 +840,14 @@ __device__ __forceinline__ void uni_take_runs(const Pipe& p, UniRuns& ru, bool h
   __syncthreads();
   UNI_T(w1);
   UNI_ADD(9, w0, w1);
+  return w;
+}
+
+// Once the list is final: every run's nc as last published (a long run published early got its M
+// after), for the INDEX sweep's slices -- the same in every workgroup
+__device__ __forceinline__ void uni_refresh_nc(const Pipe& p, UniRuns& ru) {
+  if (blockIdx.x != 0 && (int)threadIdx.x < ru.n) ru.r[threadIdx.x].nc = uni_recs(p)[threadIdx.x].nc;
+  __syncthreads();
 }
 
 template <bool kMulti>
@@ -929,8 +973,8 @@ __device__ __forceinline__ void uni_level(GpuWave& wp, const uint32_t* T, uint32
 // NW: the workgroup's verifying waves (waves 0 .. NW-1; kUniWaves, or one fewer beside a fill wave).
 template <int S, bool kChunk, bool kHash, bool kFill, bool kAl, int NW>
 __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint64_t* F, const uint8_t* lp2,
-                                          const uint32_t* T, int lane, int wave, uint64_t a_lo, uint64_t a_hi,
-                                          uint64_t bound) {
+                                          const uint32_t* T, int lane, int wave, uint32_t wg, uint32_t nwg,
+                                          uint64_t a_lo, uint64_t a_hi, uint64_t bound) {
   if (!kChunk) {   // the whole image in one launch (the device-resident API): no range arithmetic
     a_lo = 0;
     a_hi = p.len;
@@ -973,7 +1017,8 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
   v2u32 kv = {(uint32_t)bound, (uint32_t)(bound >> 32)};   // F as loaded during the previous batch (vector value:
                                                            // read at the next top); first the probes' bound
   const __amdgpu_buffer_rsrc_t krs = rsrc_of(F, 8);
-  for (uint64_t b = b_first + (uint64_t)blockIdx.x * NW + wave; b < nbatch; b += (uint64_t)gridDim.x * NW) {
+  // (wg, nwg: this workgroup's place among the verifying ones; a kMulti launch leaves workgroup 0 out)
+  for (uint64_t b = b_first + (uint64_t)wg * NW + wave; b < nbatch; b += (uint64_t)nwg * NW) {
     if (kChunk && b * Esz > (all_hi ? p.len : a_hi)) break;   // wave-uniform: no candidate of this launch from here on
     // uniform by construction (one address), but a load's result is divergent to the compiler: the
     // loop exit on it would make b, and every descriptor built from b, divergent (waterfall loops)
@@ -1284,13 +1329,13 @@ __device__ __forceinline__ bool scan_done(const Pipe& p) { return p.dyn[3] == kU
 template <bool kChunk, bool kHash, bool kFill, int NW>
 __device__ __forceinline__ void uni_run(const Pipe& p, const UniRun& q, uint64_t* F, const uint8_t* lp2,
                                         const uint32_t* comb, int lane, int wave, uint64_t a_lo, uint64_t a_hi,
-                                        uint64_t bound) {
+                                        uint64_t bound, uint32_t wg = blockIdx.x, uint32_t nwg = gridDim.x) {
   const bool al = (q.m.sz & 3u) == 0 && (q.g.t & 3u) == 0 && (q.y & 3u) == 0;   // every window and header dword-aligned
   switch (q.g.S) {   // uni_geometry: 1 <= S <= kUniSteps
 #define LDB_UNI_CASE(n)                                                                                 \
   case n:                                                                                               \
-    if (al) uni_waves<n, kChunk, kHash, kFill, true, NW>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, bound);  \
-    else uni_waves<n, kChunk, kHash, kFill, false, NW>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, bound);    \
+    if (al) uni_waves<n, kChunk, kHash, kFill, true, NW>(p, q, F, lp2, comb, lane, wave, wg, nwg, a_lo, a_hi, bound); \
+    else uni_waves<n, kChunk, kHash, kFill, false, NW>(p, q, F, lp2, comb, lane, wave, wg, nwg, a_lo, a_hi, bound);  \
     break;
     LDB_UNI_CASE(1) LDB_UNI_CASE(2) LDB_UNI_CASE(3) LDB_UNI_CASE(4) LDB_UNI_CASE(5) LDB_UNI_CASE(6)
     LDB_UNI_CASE(7) LDB_UNI_CASE(8) LDB_UNI_CASE(9) LDB_UNI_CASE(10) LDB_UNI_CASE(11) LDB_UNI_CASE(12)
@@ -1324,7 +1369,7 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
 #endif
   uint64_t bound;
   if (!uni_prepare<kMulti>(p, su, ru, comb, kChunk ? a_hi : p.len, bound)) return;   // (its __syncthreads also publish the LP2 block)
-  if (kMulti && blockIdx.x == 0) lp2_build(lp2, p.gtab);   // (published by uni_take_runs' barriers)
+  if (kMulti && blockIdx.x == 0 && gridDim.x == 1) lp2_build(lp2, p.gtab);   // (published by uni_take_runs' barriers)
   __syncthreads();
 #ifdef LDB_STAMPS
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2_) :: "memory");
@@ -1342,24 +1387,42 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
     UNI_ADD(6, v0, v1);
     if (!kChunk || a_hi >= p.len) uni_finish<false>(p, ru);
   } else {
-    // the run list (uni_discover), each run verified up to its F, then the INDEX tuples written
-    uni_take_runs(p, ru, blockIdx.x != 0);
-    if (blockIdx.x == 0) uni_build_comb(p, ru.r[0].g, comb, nullptr);
-    for (int r = 0; r < ru.n; ++r) {
-      const UniRun& q = ru.r[r];
-      uint64_t* F = uni_fword(p, r);
-      if (r > 0 && (q.g.G != ru.r[r - 1].g.G || q.g.P != ru.r[r - 1].g.P)) {
-        UNI_T(c0);
-        __syncthreads();   // every wave is done with the old tables
-        uni_build_comb(p, q.g, comb, nullptr);
-        UNI_T(c1);
-        UNI_ADD(5, c0, c1);
+    // the runs as workgroup 0 publishes them (uni_discover), each verified up to its F; once the list is
+    // final, the INDEX tuples written
+    const bool verifies = gridDim.x == 1 || blockIdx.x != 0;   // workgroup 0 found the runs, and starts last
+    bool built0 = blockIdx.x != 0;   // (workgroup 0 builds its combine tables only to verify)
+    for (int have = 0;;) {
+      const uint64_t w = uni_take_runs(p, ru, have, blockIdx.x != 0);
+      const int n = (int)(uint32_t)w;
+      if (verifies) {
+        if (!built0 && n > 0) {
+          uni_build_comb(p, ru.r[0].g, comb, nullptr);
+          built0 = true;
+        }
+        for (int r = have; r < n; ++r) {
+          const UniRun& q = ru.r[r];
+          uint64_t* F = uni_fword(p, r);
+          if (r > 0 && (q.g.G != ru.r[r - 1].g.G || q.g.P != ru.r[r - 1].g.P)) {
+            UNI_T(c0);
+            __syncthreads();   // every wave is done with the old tables
+            uni_build_comb(p, q.g, comb, nullptr);
+            UNI_T(c1);
+            UNI_ADD(5, c0, c1);
+          }
+          UNI_T(v0);
+          if (gridDim.x == 1) uni_run<kChunk, kHash, !kHash, kUniWaves>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, ~0ull);
+          else
+            uni_run<kChunk, kHash, !kHash, kUniWaves>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, ~0ull, blockIdx.x - 1,
+                                                      gridDim.x - 1);
+          UNI_T(v1);
+          UNI_ADD(6, v0, v1);
+        }
       }
-      UNI_T(v0);
-      uni_run<kChunk, kHash, !kHash, kUniWaves>(p, q, F, lp2, comb, lane, wave, a_lo, a_hi, ~0ull);
-      UNI_T(v1);
-      UNI_ADD(6, v0, v1);
+      have = n;
+      if (w & kUniFinal) break;
+      __syncthreads();   // (every wave past the runs before the next copy-in)
     }
+    uni_refresh_nc(p, ru);
     UNI_T(f0);
     if (p.kind == LDB_TUPLE_INDEX) uni_post_fill(p, ru);
     UNI_T(f1);
