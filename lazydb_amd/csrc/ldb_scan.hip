@@ -591,6 +591,94 @@ __device__ __forceinline__ bool uni_sliceable(uint32_t L) {
   return false;
 }
 
+// uni_memo of the entry at image offset y, computed across the wave: lane i holds byte y + i (zero past
+// len). The five header varints (log_entry.go:86-106, Go's binary.Uvarint) end at the first five bytes
+// below 0x80 from byte 5 on (one ballot); each is read by one lane from its bytes (shuffles), and a memo
+// exists only when all five are canonical, at most 10 bytes (no overflow) and inside the 38-byte window
+// -- exactly the headers uni_memo accepts (it needs `canonical`), with the same fields. The generic
+// decode run by one lane through readlane is ~2,000 scalar instructions (4.5 K cycles a run at config
+// 1, on the run search's chain); this is a few hundred.
+#ifndef LDB_UNI_FASTMEMO
+#define LDB_UNI_FASTMEMO 1   // 0: the generic decode (uni_memo through readlane), A/B
+#endif
+__device__ __forceinline__ UniMemo uni_memo_wave(const Pipe& p, uint64_t y, uint32_t b) {
+  UniMemo m;
+  m.ok = 0;
+  const int lane = (int)(threadIdx.x & 63u);
+  // the five varints' last bytes: the first five set bits of T (bytes 5 .. 37 of the window)
+  const uint64_t T = __ballot(lane >= 5 && lane < kMaxHeader && b < 0x80u);
+  // lane j < 5: varint j's first byte s and last byte e; every lane gathers the 10 bytes from its s
+  uint64_t t = T;
+  int e = -1, s0 = 5;
+  for (int j = 0; j < 5; ++j) {
+    const int ej = t ? __builtin_ctzll(t) : 64;
+    if (j == lane) { e = ej; }
+    if (j < lane) s0 = ej + 1;
+    t &= t - 1;
+  }
+  const int sj = lane < 5 ? s0 : 0;
+  uint64_t u = 0;
+  uint32_t last = 0;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const uint32_t bk = (uint32_t)__shfl((int)b, (sj + k) & 63);
+    if (lane < 5 && sj + k <= e) {
+      u |= (uint64_t)(bk & 0x7Fu) << (7 * k);
+      last = bk;
+    }
+  }
+  const int n = e - sj + 1;   // the varint's length (lane < 5)
+  // per varint: terminated inside the window, <= 10 bytes, no overflow in byte 10, canonical
+  const bool vok = lane >= 5 || (e < kMaxHeader && n <= 10 && !(n == 10 && last > 1u) && (n == 1 || last != 0u));
+  if (__ballot(!vok)) return m;
+  const int64_t zz = (int64_t)(u >> 1) ^ -(int64_t)(u & 1);   // binary.Varint's zig-zag
+  auto field = [&](int j) -> int64_t {
+    const uint64_t v = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)zz >> 32), j) << 32) |
+                       (uint32_t)__shfl((int)(uint32_t)(uint64_t)zz, j);
+    return (int64_t)v;
+  };
+  const int64_t ea = field(0), tx = field(1), ts = field(2), ks = field(3), vs = field(4);
+  const int hs = __shfl(e, 4) + 1;   // decodeHeader's offset after the five varints
+  if (ks < 0 || vs < 0 || ks > 0xFFFFFFFFll || vs > 0xFFFFFFFFll) return m;   // (canonical)
+  const uint32_t crc = (uint32_t)__shfl((int)b, 0) | ((uint32_t)__shfl((int)b, 1) << 8) |
+                       ((uint32_t)__shfl((int)b, 2) << 16) | ((uint32_t)__shfl((int)b, 3) << 24);
+  // classify_entry: the header window readable, not the zero sentinel, key/value readable
+  if (read_eof(p.len, p.io, (int64_t)y, kMaxHeader)) return m;
+  const uint32_t k = (uint32_t)ks, v = (uint32_t)vs;
+  if (crc == 0u && k == 0u && v == 0u) return m;
+  const uint64_t kv = (uint64_t)k + v;
+  if (kv && read_eof(p.len, p.io, (int64_t)(y + (uint64_t)hs), kv)) return m;
+  const uint64_t size = (uint64_t)hs + kv;
+  if (hs < 10 || hs > kMaxHeader || size > kUniMaxSize || size < kUniMinSize) return m;
+  m.hs = (uint32_t)hs;
+  m.enc = (uint32_t)(5 + varint_len(ea) + varint_len(tx) + varint_len((int64_t)(uint16_t)ts) + varint_len((int64_t)k) +
+                     varint_len((int64_t)v));
+  m.stat = (uint32_t)__shfl((int)b, 4);
+  m.tx_stat = (uint32_t)(uint16_t)ts;
+  m.k = k;
+  m.v = v;
+  m.expired_at = ea;
+  m.tx_id = (uint64_t)tx;
+  m.sz = size;
+  m.nw = (m.hs - 4 + 3) / 4;
+  // header dwords [4 + 4 i, + 4) (bytes past the 38-byte window read as 0, as uni_memo's fetch)
+  const int lb = 4 + 4 * (lane < 9 ? lane : 0);
+  uint32_t dw = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t bq = (uint32_t)__shfl((int)b, lb + q);
+    dw |= (lb + q < kMaxHeader ? bq : 0u) << (8 * q);
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int nb = (int)m.hs - 4 - 4 * i;
+    m.msk[i] = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * nb)));
+    m.w[i] = (uint32_t)__shfl((int)dw, i) & m.msk[i];
+  }
+  m.ok = 1;
+  return m;
+}
+
 // Wave 0 of the workgroup, all 64 lanes (wave-uniform control): run q's memo from the entry at image
 // offset y, lane i holding byte y + i (zero past len), decoded through readlane, not by one lane's
 // dependent byte reads (each an LDS or memory round trip: ~5 us per run). kGeo: its slicing too (a
@@ -599,7 +687,7 @@ template <bool kGeo>
 __device__ __forceinline__ bool uni_decode_wave(const Pipe& p, uint64_t y, uint32_t b, UniRun& q) {
   auto fetch = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)b, i); };
   UNI_T(d0);
-  const UniMemo m = uni_memo(fetch, p.len, p.io, y);
+  const UniMemo m = LDB_UNI_FASTMEMO ? uni_memo_wave(p, y, b) : uni_memo(fetch, p.len, p.io, y);
   UNI_T(d1);
   if (blockIdx.x == 0) UNI_ADD(4, d0, d1);
   UniGeo g{};
@@ -640,7 +728,8 @@ __device__ __forceinline__ bool uni_probe16(const Pipe& p, const UniMemo& m, uin
 // probes of a wave are in increasing order, so its smallest failing and largest passing probe are one
 // ballot each (one LDS atomic per wave, not per lane). The probe that sets the final M leaves its 48
 // header bytes in stash[0..12) (stash[12] = x & 3): the next run's entry 0 without another load.
-// Returns nc - 1 when round 0 finds no mismatch.
+// (Measured and rejected: one barrier a round, every thread reducing the waves' pairs from LDS -- config
+// 1 k_uniform 0.142 -> 0.158 ms.)
 // Runs the search from bracket (lo, hi) (lo: a passing candidate or the start, hi: a failing one or nc - 1)
 // and returns true with hi = M, or, when `stop_wide` and round 0 left a bracket of more than blockDim
 // candidates (two rounds more), false after round 0 with the bracket in (lo, hi). `first`: round 0 is the
