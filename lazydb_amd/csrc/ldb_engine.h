@@ -109,7 +109,10 @@ constexpr uint32_t kSkip = 2u;       // its CRC span starts < 4 bytes before (or
 constexpr uint32_t kNoCrc = 4u;      // its decoded header size <= 4: getEntryCrc returns 0 (already checked)
 
 constexpr int kOverflow = 100;       // internal: region needs more than kRegionCap tuple slots
-constexpr uint64_t kWarm = 2;        // k_scan_main: regions a wave's run starts early, processed dry (chain warm-up)
+#ifndef LDB_KWARM
+#define LDB_KWARM 2
+#endif
+constexpr uint64_t kWarm = LDB_KWARM;   // k_scan_main: regions a wave's run starts early, processed dry (chain warm-up)
 #ifndef LDB_SWALLOW_LOG2
 #define LDB_SWALLOW_LOG2 18
 #endif
