@@ -285,7 +285,7 @@ __device__ uint64_t g_stamps[kStampSlots];
 // k_uniform's phases (tools/uni_stamps.py), thread 0 of every workgroup: 0 run 0's window, 1 its decode +
 // combine tables + publication, 2 header probes, 3 later runs' windows, 4 their decodes, 5 combine
 // rebuilds between runs, 6 the verify loops, 7 the INDEX fill, 8 uni_finish
-constexpr int kUniStampSlots = 16;
+constexpr int kUniStampSlots = 24;
 __device__ uint64_t g_ustamps[kUniStampSlots];
 __device__ __forceinline__ uint64_t uni_now() {
   uint64_t t;
@@ -978,8 +978,11 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
   if (threadIdx.x < 64) {   // entry 0 decoded by wave 0 (readlane), entry 1's header from the window
     UniRun& q = ru.r[0];
     // (workgroup 0 of a kMulti launch leaves the slicing for later: it finds the runs first)
+    UNI_T(q0);
     bool ok = kMulti && blockIdx.x == 0 ? uni_decode_wave<false>(p, 0, wb[threadIdx.x], q)
                                         : uni_decode_wave<true>(p, 0, wb[threadIdx.x], q);
+    UNI_T(q1);
+    if (blockIdx.x != 0) UNI_ADD(16, q0, q1);
     if (threadIdx.x == 0) {
       if (ok) {
         const uint8_t* h = wb + q.m.sz;   // sz + 40 < kUniWin
@@ -1001,10 +1004,14 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
     }
   }
   __syncthreads();
+  UNI_T(q2);
+  if (blockIdx.x != 0) UNI_ADD(17, s1, q2);
   if (kMulti) {
     if (!su.g.ok) return false;
     if (blockIdx.x != 0) {
       uni_build_comb(p, su.g, T, nullptr);   // while workgroup 0 finds the runs
+      UNI_T(q3);
+      UNI_ADD(18, q2, q3);
     } else if (!LDB_UNI_NOPROBE) {
       uni_discover(p, ru);
     } else if (threadIdx.x == 0) {

@@ -16,8 +16,8 @@ L = N.lib()
 L.ldb_debug_stamps.argtypes = [C.c_void_p, C.c_int]
 L.ldb_debug_ustamps.argtypes = [C.c_void_p, C.c_int]
 buf = np.zeros(18, np.uint64)
-ub = np.zeros(16, np.uint64)
-PH = ["win0", "dec0+comb(+WG0 discovery)", "probes(WG0)", "decN(WG0)", "memo(WG0 x6)", "comb-rebuild", "verify(w0)", "fill", "finish", "wait", "rounds(WG0)", "round-time(WG0)", "publish(WG0)", "geometry(WG0 x6)", "probe-t0(WG0)", "barrier2(WG0)"]
+ub = np.zeros(24, np.uint64)
+PH = ["win0", "dec0+comb(+WG0 discovery)", "probes(WG0)", "decN(WG0)", "memo(WG0 x6)", "comb-rebuild", "verify(w0)", "fill", "finish", "wait", "rounds(WG0)", "round-time(WG0)", "publish(WG0)", "geometry(WG0 x6)", "probe-t0(WG0)", "barrier2(WG0)", "prep-decode(WG>0)", "prep-to-decoded(WG>0)", "prep-comb(WG>0)"]
 for name, (img, n, end) in (("cfg4-shape 64 MiB", coracle.gen_log(64 << 20, 1, ksize=64, vsize=256)),
                              ("cfg1 bench log", coracle.gen_bench_log(512 << 20, 1, n_entries=500_000))):
     d = torch.from_numpy(img).cuda()
@@ -36,4 +36,4 @@ for name, (img, n, end) in (("cfg4-shape 64 MiB", coracle.gen_log(64 << 20, 1, k
     print(f"{name}: LP2 block {buf[9] / (reps * nwg):8.0f} cyc/WG, uni_prepare {buf[17] / (reps * nwg):8.0f} cyc/WG "
           f"(s_memtime counts shader clocks)")
     # WG0-only phases (discovery) per launch; the rest averaged over the workgroups
-    print("   " + " ".join(f"{k} {ub[i] / (reps * (1 if 'WG0' in k and '+' not in k else nwg)):.0f}" for i, k in enumerate(PH)))
+    print("   " + " ".join(f"{k} {ub[i] / (reps * (1 if 'WG0' in k and '+' not in k else (nwg - 1 if 'WG>0' in k else nwg))):.0f}" for i, k in enumerate(PH)))
