@@ -1314,7 +1314,9 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
 // K (F may still drop) lies beyond n_entries, where the region pipeline writes its own tuples from K on.
 // F_r <= M_r (uni_discover), so no run writes into the next run's tuples. The slices come from the runs'
 // nc (the same in every workgroup; F as seen here is not).
-// (Round 4: per-wave stores of each wave's own batches, 4 scattered 256-B pieces per instruction, cost
+// (Round 4: writing each run's tuples before verifying it, once its end is known, so the stores would
+// drain under the verification's loads, measured and rejected: config 4 k_uniform 0.764 -> 0.792 ms.
+// Per-wave stores of each wave's own batches, 4 scattered 256-B pieces per instruction, cost
 // 61 us at config 4 against 33 for the separate dense sweep; a fill per run, after each run's verify
 // loop, 20 us at config 1 against 8 for this one sweep -- a barrier per run. Streaming stores (nt):
 // config 4 k_uniform 0.808 -> 0.768 ms on one box -- with plain stores the tuples sat dirty in L2, and
