@@ -40,6 +40,7 @@ struct Pipe {
   void* out;
   uint64_t cap;
   int kind;
+  uint32_t epoch;             // this scan's number on its workspace (k_uniform's run-list word carries it)
   ldb_scan_result* result;
 };
 

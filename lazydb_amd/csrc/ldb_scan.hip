@@ -552,12 +552,20 @@ __device__ __forceinline__ void uni_build_comb(const Pipe& p, const UniGeo& g, u
 // trip, ~1 us, plus three barriers), the next run's header from a probe's own loads (no extra load),
 // decoded through readlane by one wave; the slicing (uni_geometry: a table load and two multmodp) is
 // left to the verifying workgroups, one wave per run.
+#ifndef LDB_FOLD_INIT
+#define LDB_FOLD_INIT 0   // 1: k_uniform<false, false> sets the control words itself (no k_init launch)
+#endif
 #ifndef LDB_UNI_SPIN
 #define LDB_UNI_SPIN 4   // s_sleep between polls of dyn[6] (x 64 cycles)
 #endif
 constexpr uint64_t kUniRunsOff = kUniSetupBytes + 4 * kUniTabWords;
 constexpr uint64_t kUniFOff = kUniRunsOff + 256 * kUniMaxRuns;
 constexpr uint64_t kUniFinal = 1ull << 32;
+constexpr int kUniEpochShift = 33;   // dyn[6] = epoch << 33 | kUniFinal | count: a word left by an earlier
+                                     // scan on the workspace never reads as this scan's
+__device__ __forceinline__ uint64_t uni_word(const Pipe& p, uint64_t v) {
+  return ((uint64_t)(p.epoch & 0x7FFFFFFFu) << kUniEpochShift) | v;
+}
 constexpr uint64_t kUniBlockBytes = kUniFOff + 8 * kUniMaxRuns;   // the workspace's p.uni block
 static_assert(sizeof(UniRun) <= 256, "run records are 256 B apart");
 __device__ __forceinline__ UniRun* uni_recs(const Pipe& p) { return reinterpret_cast<UniRun*>(p.uni + kUniRunsOff); }
@@ -814,7 +822,8 @@ __device__ void uni_publish_runs(const Pipe& p, const UniRuns& ru, int from, int
   if ((int)threadIdx.x >= from && (int)threadIdx.x < to) *uni_fword(p, threadIdx.x) = s_f[threadIdx.x];
   __syncthreads();
   if (threadIdx.x == 0)
-    __hip_atomic_store(&p.dyn[6], (uint64_t)to | (fin ? kUniFinal : 0ull), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&p.dyn[6], uni_word(p, (uint64_t)to | (fin ? kUniFinal : 0ull)), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
   UNI_T(p1);
   UNI_ADD(12, p0, p1);
 }
@@ -901,7 +910,7 @@ __device__ __forceinline__ uint64_t uni_take_runs(const Pipe& p, UniRuns& ru, in
     uint64_t w;
     for (;;) {
       w = __hip_atomic_load(&p.dyn[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((int)(uint32_t)w > have || (w & kUniFinal)) break;
+      if ((w >> kUniEpochShift) == (p.epoch & 0x7FFFFFFFu) && ((int)(uint32_t)w > have || (w & kUniFinal))) break;
       __builtin_amdgcn_s_sleep(LDB_UNI_SPIN);   // (every workgroup's thread 0 polls one word)
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1016,7 +1025,7 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
       uni_discover(p, ru);
     } else if (threadIdx.x == 0) {
       uni_recs(p)[0] = ru.r[0];
-      __hip_atomic_store(&p.dyn[6], 1ull | kUniFinal, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&p.dyn[6], uni_word(p, 1ull | kUniFinal), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     UNI_T(s2);
     UNI_ADD(1, s1, s2);
@@ -1459,6 +1468,14 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   uint64_t t0_, t1_, t2_;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_) :: "memory");
 #endif
+  // kMulti: workgroup 0 sets the control words k_init sets on the other paths (enqueue_scan): the region
+  // pipeline's counters, the done flag and its counter (no other workgroup touches them before it has
+  // taken the run list, which workgroup 0 publishes after this), x0 unset
+  if (kMulti && LDB_FOLD_INIT && blockIdx.x == 0 && threadIdx.x < 8) {
+    p.ctr[threadIdx.x] = 0u;
+    if (threadIdx.x == 3 || threadIdx.x == 4) p.dyn[threadIdx.x] = 0;
+    if (threadIdx.x == 5) p.dyn[5] = ~0ull;
+  }
   // (workgroup 0 of a kMulti launch finds the runs first: its LP2 block afterwards, off that chain)
   if (!kMulti || blockIdx.x != 0) lp2_build(lp2, p.gtab);
 #ifdef LDB_STAMPS
@@ -2324,6 +2341,7 @@ struct ldb_ctx {
   hipEvent_t ws_ev = nullptr;
   hipStream_t ws_stream = nullptr;
   bool ws_ev_live = false;
+  uint32_t scan_epoch = 0;   // device scans enqueued on this context (Pipe::epoch)
   // kernel timing: one event triple per timed launch, recorded without host synchronisation and
   // resolved when the timing is queried (or when the pool is full)
   struct EvTriple { hipEvent_t e0, eu, ef, e1, e2; };   // start, after k_uniform, after its fill, after k_scan_main, end
@@ -2597,7 +2615,12 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   // the run prefix: K = ~0 until k_uniform lowers it to the first entry outside the run
   // ctr zero; K = ~0 and the setup not published (no_run: K = 0): one tiny launch instead of two
   // memsets (a blit launch each, ~10 us of the config-4 step between them)
-  hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, s, p.ctr, p.dyn, no_run ? 0ull : ~0ull);
+  // the device path's whole-image run prefix (k_uniform<false, false>) sets the control words itself
+  // (its workgroup 0, before it publishes the run list; the list word carries this scan's epoch): one
+  // launch fewer, ~4.5 us of every such scan
+  p.epoch = ++c->scan_epoch;
+  const bool fold_init = !no_run && !chunked && !p.hash_out && LDB_FOLD_INIT;
+  if (!fold_init) hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, s, p.ctr, p.dyn, no_run ? 0ull : ~0ull);
   if (!no_run) {
     auto launch = [&](uint64_t lo, uint64_t hi) {
       const int ug = uniform_grid(c, hi - lo);
