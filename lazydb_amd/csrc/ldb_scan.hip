@@ -433,7 +433,9 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // scan: grid.y = file, its Pipe from the device array pb (enqueue_scan_batch).
 #define LDB_PIPE_SELECT const Pipe p = kB ? pb[blockIdx.y] : p0
 
-// Header probes (the unpublished path only). The first header mismatch of a run past its entry 1: the
+// Header probes of a one-run launch (chunked, batched or hashed scans; every workgroup probes, 64 probes
+// in round 0: the device path's several runs use uni_search below, one workgroup). The first header
+// mismatch of a run past its entry 1: the
 // smallest e in (1, nc - 1) whose header bytes or IOController bounds differ from the memo
 // (uni_header_ok), where candidate nc - 1 lies past the file's last whole entry and always fails. Rounds
 // of one probe per thread: the smallest failing probe bounds it from above, the largest passing probe
