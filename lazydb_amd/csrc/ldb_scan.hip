@@ -555,7 +555,8 @@ __device__ __forceinline__ void uni_build_comb(const Pipe& p, const UniGeo& g, u
 // decoded through readlane by one wave; the slicing (uni_geometry: a table load and two multmodp) is
 // left to the verifying workgroups, one wave per run.
 #ifndef LDB_FOLD_INIT
-#define LDB_FOLD_INIT 0   // 1: k_uniform<false, false> sets the control words itself (no k_init launch)
+#define LDB_FOLD_INIT 1   // k_uniform<false, false> sets the control words itself (no k_init launch): config 1
+                          // pipeline 0.150 -> 0.145 ms, config 4 neutral (profiles/r04_fold_init_ab.txt); 0 restores k_init
 #endif
 #ifndef LDB_UNI_SPIN
 #define LDB_UNI_SPIN 4   // s_sleep between polls of dyn[6] (x 64 cycles)
