@@ -733,9 +733,9 @@ __device__ __forceinline__ bool uni_probe16(const Pipe& p, const UniMemo& m, uin
 }
 
 // Run q's end M: the smallest candidate in (lo, nc - 1) whose header mismatches (as uni_boundary), by
-// rounds of probes over the whole workgroup. Round 0: 128 probes at lo + 1 .. lo + 128, then 128 spaced
-// geometrically to nc - 1, so a short run ends exactly in one round and a long one is bracketed to ~7 %;
-// later rounds probe every candidate of the bracket (<= blockDim of them) or spread evenly over it. The
+// rounds of probes over the whole workgroup. Round 0: 128 probes at lo + 1 .. lo + 128, then kUniR0 - 128
+// spaced geometrically to nc - 1, so a short run ends exactly in one round and a long one is bracketed to
+// ~7 % (128 of them) or ~1 % (896); later rounds probe every candidate of the bracket (<= blockDim of them) or spread evenly over it. The
 // probes of a wave are in increasing order, so its smallest failing and largest passing probe are one
 // ballot each (one LDS atomic per wave, not per lane). The probe that sets the final M leaves its 48
 // header bytes in stash[0..12) (stash[12] = x & 3): the next run's entry 0 without another load.
@@ -745,6 +745,12 @@ __device__ __forceinline__ bool uni_probe16(const Pipe& p, const UniMemo& m, uin
 // and returns true with hi = M, or, when `stop_wide` and round 0 left a bracket of more than blockDim
 // candidates (two rounds more), false after round 0 with the bracket in (lo, hi). `first`: round 0 is the
 // dense + geometric one (a continuation probes the bracket only).
+#ifndef LDB_UNI_R0
+#define LDB_UNI_R0 256   // threads probing in round 0: 128 dense, the rest geometric. Measured (config 1
+                         // k_uniform, 3 alternating reps, profiles/r04_uni_r0_ab.txt): 256 0.119 ms, 512
+                         // 0.122, 1024 0.139 -- fewer rounds, but each round waits on more scattered loads
+#endif
+constexpr uint32_t kUniR0 = LDB_UNI_R0;
 __device__ bool uni_search(const Pipe& p, const UniRun& q, uint64_t& lo, uint64_t& hi, uint32_t* stash, bool first,
                            bool stop_wide) {
   // a round's smallest failing and largest passing probe: two slots, alternating by round, so the next
@@ -765,10 +771,11 @@ __device__ bool uni_search(const Pipe& p, const UniRun& q, uint64_t& lo, uint64_
     const uint64_t w = hi - lo - 1;   // candidates strictly between
     uint64_t e = 0;
     if (rz) {
+      const uint32_t ng = (kUniR0 < nt ? kUniR0 : nt) - 128;   // geometric probes
       if (t < 128) {
         e = lo + 1 + t;
-      } else if (t < 256) {
-        const float a = fmaxf(0.0f, __logf((float)w / 128.0f) * (1.0f / 128.0f));
+      } else if (t < 128 + ng) {
+        const float a = fmaxf(0.0f, __logf((float)w / 128.0f) / (float)ng);
         e = lo + (uint64_t)(128.0f * __expf(a * (float)(t - 127)));
       }
     } else {
