@@ -1650,7 +1650,8 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   if (scan_done(p)) return;   // the run prefix ended on the chain's terminal (uni_finish)
-  // ctr[] was zeroed by k_init, which opens every pipeline (enqueue_scan); the terminal words start
+  // ctr[] was zeroed by k_init, which opens every pipeline (enqueue_scan), or on a run-prefix scan by
+  // k_uniform's workgroup 0 (LDB_FOLD_INIT); the terminal words start
   // at "none" (read only by the later kernels, stream-ordered after this one)
   if (blockIdx.x == 0 && threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
   {   // a workgroup whose waves have no region (the run prefix took them) leaves before the table copy
