@@ -880,6 +880,9 @@ __device__ void uni_discover(const Pipe& p, UniRuns& ru) {
     if (threadIdx.x == 0) {
       s_f[r] = brk ? M : ~0ull;
       if (brk) q.nc = M;
+      // (Measured and rejected: these two stores deferred to the final publication, sparing the next
+      // barrier their drain -- config 1 k_uniform 0.119 -> 0.124 ms, profiles/r04_defer_f_ab.txt: M must
+      // reach the verifiers at once, or they verify past it.)
       if (wide) {   // already published: its F may be lower by now (a verified failure)
         atomicMin((unsigned long long*)uni_fword(p, r), (unsigned long long)M);
         uni_recs(p)[r].nc = q.nc;
