@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define LDB_ABI_VERSION 2
+#define LDB_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------
  * Normal terminations of the replay loop (index.go:86-88 `break`) are > 0;
@@ -106,6 +106,8 @@ typedef struct ldb_scan_result {
                             repair's sources; 0 on well-formed logs) */
   uint64_t n_run;        /* diagnostics: leading entries verified as one run of equal-sized entries
                             (k_uniform); they are tuples [0, n_run) */
+  uint64_t n_sweep;      /* diagnostics (ABI 3): the entries after them verified by the sweep tier
+                            (k_sweep: variable-length entries, ldb_sweep.h); tuples [n_run, n_run + n_sweep) */
 } ldb_scan_result;
 
 /* ---- context ---------------------------------------------------------------
@@ -142,6 +144,17 @@ int ldb_scan_file_dev(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len, uint32
  * Synchronous. This is what a cgo caller holding an mmap'd file uses. */
 int ldb_scan_file(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type,
                   int tuple_kind, void* h_out, uint64_t cap, ldb_scan_result* h_result);
+
+/* Host-memory scan in two calls, for callers that size their output exactly (ABI 3). The replay's
+ * ReadLogEntry loop (logfile/log_file.go:116, index.go:84-95) returns one tuple per entry; a caller
+ * that cannot bound the count beforehand would otherwise allocate len/10 + 1 tuples (4.8x the image for
+ * ldb_entry). ldb_scan_file_count scans like ldb_scan_file and keeps the tuples in the context's device
+ * staging; *h_result says how many there are (n_entries). ldb_scan_copy_out then copies
+ * min(n_entries, cap) of them into h_out and sets *n_copied. Synchronous. The tuples stay valid until
+ * the next scan call on the same context (copy_out returns LDB_ERR_ARG after one). */
+int ldb_scan_file_count(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type,
+                        int tuple_kind, ldb_scan_result* h_result);
+int ldb_scan_copy_out(ldb_ctx* ctx, void* h_out, uint64_t cap, uint64_t* n_copied);
 
 /* Page-lock a host range (e.g. an mmap'd log file, mmap/mmap_linux.go:14-20) for the lifetime of the
  * mapping, so ldb_scan_file's host-to-device copy runs as direct DMA at PCIe rate instead of through

@@ -28,7 +28,8 @@ ENTRY_TUPLE = np.dtype([("offset", "<u8"), ("expired_at", "<i8"), ("tx_id", "<u8
 class ScanResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("fid", C.c_uint32), ("n_entries", C.c_uint64), ("end_off", C.c_uint64),
                 ("n_repairs", C.c_uint32), ("n_regions", C.c_uint32),
-                ("n_fast", C.c_uint32), ("n_broken", C.c_uint32), ("n_run", C.c_uint64)]
+                ("n_fast", C.c_uint32), ("n_broken", C.c_uint32), ("n_run", C.c_uint64),
+                ("n_sweep", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -62,7 +63,7 @@ ROUTE_REC = np.dtype([("hash", "<u8"), ("seq", "<u4"), ("k_size", "<u4"), ("key_
 assert ROUTE_REC.itemsize == 24
 
 RESULT_BYTES = C.sizeof(ScanResult)
-assert RESULT_BYTES == 48
+assert RESULT_BYTES == 56
 
 _lib = None
 
@@ -89,6 +90,8 @@ def lib():
         L.ldb_scan_file_dev.argtypes = [vp, vp, u64, u32, i32, i32, vp, u64, vp, vp]
         L.ldb_scan_file_dev_serial.argtypes = [vp, vp, u64, u32, i32, i32, vp, u64, vp, vp]
         L.ldb_scan_file.argtypes = [vp, vp, u64, u32, i32, i32, vp, u64, C.POINTER(ScanResult)]
+        L.ldb_scan_file_count.argtypes = [vp, vp, u64, u32, i32, i32, C.POINTER(ScanResult)]
+        L.ldb_scan_copy_out.argtypes = [vp, vp, u64, C.POINTER(u64)]
         L.ldb_scan_files_dev.argtypes = [vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]
         L.ldb_kernel_timing.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)]
         L.ldb_kernel_timing_split.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -129,14 +132,15 @@ def lib():
             L.ldb_encode_entries_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u64, vp, u64, vp, u32,
                                                  C.POINTER(MergeResult), vp]
             L.ldb_encode_entries_dev.restype = i32
-        if L.ldb_abi_version() != 2:
+        if L.ldb_abi_version() != 3:
             raise LdbError("liblazydb_gpu ABI version mismatch")
         _lib = L
     return _lib
 
 
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
-           "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_files_dev",
+           "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_file_count", "ldb_scan_copy_out",
+           "ldb_scan_files_dev",
            "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_kernel_timing_split", "ldb_kernel_timing_fill",
            "ldb_read_ceiling", "ldb_merge_files_dev",
            "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_merge_repack_dev", "ldb_host_register", "ldb_host_unregister",

@@ -196,6 +196,11 @@ LDB_HD uint32_t field_value(uint32_t b, uint32_t n, bool* canon) {
 
 // The lean decode takes Go's whole varint range for ExpiredAt and TxID (up to 10 bytes each: a
 // snowflake TxID, tx.go:47-56, is a 9-10 byte varint), so Tx.Commit's entries stay on the lean path.
+// The decode itself over the header-window dwords w[0..8] (bytes [p, p + 36)) of the entry at image
+// offset `at` (the IOController bounds); o->X is relative: p + the entry size. The sweep tier
+// (ldb_sweep.h) calls it on dwords held in registers.
+LDB_HD bool decode_lean_w(const uint32_t* w, uint64_t at, uint32_t p, uint64_t len, int io, Lean* o);
+
 LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   const int a = p + kPre;
   const int q = a & ~3;
@@ -206,6 +211,10 @@ LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   uint32_t w[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) w[i] = funnel(d[i + 1], d[i], sh);
+  return decode_lean_w(w, v.R0 + (uint64_t)p, (uint32_t)p, v.len, v.io, o);
+}
+
+LDB_HD bool decode_lean_w(const uint32_t* w, uint64_t at, uint32_t p, uint64_t len, int io, Lean* o) {
   // terminator bits of window bytes 5..35 (bit i <-> byte 4 + i)
   const uint32_t M = msb4(w[1]) | (msb4(w[2]) << 4) | (msb4(w[3]) << 8) | (msb4(w[4]) << 12) | (msb4(w[5]) << 16) |
                      (msb4(w[6]) << 20) | (msb4(w[7]) << 24) | (msb4(w[8]) << 28);
@@ -231,10 +240,10 @@ LDB_HD bool decode_lean(const View& v, int p, Lean* o) {
   ok = ok && ck && cv && (uk & 1u) == 0u && uk >= 2u && (uv & 1u) == 0u;
   const uint32_t hs = 5 + e4;
   const uint32_t k = uk >> 1, vv = uv >> 1;
-  const uint32_t X = (uint32_t)p + hs + k + vv;
-  ok = ok && !read_eof(v.len, v.io, (int64_t)(v.R0 + (uint64_t)p + hs), k + vv);   // key/value read (log_file.go:130-139)
+  const uint32_t X = p + hs + k + vv;
+  ok = ok && !read_eof(len, io, (int64_t)(at + hs), k + vv);   // key/value read (log_file.go:130-139)
 #ifndef LDB_NO_WINCHK   // timing variant only (results invalid near the file end)
-  ok = ok && !read_eof(v.len, v.io, (int64_t)(v.R0 + (uint64_t)p), kMaxHeader);   // header window (log_file.go:117-122)
+  ok = ok && !read_eof(len, io, (int64_t)at, kMaxHeader);   // header window (log_file.go:117-122)
 #endif
   o->crc = w[0];
   o->stat = stat;

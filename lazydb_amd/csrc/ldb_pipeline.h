@@ -15,6 +15,9 @@
 
 namespace ldb {
 
+struct SwRun;
+struct SwCtl;
+
 struct Pipe {
   const uint8_t* img;
   uint64_t len;
@@ -42,6 +45,14 @@ struct Pipe {
   int kind;
   uint32_t epoch;             // this scan's number on its workspace (k_uniform's run-list word carries it)
   ldb_scan_result* result;
+  // the sweep tier (ldb_sweep.h; null where it does not run): per-window and per-group raw registers,
+  // its run records and control block, its global tables; its candidate slabs are the scratch tuples
+  uint32_t* swrw;
+  uint32_t* swrg;
+  SwRun* swrun;
+  SwCtl* swctl;
+  const uint32_t* swt;
+  uint64_t scratch_bytes;
 };
 
 constexpr int kBlkRegions = 256;   // regions per k_combine / k_compact workgroup
@@ -409,3 +420,5 @@ LDB_HD uint32_t walk_source(const Pipe& p, int64_t src, Rd rd, Claim claim, Run 
 }
 
 }  // namespace ldb
+
+#include "ldb_sweep.h"

@@ -1438,6 +1438,7 @@ __device__ __forceinline__ void uni_finish(const Pipe& p, const UniRuns& ru) {
   res.n_fast = 0;
   res.n_broken = 0;
   res.n_run = K;
+  res.n_sweep = 0;
   *p.result = res;
   p.dyn[3] = kUniDone;
 }
@@ -1486,8 +1487,15 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
   // taken the run list, which workgroup 0 publishes after this), x0 unset
   if (kMulti && LDB_FOLD_INIT && blockIdx.x == 0 && threadIdx.x < 8) {
     p.ctr[threadIdx.x] = 0u;
-    if (threadIdx.x == 3 || threadIdx.x == 4) p.dyn[threadIdx.x] = 0;
+    if (threadIdx.x == 3 || threadIdx.x == 4 || threadIdx.x == 7) p.dyn[threadIdx.x] = 0;
     if (threadIdx.x == 5) p.dyn[5] = ~0ull;
+    if (p.swctl && threadIdx.x == 0) {   // the sweep tier's control words (k_sweep, k_sweep_fin follow)
+      p.swctl->fail = ~0ull;
+      p.swctl->stop = ~0ull;
+      p.swctl->done0 = 0;
+      p.swctl->done1 = 0;
+      p.swctl->state = 0;
+    }
   }
   // (workgroup 0 of a kMulti launch finds the runs first: its LP2 block afterwards, off that chain)
   if (!kMulti || blockIdx.x != 0) lp2_build(lp2, p.gtab);
@@ -2177,7 +2185,8 @@ __device__ void serial_walk(const Pipe& p) {
   res.n_regions = (uint32_t)p.nreg;
   res.n_fast = 0;
   res.n_broken = 0;
-  res.n_run = run_k(p);
+  res.n_run = run_k(p) - p.dyn[7];
+  res.n_sweep = p.dyn[7];
   *p.result = res;
 }
 template <bool kB>
@@ -2227,7 +2236,8 @@ __device__ __forceinline__ void compact_body(const Pipe& p) {
       res.n_regions = 0;
       res.n_fast = 0;
       res.n_broken = 0;
-      res.n_run = K;
+      res.n_run = K - p.dyn[7];
+      res.n_sweep = p.dyn[7];
       if (K > p.cap) res.status = LDB_ERR_CAPACITY;
       *p.result = res;
     }
@@ -2285,7 +2295,8 @@ __device__ __forceinline__ void compact_body(const Pipe& p) {
     res.n_regions = (uint32_t)(p.nreg - rf);
     res.n_fast = p.ctr[3];
     res.n_broken = p.ctr[7];
-    res.n_run = K;
+    res.n_run = K - p.dyn[7];
+    res.n_sweep = p.dyn[7];
     if (n > p.cap) res.status = LDB_ERR_CAPACITY;
     if (p.ctr[5]) res.status = LDB_ERR_INTERNAL;   // a device-side index guard fired (never expected)
     if (p.ctr[1]) res.status = kOverflow;  // k_serial redoes the scan
@@ -2333,6 +2344,8 @@ __global__ __launch_bounds__(256) void k_read_reduce(const uint4* __restrict__ p
   if ((threadIdx.x & 63) == 0) atomicXor(&sink[blockIdx.x], acc);
 }
 
+#include "ldb_sweep_kern.h"
+
 size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
 size_t repair_lds_bytes() { return kRepWaves * (sizeof(WaveLds) + kBuf); }
 static_assert(kRepWaves * (sizeof(WaveLds) + kBuf) + kTabBytes + 64 <= 160 * 1024, "k_repair: LDS per workgroup");
@@ -2346,6 +2359,7 @@ struct ldb_ctx {
   uint32_t* d_tab = nullptr;   // kTabWords
   uint32_t* d_xw = nullptr;    // kW + 1
   uint32_t* d_gsh = nullptr;   // kGsWords register-shift tables (k_combine)
+  uint32_t* d_swt = nullptr;   // kSwTabWords: the sweep tier's shift and slicing-by-16 tables (ldb_sweep.h)
   uint8_t* ws = nullptr;       // workspace
   uint64_t ws_bytes = 0;
   // Workspace fence: the event recorded after the last pipeline enqueued on this context, and the
@@ -2388,6 +2402,9 @@ struct ldb_ctx {
   // host ranges page-locked through ldb_host_register: ldb_scan_file reads or writes a host buffer
   // in place only when one of them covers it whole (the device mapping alone says nothing of its size)
   std::vector<std::pair<uintptr_t, uint64_t>> regs;
+  // ldb_scan_file_count's tuples, left in h_out for ldb_scan_copy_out (any other scan call clears it)
+  bool ret_valid = false;
+  uint64_t ret_n = 0, ret_tsz = 0;
   bool registered(const void* p, uint64_t n) const {
     const uintptr_t a = (uintptr_t)p;
     for (const auto& r : regs)
@@ -2423,7 +2440,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_dyn, o_uni, o_blk, total;
+  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_dyn, o_uni, o_blk, o_swrw, o_swrg, o_swrun, o_swctl, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -2447,6 +2464,12 @@ WsLayout layout(uint64_t len) {
   L.o_rs = take(sizeof(RegionSum) * L.nreg);
   L.o_fail = take(8 * (L.nreg + 1) + 64);   // fail flags + walker claims (ldb_pipeline.h fail_flags)
   L.o_scratch = take(sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg);
+  // the sweep tier (ldb_sweep.h): a register per 256-B window and per 16 windows (the image's batches,
+  // rounded up, plus one), its run records and control block; its slabs are the scratch tuples above
+  L.o_swrw = take(4 * ((len + kSwBatch) / kSwW + 1));
+  L.o_swrg = take(4 * ((len + kSwBatch) / (kSwW * kSwG) + 1));
+  L.o_swrun = take(sizeof(SwRun) * (uint64_t)kSwMaxRuns);
+  L.o_swctl = take(sizeof(SwCtl));
   L.total = o;
   return L;
 }
@@ -2493,6 +2516,12 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.cap = cap;
   p.kind = kind;
   p.result = res;
+  p.swrw = reinterpret_cast<uint32_t*>(w + L.o_swrw);
+  p.swrg = reinterpret_cast<uint32_t*>(w + L.o_swrg);
+  p.swrun = reinterpret_cast<SwRun*>(w + L.o_swrun);
+  p.swctl = reinterpret_cast<SwCtl*>(w + L.o_swctl);
+  p.swt = c->d_swt;
+  p.scratch_bytes = sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg;
   return p;
 }
 
@@ -2580,6 +2609,17 @@ int fill_grid(const ldb_ctx* c, uint64_t bytes) {
   return std::max(1, (int)std::min<uint64_t>(bytes / 16 / kFillThreads + 1, (uint64_t)c->n_cu * 2));
 }
 
+// k_sweep: one workgroup of kSwWaves per CU (the LP2 block), fewer for a file of few batches
+int sweep_grid(const ldb_ctx* c, uint64_t len) {
+  const uint64_t batches = len / kSwBatch + 2;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((batches + kSwWaves - 1) / kSwWaves, (uint64_t)c->n_cu));
+}
+// LDB_SWEEP=0 turns the sweep tier off (A/B: the region pipeline from the run prefix's end, rounds 1-4)
+bool sweep_enabled() {
+  static const bool on = getenv("LDB_SWEEP") == nullptr || atoi(getenv("LDB_SWEEP")) != 0;
+  return on;
+}
+
 // An image that is still being copied in: bytes [0, avail[i]) are in place once ev[i] has fired
 // (avail ascending, the last = len). The run prefix then verifies its candidates chunk by chunk,
 // each launch waiting only for its chunk, so it overlaps the copy; the region pipeline waits for all.
@@ -2660,6 +2700,10 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
     } else {
       launch(0, len);   // its workgroups also write the runs' INDEX tuples (uni_post_fill)
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+      if (fold_init && sweep_enabled()) {   // the sweep tier from the run prefix's end (ldb_sweep.h)
+        hipLaunchKernelGGL(k_sweep, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p);
+        hipLaunchKernelGGL(k_sweep_fin, dim3(4 * c->n_cu), dim3(64 * kSwFinWaves), 0, s, p);
+      }
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
   } else if (ev) {
@@ -2877,18 +2921,20 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
   c->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-  std::vector<uint32_t> tab(kTabWords), xw(kW + 1), gsh(kGsWords);
+  std::vector<uint32_t> tab(kTabWords), xw(kW + 1), gsh(kGsWords), swt(kSwTabWords);
   build_tables(tab.data());
   for (int n = 0; n <= kW; ++n) xw[n] = x8n_modp((uint64_t)n);
   build_gshift(gsh.data());
+  build_swtab(swt.data());
   if (hipMalloc(&c->d_tab, tab.size() * 4) != hipSuccess || hipMalloc(&c->d_xw, xw.size() * 4) != hipSuccess ||
-      hipMalloc(&c->d_gsh, gsh.size() * 4) != hipSuccess) {
+      hipMalloc(&c->d_gsh, gsh.size() * 4) != hipSuccess || hipMalloc(&c->d_swt, swt.size() * 4) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_NOMEM;
   }
   if (hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_xw, xw.data(), xw.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_gsh, gsh.data(), gsh.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(c->d_gsh, gsh.data(), gsh.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_swt, swt.data(), swt.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }
@@ -2914,6 +2960,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->d_xw) (void)hipFree(c->d_xw);
   if (c->d_gsh) (void)hipFree(c->d_gsh);
+  if (c->d_swt) (void)hipFree(c->d_swt);
   if (c->ws) (void)hipFree(c->ws);
   if (c->h_img) (void)hipFree(c->h_img);
   if (c->h_out) (void)hipFree(c->h_out);
@@ -2946,6 +2993,7 @@ int ldb_ctx_reserve(ldb_ctx* c, uint64_t max_len) {
 int ldb_scan_file_dev(ldb_ctx* c, const uint8_t* d_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
                       void* d_out, uint64_t cap, ldb_scan_result* d_result, void* stream) {
   if (!c) return LDB_ERR_ARG;
+  c->ret_valid = false;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
   return enqueue_scan(c, d_image, len, fid, io_type, tuple_kind, d_out, cap, d_result, (hipStream_t)stream, false);
 }
@@ -3003,9 +3051,12 @@ int ldb_host_unregister(ldb_ctx* c, const void* h_ptr) {
   return LDB_OK;
 }
 
-int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
-                  void* h_out, uint64_t cap, ldb_scan_result* h_result) {
-  if (!c || !h_result || (len && !h_image) || (cap && !h_out)) return LDB_ERR_ARG;
+// ldb_scan_file's body; retain: the count half of ldb_scan_file_count / ldb_scan_copy_out (no h_out: the
+// tuples stay in the context's device staging for the copy-out, cap tuples of it)
+static int scan_file_impl(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
+                          void* h_out, uint64_t cap, ldb_scan_result* h_result, bool retain) {
+  if (!c || !h_result || (len && !h_image) || (cap && !h_out && !retain)) return LDB_ERR_ARG;
+  c->ret_valid = false;
   if (tuple_kind != LDB_TUPLE_INDEX && tuple_kind != LDB_TUPLE_ENTRY) return LDB_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
   const size_t tsz = tuple_kind == LDB_TUPLE_ENTRY ? sizeof(ldb_entry) : sizeof(ldb_index_tuple);
@@ -3109,10 +3160,45 @@ int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid
       hipStreamSynchronize(s) != hipSuccess)
     return LDB_ERR_HIP;
   const uint64_t n = out_mapped ? 0 : std::min<uint64_t>(res.n_entries, cap);
+  if (retain) {   // the tuples stay on the device for ldb_scan_copy_out
+    c->ret_valid = true;
+    c->ret_n = n;
+    c->ret_tsz = tsz;
+    *h_result = res;
+    return LDB_OK;
+  }
   if (n && (hipMemcpyAsync(h_out, c->h_out, n * tsz, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess))
     return LDB_ERR_HIP;
   *h_result = res;
+  return LDB_OK;
+}
+
+int ldb_scan_file(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
+                  void* h_out, uint64_t cap, ldb_scan_result* h_result) {
+  return scan_file_impl(c, h_image, len, fid, io_type, tuple_kind, h_out, cap, h_result, false);
+}
+
+// Count, then copy: the scan's tuples stay in the context's device staging (room for one per 10 bytes of
+// image: an entry's header alone is >= 10 bytes on any log LazyDB writes; a log with more entries is
+// scanned again with room for exactly n_entries), and ldb_scan_copy_out moves exactly the n the caller
+// sized its array for. A Go caller's output slice is then allocated once at its final size.
+int ldb_scan_file_count(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type, int tuple_kind,
+                        ldb_scan_result* h_result) {
+  int rc = scan_file_impl(c, h_image, len, fid, io_type, tuple_kind, nullptr, len / 10 + 1, h_result, true);
+  if (rc == LDB_OK && h_result->status == LDB_ERR_CAPACITY)
+    rc = scan_file_impl(c, h_image, len, fid, io_type, tuple_kind, nullptr, h_result->n_entries, h_result, true);
+  return rc;
+}
+
+int ldb_scan_copy_out(ldb_ctx* c, void* h_out, uint64_t cap, uint64_t* n_copied) {
+  if (!c || !c->ret_valid || (cap && !h_out) || !n_copied) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  const uint64_t n = std::min<uint64_t>(c->ret_n, cap);
+  if (n && (hipMemcpyAsync(h_out, c->h_out, n * c->ret_tsz, hipMemcpyDeviceToHost, c->h_stream) != hipSuccess ||
+            hipStreamSynchronize(c->h_stream) != hipSuccess))
+    return LDB_ERR_HIP;
+  *n_copied = n;
   return LDB_OK;
 }
 

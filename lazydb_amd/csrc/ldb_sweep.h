@@ -1,0 +1,96 @@
+// ldb_sweep.h — the sweep tier of the log scan (round 5): variable-length entries at the HBM roofline.
+//
+// The replay (index.go:84-95) is a chain: entry i+1 starts where entry i ends, and each entry's
+// CRC-32 covers its bytes [off+4, off+size) (logfile/log_entry.go:110-121, log_file.go:141-143). The run
+// prefix (k_uniform) verifies runs of equal-sized entries; the region pipeline (k_scan_main ...) walks
+// anything. The sweep sits between them for logs of long variable-length entries (BASELINE config 3:
+// Zipf values of 16 B - 64 KiB, 5.2 KB per entry on average), where the region pipeline spends its time
+// on per-region machinery around one or two entry starts. It splits the work by what it depends on:
+//
+//   k_sweep      one streaming pass over the image, 16-B rows straight into registers (the run
+//                prefix's load pattern): every lane CRC-32s its 256-B window from register 0 on the
+//                lane-private LP2 tables (RW: one raw register per window, RG: per 16 windows by a DPP
+//                tree), and tests every byte position as a header candidate by its first bytes
+//                (Status <= 2, ExpiredAt >= 0, crc != 0: SWAR masks). Candidates are decoded 64 at a
+//                time (decode_lean_w, the region pipeline's Go-exact decode of canonical headers, with
+//                the IOController bounds) into the wave's slab: index tuples in file order.
+//                Each wave owns a contiguous run of the image and then walks its slab: from the run's
+//                first candidate (run 0: the chain's entry point x_s), each entry's end must be the
+//                next candidate. The last workgroup checks the links between runs (a run's exit must
+//                be the next run's first entry) and fixes where the tier ends: at the first broken
+//                link, declined run (too many candidates, slab full) or chain end.
+//   k_sweep_fin  one lane per chain entry: its CRC from the window registers (a Horner fold over the
+//                RW / RG registers between its span's ends, the partial windows at both ends by
+//                slicing-by-16 over at most 255 bytes each, two GF(2) multiplies), the tuple written at
+//                its index. The last workgroup writes the result when the tier ends on a terminal
+//                (io.EOF, ErrLogEndOfFile, a failed CRC) or hands the rest to the region pipeline: K
+//                entries and position x, as the run prefix does (dyn[0], dyn[5]).
+//
+// Results are the serial scan's for every input: a candidate is decoded exactly as decodeHeader
+// would, a chain entry is accepted only when its header, bounds and CRC check, and wherever the tier
+// cannot decide (a non-canonical header, a speculated run start that is off the chain) it stops and the
+// region pipeline continues from that position. Speculation (a run's first candidate) only changes how
+// much of the file the tier takes.
+#pragma once
+
+namespace ldb {
+
+constexpr uint32_t kSwW = 256;                 // window: one lane's bytes per batch
+constexpr uint64_t kSwBatch = 64ull * kSwW;    // a wave's batch (16 KiB)
+constexpr uint32_t kSwG = 16;                  // windows per group register (4 KiB)
+constexpr int kSwWaves = 16;                   // waves per k_sweep workgroup (1 per CU: LDS)
+constexpr uint32_t kSwList = 512;              // candidate positions awaiting decode, per wave (LDS)
+constexpr uint32_t kSwTrust = 4;               // a speculated chain this long is kept when it ends in its run
+constexpr uint32_t kSwMaxRuns = 4096;
+constexpr uint32_t kSwDead = 1u, kSwDecl = 2u;
+constexpr uint64_t kSwPosMask = (1ull << 60) - 1;   // slab records: index tuple, walk tag in pos bits 60-63
+constexpr int kSwFinWaves = 4;
+
+// global tables (ldb_ctx::d_swt): register shift by 256 << i bytes (i = 0..4: 256 ... 4096), then the
+// slicing-by-16 tables (S[k][b]: the raw register after byte b and k zero bytes)
+constexpr int kSwShTabs = 5;
+constexpr uint32_t kSwSl16Off = kSwShTabs * 1024;
+constexpr uint32_t kSwTabWords = kSwSl16Off + 16 * 256;
+
+struct alignas(16) SwRun {
+  uint64_t E;       // the run's first chain entry as walked (run 0: x_s), ~0 none
+  uint64_t X;       // its exit (first chain position >= hi), or (kSwDead) where the chain ended
+  uint64_t n;       // entries on that chain
+  uint32_t flags;   // kSwDead | kSwDecl | walk tag << 8
+  uint32_t ncand;   // slab records
+  uint64_t lo, hi;  // candidate positions [lo, hi)
+  uint64_t base;    // index of its first entry among the tier's (link resolution)
+  uint64_t pad;
+};
+static_assert(sizeof(SwRun) == 64, "run records are 64 B");
+
+struct alignas(16) SwCtl {
+  uint64_t xs, ks;    // where the tier starts (chain_x0 after the run prefix) and that entry's index
+  uint64_t xe, ke;    // where it ends (link resolution)
+  uint64_t ncov;      // runs whose chain entries are the tier's
+  uint64_t fail;      // smallest tier index of an entry whose CRC failed (k_sweep_fin), ~0
+  uint64_t stop;      // smallest run known to end the tier (later runs stop streaming), ~0
+  uint64_t done0, done1;   // workgroups finished (k_sweep, k_sweep_fin): the last one resolves
+  uint64_t state;     // 1 once k_sweep resolved the links; k_sweep_fin's last workgroup clears it
+  uint64_t nrun;      // runs of this scan (each run's slab: scratch_bytes / 16 / nrun records)
+  uint64_t pad[5];
+};
+static_assert(sizeof(SwCtl) == 128, "sweep control block");
+
+inline void build_swtab(uint32_t* t) {
+  for (int i = 0; i < kSwShTabs; ++i) {
+    const uint32_t xn = x8n_modp(256ull << i);
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b) t[i * 1024 + q * 256 + b] = multmodp(xn, b << (8 * q));
+  }
+  uint32_t* s = t + kSwSl16Off;
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
+    s[b] = c;
+  }
+  for (int k = 1; k < 16; ++k)
+    for (uint32_t b = 0; b < 256; ++b) s[k * 256 + b] = (s[(k - 1) * 256 + b] >> 8) ^ s[s[(k - 1) * 256 + b] & 0xFFu];
+}
+
+}  // namespace ldb

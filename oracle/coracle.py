@@ -18,7 +18,8 @@ _SO = os.path.join(_HERE, "_build", "libldb_oracle.so")
 class ScanResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("fid", C.c_uint32), ("n_entries", C.c_uint64), ("end_off", C.c_uint64),
                 ("n_repairs", C.c_uint32), ("n_regions", C.c_uint32),
-                ("n_fast", C.c_uint32), ("reserved_", C.c_uint32), ("n_run", C.c_uint64)]
+                ("n_fast", C.c_uint32), ("reserved_", C.c_uint32), ("n_run", C.c_uint64),
+                ("n_sweep", C.c_uint64)]
 
 
 class Header(C.Structure):

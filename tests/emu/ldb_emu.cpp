@@ -263,6 +263,7 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
   p.scratch = scratch.data(); p.fail_src = fail.data(); p.ctr = ctr.data(); p.tpos = tpos.data();
   p.blk = blk.data(); p.out = out; p.cap = cap; p.kind = LDB_TUPLE_INDEX; p.result = res; p.dyn = dyn.data();
   res->n_run = 0;
+  res->n_sweep = 0;
   if (len < (uint64_t)kMaxHeader) {
     // the kernels route tiny images to k_serial; mirror it
     res->status = LDB_EOF_WINDOW; res->fid = fid; res->n_entries = 0; res->end_off = 0; res->n_repairs = 0;
@@ -272,6 +273,7 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
   if (use_run) emu_uniform(emu, img, len, io, out, cap, dyn.data());
   const uint64_t rf = first_region(p), K = run_k(p), x0 = chain_x0(p);
   res->n_run = K;
+  res->n_sweep = 0;
   if (rf >= nreg) {   // k_compact: io.EOF right after the run
     res->status = K > cap ? LDB_ERR_CAPACITY : LDB_EOF_WINDOW; res->fid = fid; res->n_entries = K; res->end_off = x0;
     res->n_repairs = 0; res->n_regions = 0;

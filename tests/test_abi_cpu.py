@@ -27,13 +27,13 @@ def test_library_exports_header_symbols():
     for sym in declared:
         assert hasattr(L, sym), sym
     assert set(N.EXPORTS) == declared
-    assert L.ldb_abi_version() == 2
+    assert L.ldb_abi_version() == 3
     assert N.status_str(-1) == "invalid crc"
 
 
 def test_struct_layouts_match_header():
     from lazydb_amd import _native as N
-    assert C.sizeof(N.ScanResult) == 48
+    assert C.sizeof(N.ScanResult) == 56
     assert N.INDEX_TUPLE.itemsize == 16 and N.ENTRY_TUPLE.itemsize == 48
     assert N.INDEX_TUPLE == coracle.INDEX_TUPLE and N.ENTRY_TUPLE == coracle.ENTRY_TUPLE
 
