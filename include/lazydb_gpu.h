@@ -192,6 +192,10 @@ int ldb_kernel_timing_split(ldb_ctx* ctx, int enable, double* avg_run_ms, double
  * k_uniform verified them) over the same launches: avg_fill_ms. Query only; the reset is
  * ldb_kernel_timing's / ldb_kernel_timing_split's. */
 int ldb_kernel_timing_fill(ldb_ctx* ctx, double* avg_fill_ms);
+/* The sweep tier (variable-length entries after the run prefix, ABI 3) over the same launches: its
+ * streaming kernel (k_sweep: window CRCs, candidate decode, run walks and links) and its verify/emit
+ * kernel (k_sweep_fin), each averaged over the timed scans (0 where the tier did not run). */
+int ldb_kernel_timing_sweep(ldb_ctx* ctx, double* avg_sweep_ms, double* avg_fin_ms);
 
 /* Practical HBM-read ceiling for the roofline report: a read-only XOR
  * reduction over the device image d_image[0, len), 16-B loads, `iters` timed launches after one

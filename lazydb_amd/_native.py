@@ -100,6 +100,9 @@ def lib():
         if hasattr(L, "ldb_kernel_timing_fill"):   # absent from A/B builds of older revisions
             L.ldb_kernel_timing_fill.argtypes = [vp, C.POINTER(C.c_double)]
             L.ldb_kernel_timing_fill.restype = i32
+        if hasattr(L, "ldb_kernel_timing_sweep"):
+            L.ldb_kernel_timing_sweep.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+            L.ldb_kernel_timing_sweep.restype = i32
         for fn in ("ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve", "ldb_scan_file_dev",
                    "ldb_scan_file_dev_serial", "ldb_scan_file", "ldb_scan_files_dev", "ldb_kernel_timing"):
             getattr(L, fn).restype = i32
@@ -142,6 +145,7 @@ EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destr
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_file_count", "ldb_scan_copy_out",
            "ldb_scan_files_dev",
            "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_kernel_timing_split", "ldb_kernel_timing_fill",
+           "ldb_kernel_timing_sweep",
            "ldb_read_ceiling", "ldb_merge_files_dev",
            "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_merge_repack_dev", "ldb_host_register", "ldb_host_unregister",
            "ldb_merge_route_dev", "ldb_merge_resolve_dev", "ldb_merge_apply_dev")

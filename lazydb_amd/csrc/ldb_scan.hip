@@ -2372,7 +2372,9 @@ struct ldb_ctx {
   uint32_t scan_epoch = 0;   // device scans enqueued on this context (Pipe::epoch)
   // kernel timing: one event triple per timed launch, recorded without host synchronisation and
   // resolved when the timing is queried (or when the pool is full)
-  struct EvTriple { hipEvent_t e0, eu, ef, e1, e2; };   // start, after k_uniform, after its fill, after k_scan_main, end
+  // start, after k_uniform, after its fill (device path: after the sweep tier), after k_scan_main, end; es:
+  // between k_sweep and k_sweep_fin (recorded only where the sweep tier runs, else = ef)
+  struct EvTriple { hipEvent_t e0, eu, ef, e1, e2, es; };
   std::vector<EvTriple> evs;
   size_t ev_used = 0;
   bool timing = false;
@@ -2390,7 +2392,7 @@ struct ldb_ctx {
   int n_cp = 0;
   hipStream_t cp[kMaxCp] = {};
   std::vector<hipEvent_t> chunk_ev;
-  double t_run = 0, t_fill = 0, t_main = 0, t_total = 0;
+  double t_run = 0, t_fill = 0, t_main = 0, t_total = 0, t_sweep = 0;
   uint64_t t_n = 0;
   // batched scans (enqueue_scan_batch): page-locked staging of the per-file Pipes, reused once the
   // copy of the previous batch has completed (pipes_ev)
@@ -2428,6 +2430,9 @@ static int resolve_timing(ldb_ctx* c) {
       return LDB_ERR_HIP;
     c->t_run += u;
     c->t_fill += f;
+    float sw = 0;
+    if (hipEventElapsedTime(&sw, t.eu, t.es) != hipSuccess) return LDB_ERR_HIP;
+    c->t_sweep += sw;
     c->t_main += a;
     c->t_total += b;
     c->t_n += 1;
@@ -2561,6 +2566,7 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
       LDB_HIP(hipEventCreate(&t.e0));
       LDB_HIP(hipEventCreate(&t.eu));
       LDB_HIP(hipEventCreate(&t.ef));
+      LDB_HIP(hipEventCreate(&t.es));
       LDB_HIP(hipEventCreate(&t.e1));
       LDB_HIP(hipEventCreate(&t.e2));
       c->evs.push_back(t);
@@ -2696,18 +2702,23 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
         lo = hi;
       }
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+      if (ev) LDB_HIP(hipEventRecord(ev->es, s));
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     } else {
       launch(0, len);   // its workgroups also write the runs' INDEX tuples (uni_post_fill)
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
       if (fold_init && sweep_enabled()) {   // the sweep tier from the run prefix's end (ldb_sweep.h)
         hipLaunchKernelGGL(k_sweep, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p);
+        if (ev) LDB_HIP(hipEventRecord(ev->es, s));
         hipLaunchKernelGGL(k_sweep_fin, dim3(4 * c->n_cu), dim3(64 * kSwFinWaves), 0, s, p);
+      } else if (ev) {
+        LDB_HIP(hipEventRecord(ev->es, s));
       }
       if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
   } else if (ev) {
     LDB_HIP(hipEventRecord(ev->eu, s));
+    LDB_HIP(hipEventRecord(ev->es, s));
     LDB_HIP(hipEventRecord(ev->ef, s));
   }
   hipLaunchKernelGGL(k_scan_main<false>, dim3(scan_main_grid(c, L.nreg)), dim3(64 * kWPB), main_lds_bytes(), s, p, nullptr);
@@ -2835,6 +2846,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+  if (ev) LDB_HIP(hipEventRecord(ev->es, s));
   if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
   hipLaunchKernelGGL(k_scan_main<true>, dim3(mg, n), dim3(64 * kWPB), main_lds_bytes(), s, p0, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
@@ -2977,6 +2989,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
     (void)hipEventDestroy(t.e0);
     (void)hipEventDestroy(t.eu);
     (void)hipEventDestroy(t.ef);
+    (void)hipEventDestroy(t.es);
     (void)hipEventDestroy(t.e1);
     (void)hipEventDestroy(t.e2);
   }
@@ -3211,6 +3224,14 @@ int ldb_debug_stamps(uint64_t* out, int reset) {
   }
   return LDB_OK;
 }
+int ldb_debug_swstamps(uint64_t* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_swstamps), 8 * 16) != hipSuccess) return LDB_ERR_HIP;
+  if (reset) {
+    uint64_t z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_swstamps), z, 8 * 16) != hipSuccess) return LDB_ERR_HIP;
+  }
+  return LDB_OK;
+}
 int ldb_debug_ustamps(uint64_t* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ustamps), 8 * kUniStampSlots) != hipSuccess) return LDB_ERR_HIP;
   if (reset) {
@@ -3262,7 +3283,7 @@ int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_t
   if (n) *n = c->t_n;
   if (enable >= 0) {
     c->timing = enable != 0;
-    c->t_run = c->t_fill = c->t_main = c->t_total = 0;
+    c->t_run = c->t_fill = c->t_main = c->t_total = c->t_sweep = 0;
     c->t_n = 0;
   }
   return LDB_OK;
@@ -3284,6 +3305,15 @@ int ldb_kernel_timing_fill(ldb_ctx* c, double* avg_fill_ms) {
   const int rc = resolve_timing(c);
   if (rc != LDB_OK) return rc;
   *avg_fill_ms = c->t_n ? c->t_fill / c->t_n : 0.0;
+  return LDB_OK;
+}
+
+int ldb_kernel_timing_sweep(ldb_ctx* c, double* avg_sweep_ms, double* avg_fin_ms) {
+  if (!c || !avg_sweep_ms || !avg_fin_ms) return LDB_ERR_ARG;
+  const int rc = resolve_timing(c);
+  if (rc != LDB_OK) return rc;
+  *avg_sweep_ms = c->t_n ? c->t_sweep / c->t_n : 0.0;
+  *avg_fin_ms = c->t_n ? (c->t_fill - c->t_sweep) / c->t_n : 0.0;
   return LDB_OK;
 }
 

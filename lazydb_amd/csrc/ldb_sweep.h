@@ -46,11 +46,13 @@ constexpr uint32_t kSwDead = 1u, kSwDecl = 2u;
 constexpr uint64_t kSwPosMask = (1ull << 60) - 1;   // slab records: index tuple, walk tag in pos bits 60-63
 constexpr int kSwFinWaves = 4;
 
-// global tables (ldb_ctx::d_swt): register shift by 256 << i bytes (i = 0..4: 256 ... 4096), then the
-// slicing-by-16 tables (S[k][b]: the raw register after byte b and k zero bytes)
-constexpr int kSwShTabs = 5;
+// global tables (ldb_ctx::d_swt): register shift by 64 << i bytes (i = 0..6: 64 ... 4096), the slicing-by-16
+// tables (S[k][b]: the raw register after byte b and k zero bytes), then shifts by 16, 32 and 48 bytes (a
+// lane's four row registers joined)
+constexpr int kSwShTabs = 7;
 constexpr uint32_t kSwSl16Off = kSwShTabs * 1024;
-constexpr uint32_t kSwTabWords = kSwSl16Off + 16 * 256;
+constexpr uint32_t kSwRowOff = kSwSl16Off + 16 * 256;
+constexpr uint32_t kSwTabWords = kSwRowOff + 3 * 1024;
 
 struct alignas(16) SwRun {
   uint64_t E;       // the run's first chain entry as walked (run 0: x_s), ~0 none
@@ -79,7 +81,7 @@ static_assert(sizeof(SwCtl) == 128, "sweep control block");
 
 inline void build_swtab(uint32_t* t) {
   for (int i = 0; i < kSwShTabs; ++i) {
-    const uint32_t xn = x8n_modp(256ull << i);
+    const uint32_t xn = x8n_modp(64ull << i);
     for (int q = 0; q < 4; ++q)
       for (uint32_t b = 0; b < 256; ++b) t[i * 1024 + q * 256 + b] = multmodp(xn, b << (8 * q));
   }
@@ -91,6 +93,11 @@ inline void build_swtab(uint32_t* t) {
   }
   for (int k = 1; k < 16; ++k)
     for (uint32_t b = 0; b < 256; ++b) s[k * 256 + b] = (s[(k - 1) * 256 + b] >> 8) ^ s[s[(k - 1) * 256 + b] & 0xFFu];
+  for (int i = 0; i < 3; ++i) {
+    const uint32_t xn = x8n_modp(16ull * (i + 1));
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b) t[kSwRowOff + i * 1024 + q * 256 + b] = multmodp(xn, b << (8 * q));
+  }
 }
 
 }  // namespace ldb

@@ -69,81 +69,78 @@ __device__ __forceinline__ uint64_t sw_ld_sc1(const uint64_t* a) {
 }
 
 // The links between runs (the last k_sweep workgroup, every thread). The tier's entries are the chain
-// from x_s through the runs in order. Run r continues it when its first walked entry E_r is the previous
-// run's exit; a run the previous exit jumps over (an entry longer than the run: no start inside it) is
-// covered and passes that exit on. The tier ends at the first run that declined or does not continue the
-// chain (at its true entry, the exit before it), or at the end of a run whose chain ended inside it.
-// Every run linked to its predecessor is the common case and is checked in parallel; from the first
-// run that is not, wave 0 follows the chain run by run (64 run records in registers at a time).
+// from x_s through the runs in order. A run whose walk found a chain (E_r set; "active") continues it when
+// E_r is the exit of the last active run before it (x_s before run 0's); a run without one is passed when
+// that exit lies at or past its end (an entry longer than the run covers it). The tier ends at the first
+// run that does neither -- declined, a chain that is not the previous exit's, or an entry start the
+// walk could not take -- at the true chain position entering it (the previous exit), or at the end of an
+// active run whose chain ended inside it. Fully parallel: the last active run before each run is a
+// prefix maximum over the runs, each thread checks a contiguous share.
 __device__ void sw_link(const Pipe& p, const SwGeo& g) {
   __shared__ unsigned long long s_ev;
+  __shared__ int32_t s_la[1024];
   __shared__ uint64_t s_sum[1024];
-  __shared__ uint64_t s_ncov, s_xe;
+  __shared__ uint64_t s_xe;
+  constexpr int kPer = (kSwMaxRuns + 1023) / 1024;   // runs per thread (blockDim.x = 1024)
+  static_assert(64 * kSwWaves == 1024, "sw_link: one 1024-thread workgroup");
   SwCtl* c = p.swctl;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  const int lane = (int)(tid & 63u);
+  const uint64_t nrun = g.active ? g.nrun : 0;
+  const uint64_t r0 = (uint64_t)tid * kPer;
+  // this thread's runs, every load in flight together
+  uint64_t E[kPer], X[kPer], hi[kPer], n[kPer];
+  uint32_t fl[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const bool v = r0 + k < nrun;
+    const SwRun* q = p.swrun + (v ? r0 + k : 0);
+    E[k] = v ? q->E : ~0ull;
+    X[k] = q->X;
+    hi[k] = q->hi;
+    n[k] = q->n;
+    fl[k] = v ? q->flags : kSwDecl;
+  }
+  int32_t la = -1;   // the last active run of this thread's share
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+    if (!(fl[k] & kSwDecl) && E[k] != ~0ull) la = (int32_t)(r0 + k);
+  s_la[tid] = la;
   if (tid == 0) s_ev = ~0ull;
   __syncthreads();
-  const uint64_t nrun = g.active ? g.nrun : 0;
-  for (uint64_t r = tid; r < nrun; r += nt) {
-    const SwRun q = p.swrun[r];
-    uint64_t ev = ~0ull;
-    if ((q.flags & kSwDecl) || q.E == ~0ull || (r > 0 && p.swrun[r - 1].X != q.E)) ev = 2 * r;
-    else if (q.flags & kSwDead) ev = 2 * r + 1;
-    if (ev != ~0ull) atomicMin(&s_ev, (unsigned long long)ev);
+  for (uint32_t o = 1; o < nt; o <<= 1) {   // prefix maximum over the threads
+    const int32_t y = tid >= o ? s_la[tid - o] : -1;
+    __syncthreads();
+    if (y > s_la[tid]) s_la[tid] = y;
+    __syncthreads();
   }
-  __syncthreads();
-  if (tid < 64) {
-    const uint64_t ev = s_ev;
-    uint64_t ncov, xe;
-    if (nrun == 0) {
-      ncov = 0;
-      xe = g.xs;
-    } else if (ev == ~0ull) {
-      ncov = nrun;
-      xe = p.swrun[nrun - 1].X;
-    } else if (ev & 1) {
-      ncov = ev / 2 + 1;
-      xe = p.swrun[ev / 2].X;
-    } else {
-      const uint64_t r0 = ev / 2;
-      uint64_t T = r0 ? p.swrun[r0 - 1].X : g.xs;   // the chain's position entering run r0
-      ncov = ~0ull;
-      xe = 0;
-      for (uint64_t c0 = r0; c0 < nrun && ncov == ~0ull; c0 += 64) {
-        const uint64_t i = c0 + (uint64_t)lane;
-        SwRun q{};
-        if (i < nrun) q = p.swrun[i];
-        const uint32_t nl = nrun - c0 < 64 ? (uint32_t)(nrun - c0) : 64u;
-        for (uint32_t l = 0; l < nl; ++l) {
-          const uint64_t E = sw_readlane64(q.E, (int)l), X = sw_readlane64(q.X, (int)l), hi = sw_readlane64(q.hi, (int)l);
-          const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)q.flags, (int)l);
-          if (T >= hi) {   // covered: the chain has no entry in this run (its walk followed false candidates)
-            if ((uint32_t)lane == l) {
-              p.swrun[i].n = 0;
-              p.swrun[i].flags = fl & 0xFFu;   // walk tag 0: no record is the tier's
-            }
-            continue;
-          }
-          if ((fl & kSwDecl) || E != T) { ncov = c0 + l; xe = T; break; }
-          T = X;
-          if (fl & kSwDead) { ncov = c0 + l + 1; xe = X; break; }
-        }
-      }
-      if (ncov == ~0ull) { ncov = nrun; xe = T; }
+  const int32_t prev0 = tid ? s_la[tid - 1] : -1;   // the last active run before this share
+  uint64_t T = prev0 >= 0 ? p.swrun[prev0].X : g.xs;   // the chain's position entering the share
+  uint64_t ev = ~0ull, xe_mine = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (ev != ~0ull || r0 + k >= nrun) continue;
+    const uint64_t r = r0 + k;
+    if (!(fl[k] & kSwDecl) && E[k] != ~0ull) {
+      if (E[k] != T) { ev = 2 * r; xe_mine = T; continue; }
+      if (fl[k] & kSwDead) { ev = 2 * r + 1; xe_mine = X[k]; continue; }
+      T = X[k];
+    } else if (T < hi[k]) {   // not covered: the chain has an entry in this run that no walk took
+      ev = 2 * r;
+      xe_mine = T;
     }
-    if (tid == 0) { s_ncov = ncov; s_xe = xe; }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (ev != ~0ull) atomicMin(&s_ev, (unsigned long long)ev);
   __syncthreads();
-  const uint64_t ncov = s_ncov, xe = s_xe;
-  // bases: an exclusive prefix of the runs' entry counts, each thread a contiguous share (read past the
-  // CU's L1: wave 0 may just have zeroed a covered run's count)
-  const uint64_t per = (ncov + nt - 1) / nt;
-  const uint64_t r0 = tid * per, r1 = r0 + per < ncov ? r0 + per : ncov;
-  uint64_t s = 0;
-  for (uint64_t r = r0; r < r1; ++r) s += sw_ld_sc1(&p.swrun[r].n);
-  s_sum[tid] = s;
+  const uint64_t evm = s_ev;
+  if (evm != ~0ull && ev == evm) s_xe = xe_mine;
+  if (evm == ~0ull && tid == nt - 1) s_xe = s_la[nt - 1] >= 0 ? p.swrun[s_la[nt - 1]].X : g.xs;
+  __syncthreads();
+  const uint64_t ncov = evm == ~0ull ? nrun : ((evm & 1) ? evm / 2 + 1 : evm / 2), xe = s_xe;
+  // bases: an exclusive prefix of the runs' entry counts (inactive runs count 0)
+  uint64_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) sum += r0 + k < ncov ? n[k] : 0;
+  s_sum[tid] = sum;
   __syncthreads();
   for (uint32_t o = 1; o < nt; o <<= 1) {   // Hillis-Steele over the threads' sums
     const uint64_t y = tid >= o ? s_sum[tid - o] : 0;
@@ -151,10 +148,11 @@ __device__ void sw_link(const Pipe& p, const SwGeo& g) {
     s_sum[tid] += y;
     __syncthreads();
   }
-  uint64_t b = s_sum[tid] - s;
-  for (uint64_t r = r0; r < r1; ++r) {
-    p.swrun[r].base = b;
-    b += sw_ld_sc1(&p.swrun[r].n);
+  uint64_t b = s_sum[tid] - sum;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (r0 + k < ncov) p.swrun[r0 + k].base = b;
+    b += r0 + k < ncov ? n[k] : 0;
   }
   if (tid == nt - 1) {
     c->xs = g.xs;
@@ -169,13 +167,34 @@ __device__ void sw_link(const Pipe& p, const SwGeo& g) {
   }
 }
 
-// kHitGroups: every 64-B row of a window whose dwords may hold a candidate's Status byte
+// phase stamps (LDB_STAMPS builds, tools/sweep_time.py): s_memtime cycles summed over the waves. 0 setup,
+// 1 loads waited for in a quarter, 2 candidates, 3 CRC + tree, 4 decode (drain), 5 streaming loop in all,
+// 6 final decode + walk, 7 links (last workgroup), 8 waves
+#ifdef LDB_STAMPS
+__device__ uint64_t g_swstamps[16];
+#define SW_T(v)   \
+  uint64_t v;     \
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
+#define SW_ADD(k, a, b) swacc[k] += (b) - (a)
+#else
+#define SW_T(v)
+#define SW_ADD(k, a, b)
+#endif
+
+#ifndef LDB_SW_ABL
+#define LDB_SW_ABL 0   // attribution builds only (results invalid): 1 no CRC, 2 no candidates, 4 no walk, 8 no register
+                       // stores, 16 no lane tree
+#endif
 __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
   __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
-  __shared__ __attribute__((aligned(16))) uint32_t sh[4 * 1024];   // shift by 256, 512, 1024, 2048 bytes
+  __shared__ __attribute__((aligned(16))) uint32_t sh[9 * 1024];   // shift by 64, 128, ..., 2048, then 16, 32, 48 bytes
   __shared__ uint32_t hits[kSwWaves][kSwList];
   __shared__ int s_last;
   if (scan_done(p)) return;   // the run prefix ended the scan
+#ifdef LDB_STAMPS
+  uint64_t swacc[9] = {};
+#endif
+  SW_T(ts0);
   const SwGeo g = sw_geo(p, (uint64_t)gridDim.x * kSwWaves);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -183,9 +202,15 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
   const bool mine = g.active && r < g.nrun;
   if (__syncthreads_or(mine ? 1 : 0)) {
     lp2_build(lp2, p.gtab);
-    for (uint32_t i = threadIdx.x; i < 4 * 1024; i += blockDim.x) sh[i] = p.swt[i];
+    for (uint32_t i = threadIdx.x; i < 6 * 1024; i += blockDim.x) {
+      const uint32_t a = p.swt[i], b = i < 3 * 1024 ? p.swt[kSwRowOff + i] : 0u;
+      sh[i] = a;
+      if (i < 3 * 1024) sh[6 * 1024 + i] = b;
+    }
     __syncthreads();
   }
+  SW_T(ts1);
+  SW_ADD(0, ts0, ts1);
   if (mine) {
     const uint64_t A = g.a0 + r * g.rl;
     const uint64_t B = A + g.rl < p.len ? A + g.rl : p.len;
@@ -222,38 +247,51 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       if (ncand > cap) decl = true;
     };
     v2u32 kv = {0xFFFFFFFFu, 0xFFFFFFFFu};
-    for (uint64_t b = A; b < B; b += kSwBatch) {
-      {   // a run before this one ends the tier: nothing here is used
-        const uint64_t stop = ((uint64_t)__builtin_amdgcn_readfirstlane(kv[1]) << 32) | __builtin_amdgcn_readfirstlane(kv[0]);
-        if (stop < r) { decl = true; break; }
-      }
-      const uint32_t wo = (uint32_t)(b - A) + (uint32_t)lane * kSwW;
-      uint32_t d[64];
+    // The run in quarters of 4 KiB: lane l holds the quarter's bytes [64 l, 64 l + 64) as 4 rows (a row
+    // instruction reads 4 KiB in 64-B steps; the lane's bytes stay contiguous for its CRC), lane 63 also the
+    // next quarter's first 8 bytes. Software pipeline: the next two quarters' rows are in flight while two
+    // are processed (a wave that waited for its own loads between batches left the memory idle).
+    struct QB {
+      uint32_t d[16];
+      uint32_t n0, n1;
+    };
+    auto load_q = [&](QB& q, uint32_t qo) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint4 q = ld16(irs, wo + 16u * k);
-        d[4 * k] = q.x; d[4 * k + 1] = q.y; d[4 * k + 2] = q.z; d[4 * k + 3] = q.w;
+      for (int k = 0; k < 4; ++k) {
+        const uint4 x = ld16(irs, qo + 64u * (uint32_t)lane + 16u * k);
+        q.d[4 * k] = x.x; q.d[4 * k + 1] = x.y; q.d[4 * k + 2] = x.z; q.d[4 * k + 3] = x.w;
       }
-      const uint32_t n0l = ld4(irs, lane == 63 ? wo + kSwW : kDrop), n1l = ld4(irs, lane == 63 ? wo + kSwW + 4 : kDrop);
-      kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
-      __builtin_amdgcn_sched_barrier(0);
-      // the next window's first two dwords (lane 63: the next batch's, loaded)
-      uint32_t n0 = (uint32_t)__shfl_down((int)d[0], 1), n1 = (uint32_t)__shfl_down((int)d[1], 1);
-      n0 = lane == 63 ? n0l : n0;
-      n1 = lane == 63 ? n1l : n1;
-      auto D = [&](int i) -> uint32_t { return i < 64 ? d[i] : (i == 64 ? n0 : n1); };
+      q.n0 = ld4(irs, lane == 63 ? qo + 4096u : kDrop);
+      q.n1 = ld4(irs, lane == 63 ? qo + 4100u : kDrop);
+    };
+    // one quarter: its candidates appended to the hit list (in file order), each lane's register over its
+    // 64 bytes, the window (RW) and quarter (RG) registers. False when the run is too dense for the tier.
+    auto proc_q = [&](const QB& q, uint32_t qo) -> bool {
+      SW_T(tq0);
+      const uint32_t wo = qo + 64u * (uint32_t)lane;   // the lane's window, from A
+      // the next window's first two dwords: the next lane's (lane 63: loaded with the quarter)
+      uint32_t n0 = sw_dpp<0x130>(q.d[0]), n1 = sw_dpp<0x130>(q.d[1]);   // wave_shl:1
+      n0 = lane == 63 ? q.n0 : n0;
+      n1 = lane == 63 ? q.n1 : n1;
+      auto D = [&](int i) -> uint32_t { return i < 16 ? q.d[i] : (i == 16 ? n0 : n1); };
       uint32_t orw = 0;
 #pragma unroll
-      for (int i = 0; i < 64; ++i) orw |= d[i];
+      for (int i = 0; i < 16; ++i) orw |= q.d[i];
       const uint32_t zmask = orw ? 0xFFFFFFFFu : 0u;   // an all-zero window has no candidate but in its last 4 bytes
+#ifdef LDB_STAMPS
+      asm volatile("" ::"v"(zmask));
+#endif
+      SW_T(tq1);
+      SW_ADD(1, tq0, tq1);
       // pass 1: rows (groups of 4 dwords) where some lane may have a candidate; the lane's count
       uint32_t gm = 0, cnt = 0;
 #pragma unroll
-      for (int gi = 0; gi < 16; ++gi) {
+      for (int gi = 0; gi < 4; ++gi) {
         uint32_t any = 0;
 #pragma unroll
         for (int k = 1; k <= 4; ++k) any |= small_bytes(D(4 * gi + k));
-        if (gi < 15) any &= zmask;
+        if (gi < 3) any &= zmask;
+        if (LDB_SW_ABL & 2) any = 0;
         if (__ballot(any != 0u)) {
           gm |= 1u << gi;
 #pragma unroll
@@ -261,26 +299,27 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         }
       }
       if (gm) {
-        uint32_t x = cnt;   // inclusive scan over the lanes
+        // exclusive prefix of the counts over the lanes, bit by bit (a count is < 128): ballots, no LDS
+        uint32_t ex = 0, tot = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-          if (lane >= o) x += y;
+        for (int bit = 0; bit < 7; ++bit) {
+          const uint64_t bb = __ballot((cnt >> bit) & 1u);
+          ex += sw_rank(bb, lane) << bit;
+          tot += (uint32_t)__builtin_popcountll(bb) << bit;
         }
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-        if (npend + tot > kSwList) { decl = true; break; }   // too dense for the tier: the region pipeline takes it
+        if (npend + tot > kSwList) return false;   // too dense for the tier: the region pipeline takes it
         // pass 2: the positions, in file order (lane-major: the windows are in lane order)
-        uint32_t j = npend + x - cnt;
+        uint32_t j = npend + ex;
 #pragma unroll
-        for (int gi = 0; gi < 16; ++gi) {
+        for (int gi = 0; gi < 4; ++gi) {
           if ((gm >> gi) & 1u) {
 #pragma unroll
             for (int k = 1; k <= 4; ++k) {
               uint32_t m = sw_hits(D(4 * gi + k - 1), D(4 * gi + k), D(4 * gi + k + 1));
-              if (gi < 15 || k < 4) m &= zmask;
+              if (gi < 3 || k < 4) m &= zmask;
               const uint32_t base = wo + 4u * (4 * gi + k - 1);
 #pragma unroll
-              for (int t = 0; t < 4; ++t) {
+              for (int u = 0; u < 4; ++u) {
                 if (m) {
                   hl[j++] = base + ((uint32_t)__builtin_ctz(m) >> 3);
                   m &= m - 1;
@@ -291,27 +330,59 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         }
         npend += tot;
       }
-      // the window's raw register (LP2: conflict-free lane-private tables)
+      SW_T(tq2);
+      SW_ADD(2, tq1, tq2);
+      // the lane's raw register over its 64 bytes (LP2: conflict-free lane-private tables)
       uint32_t reg = 0;
+      if (LDB_SW_ABL & 1) {
 #pragma unroll
-      for (int k = 0; k < 32; ++k) reg = lp2_step4(lp2, lb, lp2_step4(lp2, lb, reg, d[2 * k]), d[2 * k + 1]);
-      const uint64_t wi = (b >> 8) + (uint64_t)lane;
-      p.swrw[wi] = reg;
-      // group registers: a tree over each 16-lane row (DPP row shifts), lane 15 of the row ends with it
-      {
-        uint32_t v = reg, y;
-        y = sw_dpp<0x111>(v);
-        if (lane & 1) v ^= sw_shift(sh, y);
-        y = sw_dpp<0x112>(v);
-        if ((lane & 3) == 3) v ^= sw_shift(sh + 1024, y);
-        y = sw_dpp<0x114>(v);
-        if ((lane & 7) == 7) v ^= sw_shift(sh + 2048, y);
-        y = sw_dpp<0x118>(v);
-        if ((lane & 15) == 15) {
-          v ^= sw_shift(sh + 3072, y);
-          p.swrg[wi >> 4] = v;
-        }
+        for (int k = 0; k < 16; ++k) reg ^= q.d[k];
+      } else {
+        // one chain per 16-B row (four in flight), joined by shifts of 48, 32 and 16 bytes
+        uint32_t c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          c[k] = lp2_step4(lp2, lb, lp2_step4(lp2, lb, lp2_step4(lp2, lb, lp2_step4(lp2, lb, 0u, q.d[4 * k]), q.d[4 * k + 1]),
+                                              q.d[4 * k + 2]), q.d[4 * k + 3]);
+        reg = sw_shift(sh + 8 * 1024, c[0]) ^ sw_shift(sh + 7 * 1024, c[1]) ^ sw_shift(sh + 6 * 1024, c[2]) ^ c[3];
       }
+      // a tree over the lanes (DPP): level i joins runs of 2^i lanes with a shift by 64 2^i bytes. Lane 4m+3
+      // ends level 2 with window m's register (RW, 256 B), lane 63 level 6 with the quarter's (RG, 4 KiB)
+      const uint64_t w0 = (A + qo) >> 8;
+      if (LDB_SW_ABL & 16) {   // attribution: no tree
+        if (!(LDB_SW_ABL & 8) && (lane & 3) == 3) p.swrw[w0 + (uint32_t)(lane >> 2)] = reg;
+        else asm volatile("" ::"v"(reg));
+        return true;
+      }
+      uint32_t v = reg, y;
+      y = sw_dpp<0x111>(v);                                   // row_shr:1
+      if (lane & 1) v ^= sw_shift(sh, y);
+      y = sw_dpp<0x112>(v);                                   // row_shr:2
+      if ((lane & 3) == 3) {
+        v ^= sw_shift(sh + 1024, y);
+        if (!(LDB_SW_ABL & 8)) p.swrw[w0 + (uint32_t)(lane >> 2)] = v;
+      }
+      y = sw_dpp<0x114>(v);                                   // row_shr:4
+      if ((lane & 7) == 7) v ^= sw_shift(sh + 2048, y);
+      y = sw_dpp<0x118>(v);                                   // row_shr:8
+      if ((lane & 15) == 15) v ^= sw_shift(sh + 3072, y);
+      y = sw_dpp<0x142>(v);                                   // row_bcast:15
+      if ((lane & 31) == 31) v ^= sw_shift(sh + 4096, y);
+      y = sw_dpp<0x143>(v);                                   // row_bcast:31
+      if (lane == 63) {
+        v ^= sw_shift(sh + 5120, y);
+        if (!(LDB_SW_ABL & 8)) p.swrg[w0 >> 4] = v;
+        else asm volatile("" ::"v"(v));
+      }
+#ifdef LDB_STAMPS
+      asm volatile("" ::"v"(v));
+#endif
+      SW_T(tq3);
+      SW_ADD(3, tq2, tq3);
+      return true;
+    };
+    auto drain = [&] {   // decode while 64 or more candidates wait
+      SW_T(td0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the hit list's stores, before other lanes read them
       while (npend >= 64 && !decl) {
         flush(64);
@@ -323,8 +394,34 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      if (decl) break;
+      SW_T(td1);
+      SW_ADD(4, td0, td1);
+    };
+    const uint32_t nq = (uint32_t)((B - A + 4095) / 4096);
+    SW_T(tl0);
+    QB P0, P1, Q0, Q1;
+    if (nq > 0) load_q(P0, 0);
+    if (nq > 1) load_q(P1, 4096);
+    for (uint32_t i = 0; i < nq && !decl; i += 4) {
+      {   // a run before this one ends the tier: nothing here is used
+        const uint64_t stop = ((uint64_t)__builtin_amdgcn_readfirstlane(kv[1]) << 32) | __builtin_amdgcn_readfirstlane(kv[0]);
+        if (stop < r) { decl = true; break; }
+      }
+      if (i + 2 < nq) load_q(Q0, (i + 2) * 4096u);
+      if (i + 3 < nq) load_q(Q1, (i + 3) * 4096u);
+      kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!proc_q(P0, i * 4096u)) { decl = true; break; }
+      if (i + 1 < nq && !proc_q(P1, (i + 1) * 4096u)) { decl = true; break; }
+      if (i + 4 < nq) load_q(P0, (i + 4) * 4096u);
+      if (i + 5 < nq) load_q(P1, (i + 5) * 4096u);
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 2 < nq && !proc_q(Q0, (i + 2) * 4096u)) { decl = true; break; }
+      if (i + 3 < nq && !proc_q(Q1, (i + 3) * 4096u)) { decl = true; break; }
+      drain();
     }
+    SW_T(tl1);
+    SW_ADD(5, tl0, tl1);
     if (!decl && npend) flush(npend);
     if (decl) atomicMin((unsigned long long*)&p.swctl->stop, (unsigned long long)r);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slab's stores, before the walk reads them
@@ -349,7 +446,8 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       const uint32_t i = blk * 64u + (uint32_t)lane;
       store16(srs, i < ncand ? i * 16u : kDrop, rec.x, rec.y, rec.z, rec.w);
     };
-    if (!decl && ncand <= cap) {
+    if (LDB_SW_ABL & 4) fl |= kSwDecl;
+    if (!decl && ncand <= cap && !(LDB_SW_ABL & 4)) {
       if (ncand) load_blk(0);
       if (r == 0) E = g.xs;
       else if (ncand) E = sw_readlane64(lp, 0);
@@ -391,6 +489,10 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       }
       if (dirty) write_blk(bi);
     }
+    if (E == ~0ull || (fl & kSwDecl)) {   // no chain: no record of this run is the tier's (k_sweep_fin: tag 0)
+      tag = 0;
+      cnt = 0;
+    }
     {   // the run record (SwRun, 64 B): lanes 0-3 store 16 B each
       const uint64_t u0 = lane == 0 ? E : (lane == 1 ? cnt : (lane == 2 ? lo : 0ull));
       const uint64_t u1 = lane == 0 ? X : (lane == 1 ? ((uint64_t)ncand << 32 | (fl | (tag << 8))) : (lane == 2 ? B : 0ull));
@@ -398,7 +500,14 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       store16(rrs, lane < 4 ? (uint32_t)lane * 16u : kDrop, (uint32_t)u0, (uint32_t)(u0 >> 32), (uint32_t)u1,
               (uint32_t)(u1 >> 32));
     }
+    SW_T(tl2);
+    SW_ADD(6, tl1, tl2);
   }
+#ifdef LDB_STAMPS
+  swacc[8] = mine ? 1 : 0;
+  if (lane == 0)
+    for (int k = 0; k < 9; ++k) atomicAdd((unsigned long long*)&g_swstamps[k], (unsigned long long)swacc[k]);
+#endif
   // the last workgroup resolves the links
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -412,7 +521,12 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  SW_T(tk0);
   sw_link(p, g);
+  SW_T(tk1);
+#ifdef LDB_STAMPS
+  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&g_swstamps[7], (unsigned long long)(tk1 - tk0));
+#endif
 }
 
 // ---------------------------------------------------------------- k_sweep_fin
@@ -608,11 +722,17 @@ __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
   if (scan_done(p)) return;
   SwCtl* c = p.swctl;
   if (c->state != 1) return;
-  for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
-    st[i] = p.swt[i];                         // shift by 256
-    st[1024 + i] = p.swt[4 * 1024 + i];       // shift by 4096
+  {   // shift by 256, shift by 4096, slicing-by-16: every load in flight before the stores
+    static_assert(64 * kSwFinWaves == 256, "k_sweep_fin: 256 threads copy 6144 words");
+    uint32_t v[24];
+#pragma unroll
+    for (int k = 0; k < 24; ++k) {
+      const uint32_t i = threadIdx.x + 256u * k;
+      v[k] = p.swt[i < 1024 ? 2 * 1024 + i : (i < 2048 ? 6 * 1024 + i - 1024 : kSwSl16Off + i - 2048)];
+    }
+#pragma unroll
+    for (int k = 0; k < 24; ++k) st[threadIdx.x + 256u * k] = v[k];
   }
-  for (uint32_t i = threadIdx.x; i < 16 * 256; i += blockDim.x) st[2048 + i] = p.swt[kSwSl16Off + i];
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;

@@ -316,3 +316,9 @@ class Engine:
         f = C.c_double()
         N.check(N.lib().ldb_kernel_timing_fill(self.ctx, C.byref(f)), "timing_fill")
         return f.value
+
+    def timing_sweep(self):
+        """(avg k_sweep ms, avg k_sweep_fin ms) over the timed launches: the sweep tier (query)."""
+        a, b = C.c_double(), C.c_double()
+        N.check(N.lib().ldb_kernel_timing_sweep(self.ctx, C.byref(a), C.byref(b)), "timing_sweep")
+        return a.value, b.value

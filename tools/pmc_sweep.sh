@@ -1,0 +1,28 @@
+# PMC passes on the sweep tier's kernels (k_sweep, k_sweep_fin) over a 1 GiB Zipf log (tools/sweep_time.py),
+# one counter set per rocprofv3 run (never combined with other traces), summarised per kernel.
+# usage: bash tools/pmc_sweep.sh <tag>   -> gpurun_out/pmcsw_<tag>/
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+TAG=${1:-x}
+OUT=gpurun_out/pmcsw_$TAG
+mkdir -p $OUT
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+           "SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+           "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $set --kernel-include-regex 'k_sweep' -d $OUT/pmc$i -o pmc -f csv -- python3 tools/sweep_time.py ${MIB:-1024} 5 > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 1; }
+done
+python3 - "$OUT" <<'PY'
+import csv, glob, sys, collections
+out = sys.argv[1]
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(out + "/pmc*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in acc.items():
+    print("==", k)
+    for c, v in sorted(cs.items()):
+        print(f"  {c:22s} {sum(v) / len(v):16.1f}   (n={len(v)})")
+PY

@@ -66,9 +66,9 @@ def main():
             res, _ = eng.scan_dev(d, cap=n0 + 1024)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / 10
-        sw = eng.timing_fill()
+        sw, fin = eng.timing_sweep()
         u, mm, tot, k = eng.timing_split(0)
-        print(f"   {name}: {dt * 1e3:.3f} ms/scan wall, k_uniform {u:.4f} sweep {sw:.4f} k_scan_main {mm:.4f} "
+        print(f"   {name}: {dt * 1e3:.3f} ms/scan wall, k_uniform {u:.4f} k_sweep {sw:.4f} fin {fin:.4f} k_scan_main {mm:.4f} "
               f"pipeline {tot:.4f} ms = {im.size / tot / 1e6:.1f} GB/s", flush=True)
     eng.close()
     print("ALL OK" if bad == 0 else f"{bad} BAD")
