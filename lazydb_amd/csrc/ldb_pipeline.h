@@ -49,6 +49,7 @@ struct Pipe {
   // its run records and control block, its global tables; its candidate slabs are the scratch tuples
   uint32_t* swrw;
   uint32_t* swrg;
+  uint32_t* swpl;
   SwRun* swrun;
   SwCtl* swctl;
   const uint32_t* swt;

@@ -2445,7 +2445,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_dyn, o_uni, o_blk, o_swrw, o_swrg, o_swrun, o_swctl, total;
+  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_dyn, o_uni, o_blk, o_swrw, o_swrg, o_swpl, o_swrun, o_swctl, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -2473,6 +2473,7 @@ WsLayout layout(uint64_t len) {
   // rounded up, plus one), its run records and control block; its slabs are the scratch tuples above
   L.o_swrw = take(4 * ((len + kSwBatch) / kSwW + 1));
   L.o_swrg = take(4 * ((len + kSwBatch) / (kSwW * kSwG) + 1));
+  L.o_swpl = take(4 * ((len + kSwBatch) / 64 + 1));
   L.o_swrun = take(sizeof(SwRun) * (uint64_t)kSwMaxRuns);
   L.o_swctl = take(sizeof(SwCtl));
   L.total = o;
@@ -2523,6 +2524,7 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.result = res;
   p.swrw = reinterpret_cast<uint32_t*>(w + L.o_swrw);
   p.swrg = reinterpret_cast<uint32_t*>(w + L.o_swrg);
+  p.swpl = reinterpret_cast<uint32_t*>(w + L.o_swpl);
   p.swrun = reinterpret_cast<SwRun*>(w + L.o_swrun);
   p.swctl = reinterpret_cast<SwCtl*>(w + L.o_swctl);
   p.swt = c->d_swt;

@@ -64,7 +64,7 @@ def agree(ok: bool, what: str, device) -> None:
                            f"{'' if not ok else ', not this one'})")
 
 
-def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0):
+def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0, device=None):
     """Gather every rank's tuple byte buffer (uint8, 1-D, on the rank's device) to `dst`: a gatherv.
 
     One all_gather of the byte counts, then point-to-point transfers of exactly those bytes (one
@@ -72,20 +72,22 @@ def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0):
     unequal files ship no padding. Returns the list of per-rank buffers (rank order) on `dst`, None
     elsewhere; gather_tuples.last_bytes is the byte total that crossed to dst. A rank whose buffer is
     not a 1-D uint8 tensor makes every rank raise (agree) instead of leaving the others blocked.
+    `device`: the rank's GPU (default: the buffer's device), where the collective buffers live under RCCL.
     """
     world = dist.get_world_size()
     rank = dist.get_rank()
     ok = isinstance(tuple_bytes, torch.Tensor) and tuple_bytes.dtype == torch.uint8 and tuple_bytes.dim() == 1 \
         and 0 <= dst < world
-    dev = coll_device(tuple_bytes.device if isinstance(tuple_bytes, torch.Tensor) else torch.device("cpu"))
+    if device is None:
+        device = tuple_bytes.device if isinstance(tuple_bytes, torch.Tensor) else \
+            (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+    dev = coll_device(device)
     agree(ok, "gather_tuples", dev)
     tuple_bytes = tuple_bytes.to(dev).contiguous()
     n = torch.tensor([tuple_bytes.numel()], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
-    if counts[rank] != tuple_bytes.numel():   # every rank sees the same list; this would be a transport fault
-        raise RuntimeError(f"gather_tuples: rank {rank} counted {counts[rank]} B, holds {tuple_bytes.numel()}")
     gather_tuples.last_bytes = sum(c for r, c in enumerate(counts) if r != dst)
     if rank == dst:
         bufs = [tuple_bytes if r == dst else torch.empty(counts[r], dtype=torch.uint8, device=dev)

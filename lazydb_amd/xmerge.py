@@ -337,18 +337,19 @@ def merge_distributed(eng, files, max_fid: int, active_fid: int, active_off: int
     return pl
 
 
-def _all_to_all_varlen(chunks, dist):
+def _all_to_all_varlen(chunks, dist, device):
     """chunks[o] (1-D uint8 device tensors) to rank o; returns what every rank sent here, rank order.
     RCCL: all_to_all_single with the splits; gloo (CPU tests): an all-gather of everything, host copies.
-    A rank with the wrong number of chunks makes every rank raise (multi.agree) before any byte moves;
-    after the size exchange, the bytes all ranks will send and receive are summed and must agree."""
+    `device` is the engine's GPU (the collective's buffers follow the backend through coll_device), never
+    taken from the chunks, which a refused call may not have. A rank with the wrong number of chunks makes
+    every rank raise (multi.agree) before any byte moves."""
     import torch
     from .multi import agree, coll_device
     world = dist.get_world_size()
     rank = dist.get_rank()
     ok = len(chunks) == world and all(c.dtype == torch.uint8 and c.dim() == 1 for c in chunks)
-    dev = chunks[0].device if chunks else torch.device("cpu")
-    agree(ok, "all-to-all exchange", dev)
+    agree(ok, "all-to-all exchange", device)
+    dev = coll_device(device)
     sizes = torch.tensor([int(c.numel()) for c in chunks], dtype=torch.int64)
     if dist.get_backend() == "gloo":
         flat = torch.cat(chunks).cpu() if chunks else torch.zeros(0, dtype=torch.uint8)
@@ -358,17 +359,11 @@ def _all_to_all_varlen(chunks, dist):
         out = []
         for src in range(world):
             off = int(allsz[src][:rank].sum())
-            out.append(got[src][off: off + int(allsz[src][rank])].to(dev))
+            out.append(got[src][off: off + int(allsz[src][rank])].to(device))
         return out
     sizes_d = sizes.to(dev)
     recv_sz = torch.empty_like(sizes_d)
     dist.all_to_all_single(recv_sz, sizes_d)
-    # the sizes every rank will send must equal what every rank expects to receive (a transport or
-    # caller fault otherwise: all_to_all_single with mismatched splits would fail or hang mid-transfer)
-    bal = torch.stack([sizes_d.sum(), recv_sz.sum()]).to(coll_device(dev))
-    dist.all_reduce(bal)
-    if int(bal[0]) != int(bal[1]):
-        raise RuntimeError(f"all-to-all exchange: ranks send {int(bal[0])} B in all but expect {int(bal[1])} B")
     recv_sz = [int(x) for x in recv_sz.cpu()]
     send = torch.cat(chunks) if chunks else torch.zeros(0, dtype=torch.uint8, device=dev)
     recv = torch.empty(sum(recv_sz), dtype=torch.uint8, device=dev)
@@ -388,12 +383,13 @@ def merge_hashed_distributed(eng, files, active_fid: int, active_off: int, max_f
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
-    check_fid_blocks(files, dist, torch.device("cuda", eng.device))
+    gdev = torch.device("cuda", eng.device)
+    check_fid_blocks(files, dist, gdev)
     ro = route_phase(eng, files, world, io_type)
     rc = [ro["recs"][sum(ro["rec_splits"][:o]): sum(ro["rec_splits"][:o + 1])] for o in range(world)]
     kc = [ro["keys"][sum(ro["key_splits"][:o]): sum(ro["key_splits"][:o + 1])] for o in range(world)]
-    got_r = _all_to_all_varlen(rc, dist)
-    got_k = _all_to_all_varlen(kc, dist)
+    got_r = _all_to_all_varlen(rc, dist, gdev)
+    got_k = _all_to_all_varlen(kc, dist, gdev)
     recs, keys, ord_ = owner_inputs(torch, got_r, got_k, [int(x.numel()) // ROUTE_REC_BYTES for x in got_r])
     last = eng.merge_resolve(recs, keys, ord_)
     back, b = [], 0
@@ -401,7 +397,7 @@ def merge_hashed_distributed(eng, files, active_fid: int, active_off: int, max_f
         n = int(x.numel()) // ROUTE_REC_BYTES
         back.append(last[b: b + n])
         b += n
-    mine = _all_to_all_varlen(back, dist)
+    mine = _all_to_all_varlen(back, dist, gdev)
     lr = last_by_seq(torch, ro, mine, int(ro["result"].n_records))
     part = apply_phase(eng, files, lr, active_fid, active_off, max_file_size, now, io_type)
     sizes = _all_gather_varlen(entry_sizes(eng, part), dist) if world > 1 else []

@@ -65,7 +65,7 @@ def _a2a_worker(rank, world, port, q):
         # rank r sends (r + 1) * o + 1 bytes of value 10 r + o to rank o (rank 0 sends nothing to rank 0)
         chunks = [torch.full(((rank + 1) * o + (0 if rank == 0 and o == 0 else 1),), 10 * rank + o, dtype=torch.uint8)
                   for o in range(world)]
-        got = _all_to_all_varlen(chunks, dist)
+        got = _all_to_all_varlen(chunks, dist, torch.device("cpu"))
         q.put((rank, [x.tolist() for x in got]))
     finally:
         dist.destroy_process_group()
@@ -201,7 +201,7 @@ def _a2a_bad_worker(rank, world, port, q):
         n = world if rank != 1 else world - 1
         chunks = [torch.full((3 + o,), rank, dtype=torch.uint8) for o in range(n)]
         try:
-            _all_to_all_varlen(chunks, dist)
+            _all_to_all_varlen(chunks, dist, torch.device("cpu"))
             q.put((rank, "ok"))
         except RuntimeError as e:
             q.put((rank, "refused: " + str(e)))
