@@ -111,9 +111,11 @@ typedef struct ldb_scan_result {
 } ldb_scan_result;
 
 /* ---- context ---------------------------------------------------------------
- * One context per (thread, device). Holds the device's CRC tables and a
- * growable scan workspace. Not safe for concurrent calls; use one context per
- * caller thread (index.go:103-108 replays the 5 value types from 5 goroutines). */
+ * One context per device and concurrent caller. Holds the device's CRC tables and a
+ * growable scan workspace. A context serves one call at a time but is bound to no
+ * thread (every entry point selects its device first): callers may pool contexts and
+ * hand them to any thread, never to two at once (index.go:103-108 replays the 5 value
+ * types from 5 goroutines: 5 contexts). */
 typedef struct ldb_ctx ldb_ctx;
 
 int ldb_abi_version(void);

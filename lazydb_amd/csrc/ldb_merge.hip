@@ -403,7 +403,7 @@ __global__ __launch_bounds__(256) void k_live(uint64_t n, const FileDesc* __rest
     esz[seq] = emit ? size : 0u;
     if (live_out) live_out[seq] = live ? 1 : 0;
   }
-  const uint64_t last = min(n, b0 + blockDim.x) - 1;
+  const uint64_t last = (n < b0 + blockDim.x ? n : b0 + blockDim.x) - 1;
   const bool uniform = file_of(fd, n_files, b0) == file_of(fd, n_files, last);
   if (!uniform) {
     if (valid && live) {
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(256) void k_file_stats(const FileDesc* __restrict__
   if (hi > lo) {
     const uint64_t blo = lo / 256, bhi = (hi - 1) / 256;   // k_live blocks touching the file
     for (uint64_t k = blo + threadIdx.x; k <= bhi; k += blockDim.x) {
-      const uint64_t s0 = k * 256, s1 = min(n, s0 + 256) - 1;
+      const uint64_t s0 = k * 256, s1 = (n < s0 + 256 ? n : s0 + 256) - 1;
       if (s0 >= lo && s1 < hi) {   // wholly inside: a uniform block (straddlers added per record)
         c += part[2 * k];
         b += part[2 * k + 1];
@@ -729,7 +729,7 @@ __device__ uint64_t last_le(const uint64_t* P, uint64_t n, uint64_t x, int lane)
     const uint64_t idx = lo + (uint64_t)lane * step;
     const uint64_t m = __ballot(idx <= hi && P[idx] <= x);   // a prefix of the lanes; lane 0 always
     const uint64_t nlo = lo + (uint64_t)(63 - __builtin_clzll(m)) * step;
-    hi = min(hi, nlo + step - 1);
+    hi = hi < nlo + step - 1 ? hi : nlo + step - 1;
     lo = nlo;
   }
   return lo;

@@ -1153,7 +1153,7 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
     const uint64_t b0 = y0 + b * E * sz;
     const uint64_t base = b0 >= 512 ? (b0 - 512) & ~15ull : 0;   // wave-uniform; the lead t < 8 G <= 512
     const uint64_t nrec = (p.len - base + 3) & ~3ull;
-    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)min(nrec, (uint64_t)0xFFFFFFFFu));
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + base, (uint32_t)(nrec < 0xFFFFFFFFull ? nrec : 0xFFFFFFFFull));
     // the group's last lane: the header (stored crc and bytes [4, 40)), in flight with the rows
     const uint32_t hx = (uint32_t)(x - base), ha = hx & ~3u, hsh = kAl ? 0u : hx & 3u;
     // the header rows the check reads: dwords [0, nw + 2) from ha (the stored crc, nw template words and
@@ -1624,7 +1624,8 @@ __global__ __launch_bounds__(kFillThreads) void k_uniform_fill_batch(UniBatch b)
   for (uint64_t e0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); e0 < n; e0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t e = e0 + (threadIdx.x & 63u);
     const uint64_t wb = (e0 * sz + hs) & ~3ull;
-    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + wb, (uint32_t)min((p.len - wb + 3) & ~3ull, (uint64_t)0xFFFFFFFFu));
+    const uint64_t wbn = (p.len - wb + 3) & ~3ull;
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.img + wb, (uint32_t)(wbn < 0xFFFFFFFFull ? wbn : 0xFFFFFFFFull));
     if (e >= n) continue;
     const uint32_t kx = (uint32_t)(e * sz + hs - wb), ka = kx & ~3u, s0 = kx & 3u;
     p.hash_out[e] = key_hash_w(
@@ -1696,7 +1697,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
   // summary), so the speculative entry has settled onto the chain by the run's first region (a chain
   // from a false start falls back onto the true one within a few entries): far fewer broken links
   // between runs for k_repair to walk.
-  const uint64_t warm = (count && rb > rf) ? min((uint64_t)kWarm, rb - rf) : 0;
+  const uint64_t warm = (count && rb > rf) ? ((uint64_t)kWarm < rb - rf ? (uint64_t)kWarm : rb - rf) : 0;
   const uint64_t r00 = rb - warm, total = count + warm;
   uint32_t n_fast = 0;
   uint32_t declines = 0;        // consecutive lean declines (give-up mode, below)

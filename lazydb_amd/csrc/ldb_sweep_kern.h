@@ -222,7 +222,8 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
     const uint32_t cap = (uint32_t)(cap64 < 0x7FFFFFFFull ? cap64 : 0x7FFFFFFFull);
     ldb_index_tuple* slab = p.scratch + r * cap64;
     const __amdgpu_buffer_rsrc_t srs = rsrc_of(slab, cap * 16u);
-    const __amdgpu_buffer_rsrc_t irs = rsrc_of(p.img + A, (uint32_t)min((p.len - A + 3) & ~3ull, (uint64_t)0xFFFFFFFFu));
+    const uint64_t ib = (p.len - A + 3) & ~3ull;   // (a ternary: min() on 64-bit unsigned is HIP's double overload)
+    const __amdgpu_buffer_rsrc_t irs = rsrc_of(p.img + A, (uint32_t)(ib < 0xFFFFFFFFull ? ib : 0xFFFFFFFFull));
     const __amdgpu_buffer_rsrc_t krs = rsrc_of(&p.swctl->stop, 8);
     uint32_t npend = 0, ncand = 0;
     bool decl = false;
@@ -278,17 +279,11 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       n0 = lane == 63 ? q.n0 : n0;
       n1 = lane == 63 ? q.n1 : n1;
       auto D = [&](int i) -> uint32_t { return i < 16 ? q.d[i] : (i == 16 ? n0 : n1); };
-      uint32_t orw = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) orw |= q.d[i];
-      const uint32_t zmask = orw ? 0xFFFFFFFFu : 0u;   // an all-zero window has no candidate but in its last 4 bytes
 #ifdef LDB_STAMPS
-      asm volatile("" ::"v"(zmask));
+      asm volatile("" ::"v"(n0), "v"(n1));
 #endif
       SW_T(tq1);
       SW_ADD(1, tq0, tq1);
-      SW_T(tq2);
-      SW_ADD(2, tq1, tq2);
       // the lane's raw register over its 64 bytes (LP2: conflict-free lane-private tables)
       uint32_t reg = 0;
       if (LDB_SW_ABL & 1) {
@@ -332,69 +327,80 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         else asm volatile("" ::"v"(v));
       }
 #ifdef LDB_STAMPS
-      asm volatile("" ::"v"(v));
+      asm volatile("" ::"v"(v), "v"(pre));
 #endif
-      // candidates: first one ballot for the quarter, then per row (group of 4 dwords) where some lane may
-      // have one; the exact masks kept in registers for the write pass
-      uint32_t ag[4];
+      SW_T(tq2);
+      SW_ADD(3, tq1, tq2);
+      // candidates: a 64-bit map of the lane's positions p = 4 i + j (sw_hits' three conditions, exact). The
+      // status condition for every dword first (4 VALU each); the rest only in 16-B rows where some lane of
+      // the wave has a status byte <= 2 (text values have none: most rows end there). A pair of dwords' masks
+      // packs to 8 bits with one multiply (bit 7 + 8 j of the even dword's mask and 4 + 8 j after the odd
+      // one's shift both move by 24 - 7 j: to bit 24 + j and 28 + j, no two partial products on one bit).
+      uint32_t mlo = 0, mhi = 0;
+      if (!(LDB_SW_ABL & 2)) {
+        uint32_t sv[16], pk[8], ag[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int gi = 0; gi < 4; ++gi) {
-        uint32_t any = 0;
-#pragma unroll
-        for (int k = 1; k <= 4; ++k) any |= small_bytes(D(4 * gi + k));
-        ag[gi] = gi < 3 ? any & zmask : any;
-      }
-      if (LDB_SW_ABL & 2) ag[0] = ag[1] = ag[2] = ag[3] = 0;
-      if (__ballot((ag[0] | ag[1] | ag[2] | ag[3]) != 0u)) {
-        uint32_t m[16];
-        uint32_t cnt = 0;
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t w = D(i + 1);
+          sv[i] = ~(((w & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | w) & 0x80808080u;   // bit 7: the status byte <= 2
+          ag[i >> 2] |= sv[i];
+        }
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) {
+          pk[2 * gi] = pk[2 * gi + 1] = 0u;
           if (__ballot(ag[gi] != 0u)) {
+            uint32_t zp = sw_zero(D(4 * gi)), ce = 0;
 #pragma unroll
-            for (int k = 1; k <= 4; ++k) {
-              uint32_t x = sw_hits(D(4 * gi + k - 1), D(4 * gi + k), D(4 * gi + k + 1));
-              if (gi < 3 || k < 4) x &= zmask;
-              m[4 * gi + k - 1] = x;
-              cnt += (uint32_t)__builtin_popcount(x);
+            for (int k = 0; k < 4; ++k) {
+              const int i = 4 * gi + k;
+              const uint32_t w = D(i + 1), wn = D(i + 2);
+              const uint32_t z = sw_zero(w);
+              const uint32_t nb = __builtin_amdgcn_alignbyte(wn, w, 1) << 7;    // bit 7: ExpiredAt's first byte odd
+              const uint32_t y1 = zp & __builtin_amdgcn_alignbyte(z, zp, 1);      // crc: bytes j, j+1 zero
+              const uint32_t q4 = y1 & __builtin_amdgcn_alignbyte(z & (z >> 8), y1, 2);   // bytes j..j+3 zero
+              const uint32_t c = sv[i] & ~(nb | q4);
+              zp = z;
+              if (k & 1) pk[i >> 1] = (((c >> 3) | (ce >> 7)) * 0x01020408u) >> 24;
+              else ce = c;
             }
-          } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) m[4 * gi + k] = 0;
           }
         }
-        // exclusive prefix of the counts over the lanes, bit by bit (a count is < 128): ballots, no LDS
-        uint32_t ex = 0, tot = 0;
 #pragma unroll
-        for (int bit = 0; bit < 7; ++bit) {
-          const uint64_t bb = __ballot((cnt >> bit) & 1u);
-          ex += sw_rank(bb, lane) << bit;
-          tot += (uint32_t)__builtin_popcountll(bb) << bit;
+        for (int k = 0; k < 4; ++k) {
+          mlo |= pk[k] << (8 * k);
+          mhi |= pk[4 + k] << (8 * k);
         }
+      }
+      const uint32_t cnt = (uint32_t)__builtin_popcount(mlo) + (uint32_t)__builtin_popcount(mhi);
+      // exclusive prefix of the counts over the lanes (DPP scan: rows, then row 15 / lane 31 broadcasts)
+      uint32_t inc = cnt;
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x111, 0xF, 0xF, true);
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x112, 0xF, 0xF, true);
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x114, 0xF, 0xF, true);
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x118, 0xF, 0xF, true);
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x142, 0xA, 0xF, false);
+      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x143, 0xC, 0xF, false);
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      if (tot) {
         if (npend + tot > kSwList) return false;   // too dense for the tier: the region pipeline takes it
         // a lane with a candidate keeps the register of its window's bytes before it (the 256-B window's
         // prefix P at the lane's first byte), so k_sweep_fin gets P(x) of an entry start from <= 63 bytes
         if (cnt && !(LDB_SW_ABL & 8)) p.swpl[(A + wo) >> 6] = pre;
         // the positions, in file order (lane-major: the windows are in lane order)
-        uint32_t j = npend + ex;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          uint32_t x = m[i];
-          if (__ballot(x != 0u)) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              if (x) {
-                hl[j++] = wo + 4u * i + ((uint32_t)__builtin_ctz(x) >> 3);
-                x &= x - 1;
-              }
-            }
-          }
+        uint32_t j = npend + inc - cnt;
+        while (mlo) {
+          hl[j++] = wo + (uint32_t)__builtin_ctz(mlo);
+          mlo &= mlo - 1;
+        }
+        while (mhi) {
+          hl[j++] = wo + 32u + (uint32_t)__builtin_ctz(mhi);
+          mhi &= mhi - 1;
         }
         npend += tot;
       }
 
       SW_T(tq3);
-      SW_ADD(3, tq2, tq3);
+      SW_ADD(2, tq2, tq3);
       return true;
     };
     auto drain = [&] {   // decode while 64 or more candidates wait

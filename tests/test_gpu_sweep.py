@@ -1,0 +1,134 @@
+"""The sweep tier (ldb_sweep.h: k_sweep + k_sweep_fin) against the C oracle, bit-exact.
+
+The tier takes a log from the run prefix's end when its entries vary in length (config 3's Zipf values):
+one streaming pass of CRC window registers and entry-start candidates, a per-run walk, link resolution,
+then per-entry CRC checks from the registers (logfile/log_entry.go:110-121 getEntryCrc, log_file.go:141-143
+the comparison). These cases put corrupt bytes where that algebra changes form: the first and last byte of
+an entry's CRC span, both sides of a 256-B window edge, a 4-KiB group edge and a run edge (16 KiB at 64 MiB),
+and check the tier's share on clean logs so a silent hand-off to the region pipeline cannot pass unseen.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(gpu_engine):
+    return gpu_engine
+
+
+def to_dev(img):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(img, dtype=np.uint8)).to("cuda:0")
+
+
+def check(eng, img, kinds=(0, 1), ios=(0, 1), cap_extra=1024):
+    d = to_dev(img)
+    out = None
+    for io in ios:
+        for kind in kinds:
+            ref, rt = coracle.scan(img, io_type=io, tuple_kind=kind)
+            res, tup = eng.scan_dev(d, io_type=io, kind=kind, cap=ref.n_entries + cap_extra)
+            assert (res.status, res.end_off, res.n_entries) == (ref.status, ref.end_off, ref.n_entries), \
+                (io, kind, res.as_dict(), (ref.status, ref.end_off, ref.n_entries))
+            assert tup.tobytes() == rt.tobytes(), (io, kind)
+            out = res
+    return out
+
+
+@pytest.fixture(scope="module")
+def mixed_log():
+    """16 B .. 256 KiB values (Zipf ranks 1..16384 x 16 B), 64 MiB, zero tail."""
+    img, n, end = coracle.gen_log(64 << 20, 21, ksize=64, value_mode=1, zipf_s=1.05, zipf_max=16384)
+    ref, rt = coracle.scan(img)
+    pos = (rt["pos"] & ((1 << 40) - 1)).astype(np.int64)
+    hs = ((rt["pos"] >> 40) & 63).astype(np.int64)
+    sz = hs + rt["k_size"].astype(np.int64) + rt["v_size"].astype(np.int64)
+    return img, n, pos, sz
+
+
+def test_sweep_takes_mixed_log(eng, mixed_log):
+    img, n, pos, sz = mixed_log
+    assert sz.max() > 128 << 10 and sz.min() < 200   # the size range the tier must carry
+    res = check(eng, img)
+    assert res.status == 2 and res.n_entries == n
+    assert res.n_sweep >= 0.95 * n, res.as_dict()
+
+
+def _entry_over(pos, sz, b, lo_margin=24):
+    """An entry whose CRC span holds bytes b-1 and b well away from its header."""
+    i = int(np.searchsorted(pos, b, side="right")) - 1
+    while i >= 0 and not (pos[i] + lo_margin < b - 1 and b < pos[i] + sz[i]):
+        i -= 1
+    return i
+
+
+@pytest.mark.parametrize("where", ["first", "last", "win_lo", "win_hi", "group", "run_lo", "run_hi"])
+def test_sweep_corruption(eng, mixed_log, where):
+    img, n, pos, sz = mixed_log
+    rng = np.random.default_rng(["first", "last", "win_lo", "win_hi", "group", "run_lo", "run_hi"].index(where) + 40)
+    c = img.copy()
+    if where in ("first", "last"):
+        i = int(rng.integers(n // 4, n - 2))
+        at = int(pos[i]) + 4 if where == "first" else int(pos[i] + sz[i]) - 1
+    else:
+        step = {"win_lo": 256, "win_hi": 256, "group": 4096, "run_lo": 16384, "run_hi": 16384}[where]
+        for _ in range(1000):
+            b = int(rng.integers(len(c) // 8, int(pos[-1]))) // step * step
+            if _entry_over(pos, sz, b) >= 0:
+                break
+        at = b - 1 if where.endswith("_lo") or where == "group" else b
+    c[at] ^= 0x5A
+    ref = coracle.scan(c)[0]
+    assert ref.status == -1   # a CRC failure, not a chain break
+    check(eng, c)
+
+
+def test_sweep_corrupt_header_mid_file(eng, mixed_log):
+    img, n, pos, sz = mixed_log
+    c = img.copy()
+    i = n // 2
+    c[int(pos[i]) + 4] = 7   # Status outside 0..2: the chain's entry is no candidate
+    check(eng, c)
+
+
+@pytest.mark.parametrize("cut", [0.3, 0.71, 0.999])
+def test_sweep_truncated(eng, mixed_log, cut):
+    img, n, pos, sz = mixed_log
+    i = int(n * cut)
+    for at in (int(pos[i]) + 3, int(pos[i]) + 9, int(pos[i] + sz[i]) - 1):
+        check(eng, img[:at].copy(), kinds=(0,))
+
+
+def test_sweep_binary_and_embedded_values(eng):
+    from tests.golden import make_golden as G
+    for seed in range(3):
+        for img in (np.frombuffer(G.binary_values(seed, 3 << 20), np.uint8).copy(),
+                    np.frombuffer(G.embedded(seed, 2 << 20), np.uint8).copy(),
+                    np.frombuffer(G.big_values(seed, 3 << 20), np.uint8).copy(),
+                    np.frombuffer(G.mixed(seed, 2 << 20, maxv=3000), np.uint8).copy()):
+            check(eng, img)
+
+
+def test_sweep_dense_candidates(eng):
+    """Values of 0x02 bytes: every position passes the candidate filter; the tier declines such runs and
+    the region pipeline replays them (results unchanged)."""
+    from tests.golden import make_golden as G
+    rng = random.Random(5)
+    parts, used = [], 0
+    while used < (6 << 20):
+        e = G.ent(key=G.alpha(rng, 16), value=bytes([2]) * rng.randrange(100, 40000))
+        parts.append(e)
+        used += len(e)
+    img = np.frombuffer(G.image(parts, used + 4096), np.uint8).copy()
+    check(eng, img)
+
+
+def test_sweep_writer_mix(eng):
+    w, nw, _ = coracle.gen_writer_log(32 << 20, 17, vmax=65536)
+    check(eng, w)
