@@ -46,9 +46,6 @@ namespace ldb { extern uint64_t g_chain_why[16]; }
 // Timing ablations (tools/build_variants.py abl<N>; results are NOT valid in these builds):
 // bit 0: main-chain CRC without table lookups, bit 1: lane scan and check without lookups,
 // bit 2: no tuple stores. Checks always pass so the fast path runs.
-#ifndef LDB_ABLATE
-#define LDB_ABLATE 0
-#endif
 
 namespace ldb {
 
@@ -116,16 +113,8 @@ LDB_HD uint32_t shift_tab_uniform(const uint32_t* gtab, uint32_t r) {
 
 // register shift by a fixed byte count: 4 lookups in a byte-indexed table set at `off`
 LDB_HD uint32_t shift_tab(const uint32_t* tab, int off, uint32_t r) {
-  if (LDB_ABLATE & 2) return (r << 1) ^ (r >> 3) ^ (uint32_t)off;
-#if LDB_NIB_SHIFT
-  uint32_t x = tab[off + (r & 0xFu)];
-#pragma unroll
-  for (int q = 1; q < 8; ++q) x ^= tab[off + 16 * q + ((r >> (4 * q)) & 0xFu)];
-  return x;
-#else
   return tab[off + (r & 0xFFu)] ^ tab[off + 256 + ((r >> 8) & 0xFFu)] ^ tab[off + 512 + ((r >> 16) & 0xFFu)] ^
          tab[off + 768 + (r >> 24)];
-#endif
 }
 
 // register shift by 8 * n bytes, n in [0, 15] (binary decomposition over the kVSOff tables)
@@ -242,9 +231,7 @@ LDB_HD bool decode_lean_w(const uint32_t* w, uint64_t at, uint32_t p, uint64_t l
   const uint32_t k = uk >> 1, vv = uv >> 1;
   const uint32_t X = p + hs + k + vv;
   ok = ok && !read_eof(len, io, (int64_t)(at + hs), k + vv);   // key/value read (log_file.go:130-139)
-#ifndef LDB_NO_WINCHK   // timing variant only (results invalid near the file end)
   ok = ok && !read_eof(len, io, (int64_t)at, kMaxHeader);   // header window (log_file.go:117-122)
-#endif
   o->crc = w[0];
   o->stat = stat;
   o->hs = hs;
@@ -318,14 +305,14 @@ LDB_HD void crc_slice_cap(const uint32_t* tab, const SliceRows& rows, uint32_t k
       const uint64_t w = ((uint64_t)q[k >> 1].w[2 * (k & 1) + 1] << 32) | q[k >> 1].w[2 * (k & 1)];
       c = (uint32_t)k == kb ? ra : c;
       cw = (uint32_t)k == kb ? w : cw;
-      ra = (LDB_ABLATE & 1) ? ((ra << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(tab, ra, (uint32_t)w, (uint32_t)(w >> 32));
+      ra = crc_step8(tab, ra, (uint32_t)w, (uint32_t)(w >> 32));
     }
     const int kbb = kSplit + k;
     if (kbb < kS / 8) {
       const uint64_t w = ((uint64_t)q[kbb >> 1].w[2 * (kbb & 1) + 1] << 32) | q[kbb >> 1].w[2 * (kbb & 1)];
       c = (uint32_t)kbb == kb ? rb : c;
       cw = (uint32_t)kbb == kb ? w : cw;
-      rb = (LDB_ABLATE & 1) ? ((rb << 3) ^ (uint32_t)w ^ (uint32_t)(w >> 32)) : crc_step8(tab, rb, (uint32_t)w, (uint32_t)(w >> 32));
+      rb = crc_step8(tab, rb, (uint32_t)w, (uint32_t)(w >> 32));
     }
   }
   *ya = ra;
@@ -773,7 +760,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
   };
   wp.each([&](int l) {
     ChainPriv& c = cpriv(l);
-    const bool valid = ((starts >> l) & 1u) && !(LDB_ABLATE & 4);   // an entry (not the pseudo start)
+    const bool valid = ((starts >> l) & 1u);   // an entry (not the pseudo start)
     c.chkB = 0;
     if (!multi || c.cnt <= 1) {
       const uint32_t slot = multi ? c.pre : (uint32_t)__builtin_popcountll(starts & ((1ull << l) - 1));
@@ -852,9 +839,7 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     const uint64_t w10 = (l == kLanes - 1 && c.kb == (uint32_t)(kS / 8))
                              ? (((uint64_t)vword(v, kW + 4) << 32) | vword(v, kW)) : 0ull;   // halo
     c.wB &= ((uint64_t)rows.q[0].w[1] << 32) | rows.q[0].w[0];
-#ifndef LDB_LATE_RELEASE
     release();
-#endif
     crc_slice_cap(v.tab, rows, c.kb, &c.y, &c.ya, &c.cap, &c.wc, w10);
   });
   wp.stamp(13);
@@ -893,13 +878,10 @@ LDB_HD bool region_chained(WP& wp, const View& v, uint8_t* wbuf, WaveSh& sh, Cha
     const uint32_t n = second ? c.kb + 1 - kSplit : c.kb + 1;
     c.y = shift_8n(v.tab, base, n) ^ crc_step8(v.tab, c.cap, (uint32_t)w, (uint32_t)(w >> 32));
   });
-  const int bad = LDB_ABLATE ? -1 : wp.first([&](int l) {
+  const int bad = wp.first([&](int l) {
     const ChainPriv& c = cpriv(l);
     return (c.chk && c.y != 0u) || (c.chkB && c.yB != 0u);
   });
-#ifdef LDB_LATE_RELEASE
-  if (bad < 0) release();
-#endif
   if (bad >= 0) {
     restage();   // the buffer may already hold the next region: reload this one (original bytes)
     return LDB_DECLINE(8);

@@ -52,51 +52,21 @@ constexpr int kKeep = 2;                  // tuples a lane keeps in registers fo
 
 // Table block (uint32 offsets) shared by every wave of a workgroup (LDS) / the emulator.
 //
-// LDB_LP2=1 (round 4, measured and rejected): every 8-byte CRC step is two 2-byte slicing steps on LANE-PRIVATE byte
-// tables (the LP2 block k_uniform introduced in round 3): row i of the 64 KiB block is 256 B, dwords
-// [0, 32) = T16[i] (the register after byte i and one zero byte) and dwords [32, 64) = T8[i] (after
-// byte i alone), each replicated once per bank, and lane l reads dword l mod 32 of a half, so the 32
-// lanes a ds_read_b32 serves at once hit 32 distinct banks whatever the data. One lookup per byte,
-// conflict-free. The register shifts (lane scan, check points, region folds) then use nibble-indexed
-// tables (LDB_NIB_SHIFT: 8 lookups per shift into 16-word tables, which never conflict either), so the
-// whole block is 70 KiB and 14 waves per CU fit beside it. Against the 11/11/10-bit shared tables (61.5 %
-// of k_scan_main's LDS-active cycles at config 3 are bank-conflict cycles) it lost on one box:
-// k_scan_main config 3 3.55 vs 2.65 ms, writer mix 2.19 vs 1.67, config 1 0.313 vs 0.233 (12 waves: the
-// same). Each 8-byte step becomes 4 dependent LDS round trips instead of 2, with 60 % more VALU work, and
-// the nibble shifts double the lookups of the lane scan: the region pipeline is bound by the latency of
-// its dependent lookup chains, not by the conflicts alone.
-//
-// LDB_LP2=0 (default): 8-byte step on 11/11/10-bit chunk tables. LDB_CRC_AB=0: one table set S = shift by 32
-// bits, reg' = S(S(reg ^ w0) ^ w1) (20 KB of LDS). LDB_CRC_AB=1: A = shift by 64 bits and B = shift by
-// 32 bits, reg' = A(reg ^ w0) ^ B(w1) (40 KB, B's lookups off the register chain).
-#ifndef LDB_LP2
-#define LDB_LP2 0
-#endif
-#if LDB_LP2 && !defined(LDB_NIB_SHIFT)
-#define LDB_NIB_SHIFT 1
-#endif
-#ifndef LDB_CRC_AB
-#define LDB_CRC_AB 0
-#endif
-// chained fast path (ldb_chain.h): register shifts. Byte-indexed: 4 tables of 256 each (4 lookups per
-// shift). LDB_NIB_SHIFT=1: 8 nibble-indexed tables of 16 each (8 lookups, but the 16 words of a table
-// sit in 16 distinct banks, so a wave's lookups never conflict).
-#ifndef LDB_NIB_SHIFT
-#define LDB_NIB_SHIFT 0
-#endif
-static_assert(!LDB_LP2 || LDB_NIB_SHIFT, "the LP2 table block uses nibble-indexed shift tables");
-constexpr int kShW = LDB_NIB_SHIFT ? 128 : 1024;   // words per chain shift table
-constexpr int kLP2Off = 0;                          // LDB_LP2: the 64 KiB lane-private block
-constexpr int kLP2Words = LDB_LP2 ? 16384 : 0;
-constexpr int kTAOff = kLP2Words;                   // !LDB_LP2: 2048 + 2048 + 1024: A (LDB_CRC_AB) or S
-constexpr int kTBOff = kTAOff + (LDB_CRC_AB ? 5120 : 0);   // S again, or B
-constexpr int kT8Off = LDB_LP2 ? kLP2Words : kTBOff + 5120;   // 256: byte-at-a-time table (rare paths)
-constexpr int kZSOff = kT8Off + 256;      // !LDB_LP2: 4 x 256: register shift by kS zero bytes (fold chains)
-constexpr int kKOff = kZSOff + (LDB_LP2 ? 0 : 1024);   // kS + 1 (padded to 96): K[n] = register after n zero bytes from ~0
+// 8-byte CRC step on 11/11/10-bit chunk tables: one table set S = shift by 32 bits,
+// reg' = S(S(reg ^ w0) ^ w1) (20 KB of LDS). Chained fast path (ldb_chain.h): register shifts by
+// byte-indexed tables, 4 of 256 each (4 lookups per shift). Measured and rejected alternatives (DESIGN.md,
+// round 4): lane-private 2-byte slicing tables with nibble-indexed shifts (k_scan_main config 3 3.55 vs
+// 2.65 ms: the region pipeline is bound by its dependent lookup chains, not by bank conflicts), and a
+// shift-by-64 / shift-by-32 table pair.
+constexpr int kShW = 1024;                // words per chain shift table
+constexpr int kTBOff = 0;                 // 2048 + 2048 + 1024: S
+constexpr int kT8Off = kTBOff + 5120;     // 256: byte-at-a-time table (rare paths)
+constexpr int kZSOff = kT8Off + 256;      // 4 x 256: register shift by kS zero bytes (fold chains)
+constexpr int kKOff = kZSOff + 1024;      // kS + 1 (padded to 96): K[n] = register after n zero bytes from ~0
 constexpr int kVSOff = kKOff + 96;        // 4 x kShW: shift by 8, 16, 32, 64 bytes (check-point shifts)
 constexpr int kSCOff = kVSOff + 4 * kShW; // 5 x kShW: shift by 2, 4, 8, 16, 32 slices (lane scan)
-constexpr int kZCOff = LDB_NIB_SHIFT ? kSCOff + 5 * kShW : kZSOff;   // shift by 1 slice, chain layout
-constexpr int kTabWords = kSCOff + 5 * kShW + (LDB_NIB_SHIFT ? kShW : 0);
+constexpr int kZCOff = kZSOff;            // shift by 1 slice, chain layout
+constexpr int kTabWords = kSCOff + 5 * kShW;
 constexpr int kTabBytes = kTabWords * 4;
 
 // Force codes for a lane (re)run.
@@ -125,38 +95,19 @@ inline void build_tables(uint32_t* tab) {
     for (int k = 0; k < nbits; ++k) x = (x >> 1) ^ (kPoly & (0u - (x & 1u)));
     return x;
   };
-  if (LDB_LP2) {
-    for (uint32_t i = 0; i < 256; ++i) {
-      const uint32_t t8 = step_bits(i, 8), t16 = step_bits(i, 16);
-      for (int l = 0; l < 32; ++l) {
-        tab[kLP2Off + 64 * i + l] = t16;
-        tab[kLP2Off + 64 * i + 32 + l] = t8;
-      }
-    }
-  } else {
-    const int off[3] = {0, 11, 22}, wid[3] = {11, 11, 10}, base[3] = {0, 2048, 4096};
-    for (int q = 0; q < 3; ++q)
-      for (uint32_t v = 0; v < (1u << wid[q]); ++v) {
-        if (LDB_CRC_AB) tab[kTAOff + base[q] + v] = step_bits(v << off[q], 64);
-        tab[kTBOff + base[q] + v] = step_bits(v << off[q], 32);
-      }
-    for (int q = 0; q < 4; ++q)
-      for (uint32_t b = 0; b < 256; ++b) tab[kZSOff + q * 256 + b] = step_bits(b << (8 * q), 8 * kS);
-  }
+  const int off[3] = {0, 11, 22}, wid[3] = {11, 11, 10}, base[3] = {0, 2048, 4096};
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t v = 0; v < (1u << wid[q]); ++v) tab[kTBOff + base[q] + v] = step_bits(v << off[q], 32);
+  for (int q = 0; q < 4; ++q)
+    for (uint32_t b = 0; b < 256; ++b) tab[kZSOff + q * 256 + b] = step_bits(b << (8 * q), 8 * kS);
   for (uint32_t i = 0; i < 256; ++i) tab[kT8Off + i] = step_bits(i, 8);
   for (int n = 0; n < kVSOff - kKOff; ++n) tab[kKOff + n] = n <= kS ? step_bits(0xFFFFFFFFu, 8 * n) : 0u;
   auto shift_table = [&](int off, int nbytes) {
-    if (LDB_NIB_SHIFT) {
-      for (int q = 0; q < 8; ++q)
-        for (uint32_t b = 0; b < 16; ++b) tab[off + q * 16 + b] = step_bits(b << (4 * q), 8 * nbytes);
-    } else {
-      for (int q = 0; q < 4; ++q)
-        for (uint32_t b = 0; b < 256; ++b) tab[off + q * 256 + b] = step_bits(b << (8 * q), 8 * nbytes);
-    }
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t b = 0; b < 256; ++b) tab[off + q * 256 + b] = step_bits(b << (8 * q), 8 * nbytes);
   };
   for (int i = 0; i < 4; ++i) shift_table(kVSOff + i * kShW, 8 << i);
   for (int i = 0; i < 5; ++i) shift_table(kSCOff + i * kShW, kS << (i + 1));
-  if (LDB_NIB_SHIFT) shift_table(kZCOff, kS);
 }
 
 // ---------------------------------------------------------------- memory views
@@ -201,50 +152,11 @@ LDB_HD uint32_t ctz64(uint64_t x) {
 }
 
 // ---------------------------------------------------------------- CRC
-// This lane's byte offset inside an LP2 row half: 4 (lane mod 32) on the GPU (v_mbcnt, hoisted by the
-// compiler); the emulator reads replica 0 (every replica holds the same word).
-LDB_HD uint32_t lp2_bank() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 31u) << 2;
-#else
-  return 0u;
-#endif
-}
-
-// 4 message bytes w (little-endian, first byte lowest) into raw register reg: two 2-byte slicing steps,
-// reg' = (y >> 16) ^ T16[y & 0xFF] ^ T8[(y >> 8) & 0xFF] from y = x = reg ^ w and again from y.
-// The row address (byte << 8 | lb) is one v_perm_b32, each xor of three one v_bitop3.
-LDB_HD uint32_t lp2_step4(const uint32_t* tab, uint32_t lb, uint32_t reg, uint32_t w) {
-  const uint32_t x = reg ^ w;
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(tab + kLP2Off);
-  auto rd = [&](uint32_t a) { return *reinterpret_cast<const uint32_t*>(b + a); };
-  const uint32_t y = __builtin_amdgcn_bitop3_b32(x >> 16, rd(__builtin_amdgcn_perm(x, lb, 0x0C0C0400u)),
-                                                 rd(__builtin_amdgcn_perm(x, lb, 0x0C0C0500u) + 128u), 0x96);
-  return __builtin_amdgcn_bitop3_b32(y >> 16, rd(__builtin_amdgcn_perm(y, lb, 0x0C0C0400u)),
-                                     rd(__builtin_amdgcn_perm(y, lb, 0x0C0C0500u) + 128u), 0x96);
-#else
-  const uint32_t* t = tab + kLP2Off + (lb >> 2);
-  const uint32_t y = (x >> 16) ^ t[64 * (x & 0xFFu)] ^ t[64 * ((x >> 8) & 0xFFu) + 32];
-  return (y >> 16) ^ t[64 * (y & 0xFFu)] ^ t[64 * ((y >> 8) & 0xFFu) + 32];
-#endif
-}
-
 LDB_HD uint32_t crc_step8(const uint32_t* tab, uint32_t reg, uint32_t w0, uint32_t w1) {
-#if LDB_LP2
-  const uint32_t lb = lp2_bank();
-  return lp2_step4(tab, lb, lp2_step4(tab, lb, reg, w0), w1);
-#elif LDB_CRC_AB
-  const uint32_t x = reg ^ w0;
-  const uint32_t b = tab[kTBOff + (w1 & 0x7FFu)] ^ tab[kTBOff + 2048 + ((w1 >> 11) & 0x7FFu)] ^
-                     tab[kTBOff + 4096 + (w1 >> 22)];
-  return tab[kTAOff + (x & 0x7FFu)] ^ tab[kTAOff + 2048 + ((x >> 11) & 0x7FFu)] ^ tab[kTAOff + 4096 + (x >> 22)] ^ b;
-#else
   const uint32_t x = reg ^ w0;
   const uint32_t y = tab[kTBOff + (x & 0x7FFu)] ^ tab[kTBOff + 2048 + ((x >> 11) & 0x7FFu)] ^
                      tab[kTBOff + 4096 + (x >> 22)] ^ w1;
   return tab[kTBOff + (y & 0x7FFu)] ^ tab[kTBOff + 2048 + ((y >> 11) & 0x7FFu)] ^ tab[kTBOff + 4096 + (y >> 22)];
-#endif
 }
 
 LDB_HD uint32_t mask_from(uint32_t nbytes) {  // bytes [nbytes, 4) kept, nbytes in [0, 4]
@@ -343,18 +255,10 @@ LDB_HD void crc_slice2(const View& v, int B, int tA, uint32_t C, int uB, uint32_
   *rb = b;
 }
 
-// register shift by kS zero bytes (constant-distance GF(2) multiply: 4 byte-table reads, or with
-// LDB_NIB_SHIFT 8 nibble-table reads of the lane scan's one-slice table)
+// register shift by kS zero bytes (constant-distance GF(2) multiply: 4 byte-table reads)
 LDB_HD uint32_t shift_slice(const uint32_t* tab, uint32_t r) {
-#if LDB_NIB_SHIFT
-  uint32_t x = tab[kZCOff + (r & 0xFu)];
-#pragma unroll
-  for (int q = 1; q < 8; ++q) x ^= tab[kZCOff + 16 * q + ((r >> (4 * q)) & 0xFu)];
-  return x;
-#else
   return tab[kZSOff + (r & 0xFF)] ^ tab[kZSOff + 256 + ((r >> 8) & 0xFF)] ^ tab[kZSOff + 512 + ((r >> 16) & 0xFF)] ^
          tab[kZSOff + 768 + (r >> 24)];
-#endif
 }
 
 // ---------------------------------------------------------------- header decode

@@ -37,13 +37,10 @@ namespace {
 #ifndef LDB_WPB
 // 16 waves per CU fit beside the round-3 table block (62.8 KB); the LP2 block (70 KB, ldb_engine.h)
 // leaves room for 14 staging rings of 6.1 KiB
-#define LDB_WPB (LDB_LP2 ? 14 : 16)
+#define LDB_WPB 16
 #endif
 #ifndef LDB_NB
 #define LDB_NB 1
-#endif
-#ifndef LDB_SCAN_BPERM
-#define LDB_SCAN_BPERM 0   // 1: lane shifts of the scan by ds_bpermute instead of DPP / permlane swaps
 #endif
 constexpr int kWPB = LDB_WPB;  // wavefronts per workgroup in k_scan_main
 constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
@@ -132,8 +129,6 @@ struct GpuWave {
     uint32_t y;
     if constexpr (D == 1) {
       y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
-    } else if constexpr (LDB_SCAN_BPERM) {
-      y = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - D) << 2, (int)x);
     } else if constexpr (D == 32) {
       y = __builtin_amdgcn_permlane32_swap(x, x, false, false)[0];
     } else if constexpr (D == 16) {
@@ -234,9 +229,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint
   return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
-#ifndef LDB_ST_NT
-#define LDB_ST_NT 0   // A/B: the region pipeline's tuple stores streaming (nt): measured and rejected, config 3 k_scan_main 2.77 vs 2.75 ms, w 1.246 vs 1.245
-#endif
 constexpr int kNt = 2;   // buffer cache-policy bit: nt (streaming)
 template <int kAux = 0>
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t x, uint32_t y, uint32_t z,
@@ -351,11 +343,8 @@ struct UniRuns {
 // direct form, G - 1 tables "shift by d P bytes" (d = 1 .. G - 1); larger G the tree, lg tables
 // "shift by 2^i P bytes".
 constexpr uint32_t kUniDirectG = 8;
-#ifndef LDB_UNI_CH2
-#define LDB_UNI_CH2 0   // 1: each lane's window as two independent CRC chains (half the dependent LDS round trips)
-#endif
 constexpr uint32_t kUniHalfTab = (kUniDirectG - 1 > kUniLevels ? kUniDirectG - 1 : kUniLevels);   // its table index
-constexpr uint64_t kUniTabWords = (kUniHalfTab + (LDB_UNI_CH2 ? 1 : 0)) * 1024;
+constexpr uint64_t kUniTabWords = kUniHalfTab * 1024;
 LDB_HD inline uint32_t uni_ntab(const UniGeo& g) { return g.G <= kUniDirectG ? g.G - 1 : g.lg; }
 
 // The run prefix's CRC (round 3): 2-byte slicing on LANE-PRIVATE byte tables, so a wave's table reads
@@ -396,13 +385,7 @@ __device__ __forceinline__ void lp2_build(uint8_t* lp2, const uint32_t* __restri
     d[0] = vv; d[1] = vv; d[2] = vv; d[3] = vv;
   }
 }
-#ifndef LDB_UNI_NT
-// 1: k_uniform's row loads carry the non-temporal hint (cache policy bit 1 = "nt" on gfx950). Off: a
-// wave's 6-7 row instructions re-touch the same lines, and nt lines are evicted between them (config
-// 4: 2.03 ms against 0.90, gpurun_out/r2_sweep7.log)
-#define LDB_UNI_NT 0
-#endif
-constexpr int kUniPolicy = LDB_UNI_NT ? 2 : 0;
+constexpr int kUniPolicy = 0;
 __device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
   const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kUniPolicy);
   return make_uint4(v[0], v[1], v[2], v[3]);
@@ -411,10 +394,6 @@ __device__ __forceinline__ uint32_t ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
   return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, kUniPolicy);
 }
 
-#ifndef LDB_UNI_ABL
-#define LDB_UNI_ABL 0   // ablations for attribution only (results wrong): 1 rows loaded, no CRC (xor of the
-                        // words); 2 CRC steps on words made from x, no row loads; both skip the CRC check
-#endif
 constexpr uint64_t kUniReady = 0x5E7A11ED5E7A11EDull;   // dyn[2]: the setup in p.uni is complete
 constexpr uint64_t kUniSetupBytes = 1024;                // UniSetup, then the combine tables
 constexpr uint32_t kUniWin = 8192;                       // image bytes uni_prepare stages (entries 0 and 1)
@@ -447,9 +426,6 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // the first round fails (the run reaches the end of the file as far as sampled, and no refinement round
 // is paid: a file one run covers, configs 2, 4, 5). Probes whose bytes lie at or past probe_hi (a chunked
 // scan's bytes still in flight) are not taken. All threads of the workgroup call it.
-#ifndef LDB_UNI_NOPROBE
-#define LDB_UNI_NOPROBE 0   // A/B: no header probes
-#endif
 // One probe: run r's candidate at x matches the memo (uni_header_ok) -- the header words by aligned
 // dword loads (<= 12 of them, one round trip) instead of byte loads.
 __device__ __forceinline__ bool uni_probe_ok(const Pipe& p, const UniMemo& m, uint64_t x) {
@@ -519,9 +495,6 @@ __device__ __forceinline__ void uni_build_comb(const Pipe& p, const UniGeo& g, u
   if (t < nt) {
     const uint32_t xt = g.G <= kUniDirectG ? p.xw[(t + 1) * g.P] : p.xw[g.P << t];   // d P <= 7 * 96 < kW
     basis[t][bit] = multmodp(xt, 1u << bit);
-  }
-  if (LDB_UNI_CH2 && threadIdx.x >= 1024 - 32) {   // the second chain's length (kUniHalfTab)
-    basis[kUniHalfTab][bit] = multmodp(p.xw[8 * (g.S - g.S / 2)], 1u << bit);
   }
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < (uint32_t)kUniTabWords; e += blockDim.x) {
@@ -609,9 +582,6 @@ __device__ __forceinline__ bool uni_sliceable(uint32_t L) {
 // -- exactly the headers uni_memo accepts (it needs `canonical`), with the same fields. The generic
 // decode run by one lane through readlane is ~2,000 scalar instructions (4.5 K cycles a run at config
 // 1, on the run search's chain); this is a few hundred.
-#ifndef LDB_UNI_FASTMEMO
-#define LDB_UNI_FASTMEMO 1   // 0: the generic decode (uni_memo through readlane), A/B
-#endif
 __device__ __forceinline__ UniMemo uni_memo_wave(const Pipe& p, uint64_t y, uint32_t b) {
   UniMemo m;
   m.ok = 0;
@@ -696,9 +666,8 @@ __device__ __forceinline__ UniMemo uni_memo_wave(const Pipe& p, uint64_t y, uint
 // table load and two multmodp); otherwise only whether it has one. Lane 0 writes q.m (q.g), q.y.
 template <bool kGeo>
 __device__ __forceinline__ bool uni_decode_wave(const Pipe& p, uint64_t y, uint32_t b, UniRun& q) {
-  auto fetch = [&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)b, i); };
   UNI_T(d0);
-  const UniMemo m = LDB_UNI_FASTMEMO ? uni_memo_wave(p, y, b) : uni_memo(fetch, p.len, p.io, y);
+  const UniMemo m = uni_memo_wave(p, y, b);
   UNI_T(d1);
   if (blockIdx.x == 0) UNI_ADD(4, d0, d1);
   UniGeo g{};
@@ -1034,11 +1003,8 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
       uni_build_comb(p, su.g, T, nullptr);   // while workgroup 0 finds the runs
       UNI_T(q3);
       UNI_ADD(18, q2, q3);
-    } else if (!LDB_UNI_NOPROBE) {
+    } else {
       uni_discover(p, ru);
-    } else if (threadIdx.x == 0) {
-      uni_recs(p)[0] = ru.r[0];
-      __hip_atomic_store(&p.dyn[6], uni_word(p, 1ull | kUniFinal), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     UNI_T(s2);
     UNI_ADD(1, s1, s2);
@@ -1054,7 +1020,6 @@ __device__ __forceinline__ bool uni_prepare(const Pipe& p, UniSetup& su, UniRuns
   UNI_T(s2);
   UNI_ADD(1, s1, s2);
   if (!su.g.ok) return false;
-  if (LDB_UNI_NOPROBE) return true;
   const UniRun& r = ru.r[0];
   const uint64_t M = uni_boundary(p, r.m, r.y, r.nc, probe_hi, 64u);   // every workgroup probes: few probes
   if (M < r.nc - 1) {   // a failure of the run: K <= bound
@@ -1159,34 +1124,15 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
     // the header rows the check reads: dwords [0, nw + 2) from ha (the stored crc, nw template words and
     // the funnel's next dword), so 1 row for LazyDB's 10-13-byte Set headers, 3 at most (wave-uniform)
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-#ifdef LDB_UNI_NOHDR   // A/B only (results wrong): no header rows
-    if (false) {
-#else
     if (last) {
-#endif
       h0 = ld16(rs, ha);
-#ifdef LDB_UNI_HDR3   // A/B: the round-2 form, every header row
-      h1 = ld16(rs, ha + 16);
-      h2 = ld16(rs, ha + 32);
-#else
       if (hrows > 1) h1 = ld16(rs, ha + 16);
       if (hrows > 2) h2 = ld16(rs, ha + 32);
-#endif
     }
     const int32_t ws = (int32_t)hx + 4 - (int32_t)t + (int32_t)(j * P);   // < 0 only when base = 0
     const uint32_t a = (uint32_t)ws & ~3u, sh = kAl ? 0u : (uint32_t)ws & 3u;
     uint32_t d[4 * R];
-    if (LDB_UNI_ABL == 2) {
-#pragma unroll
-      for (int i = 0; i < 4 * R; ++i) d[i] = (uint32_t)x * (2u * i + 1u) + j;
-    } else if (LDB_UNI_ABL == 3) {   // the same rows' worth of bytes, lane-contiguous (coalesced)
-      const uint32_t cb = (uint32_t)(b0 - base) + 16u * (uint32_t)lane;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint4 q = ld16(rs, cb + 1024u * r);
-        d[4 * r] = q.x; d[4 * r + 1] = q.y; d[4 * r + 2] = q.z; d[4 * r + 3] = q.w;
-      }
-    } else if (base) {
+    if (base) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const uint4 q = ld16(rs, a + 16 * r);
@@ -1199,41 +1145,21 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
         d[i] = ld4(rs, o < 0 ? kDrop : (uint32_t)o);
       }
     }
-#ifndef LDB_UNI_NOK   // A/B only: no per-batch look at K
     // K for the next batch's exit test: a buffer load with sc1 (past this CU's L1, so it sees other CUs'
     // atomicMin), vector memory only, consumed at the next batch's top so its latency hides behind this
     // batch. (A relaxed atomic load compiled to a flat load, which also counts on lgkmcnt, and the
     // compiler waited for it before issuing the rows.)
     kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
-#endif
     // every row (and header) load in flight before the first use: left alone, the scheduler trades them
     // for registers and issues them one step ahead of the CRC (3 in flight: 1.26 vs 0.82 ms, mb_uni.hip)
     __builtin_amdgcn_sched_barrier(0);
-    // lane j's window: S steps from register 0, lane 0's first t bytes masked. LDB_UNI_CH2: steps
-    // [0, S/2) on register ra, [S/2, S) on reg, joined by ra's shift over the second half's bytes.
-    constexpr int kSA = (LDB_UNI_CH2 && S >= 4) ? S / 2 : 0;
-    uint32_t reg = 0, ra = 0;
+    // lane j's window: S steps from register 0, lane 0's first t bytes masked
+    uint32_t reg = 0;
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      uint32_t w0 = funnel(d[2 * k + 1], d[2 * k], sh), w1 = funnel(d[2 * k + 2], d[2 * k + 1], sh);
-#ifdef LDB_UNI_NOMASK   // A/B only (results wrong): no lead masks
-      if (false) {
-#else
-      {
-#endif
-        w0 &= lm0[k];
-        w1 &= lm1[k];
-      }
-      if (LDB_UNI_ABL == 1 || LDB_UNI_ABL == 3) reg ^= w0 ^ w1;
-      else if (k < kSA) ra = lp2_step4(lp2, lb, lp2_step4(lp2, lb, ra, w0), w1);
-      else reg = lp2_step4(lp2, lb, lp2_step4(lp2, lb, reg, w0), w1);
+      const uint32_t w0 = funnel(d[2 * k + 1], d[2 * k], sh) & lm0[k], w1 = funnel(d[2 * k + 2], d[2 * k + 1], sh) & lm1[k];
+      reg = lp2_step4(lp2, lb, lp2_step4(lp2, lb, reg, w0), w1);
     }
-    if (kSA) {
-      const uint32_t* Th = T + kUniHalfTab * 1024u;
-      reg ^= Th[ra & 0xFFu] ^ Th[256 + ((ra >> 8) & 0xFFu)] ^ Th[512 + ((ra >> 16) & 0xFFu)] ^ Th[768 + (ra >> 24)];
-    }
-    if (LDB_UNI_ABL) asm volatile("" ::"v"(reg));
-#ifndef LDB_UNI_NOCOMB   // A/B only (results wrong): no combine
     if (GG <= kUniDirectG) {
       // direct: lane j shifts its register by (G - 1 - j) P bytes (4 lookups in its own table), then the
       // group's registers are xor-reduced by DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror), so
@@ -1253,7 +1179,6 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
     uni_level<16>(wp, T + 4096, GG, c, reg);
     uni_level<32>(wp, T + 5120, GG, c, reg);
     }
-#endif
     // the header: bytes [4, hs) against the memo's (uni_header_ok). The memo is read from LDS through
     // an opaque offset, so its words stay per-batch VGPR loads instead of SGPRs held across the loop.
     bool ok = false;
@@ -1281,12 +1206,8 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
 #pragma unroll
       for (int i = 0; i < 9; ++i)
         if ((uint32_t)i < nw) diff |= (funnel(hd[i + 2], hd[i + 1], hsh) ^ mv->w[i]) & mv->msk[i];   // wave-uniform
-      ok = ok && diff == 0u && ((reg ^ KL) == ~crc || LDB_UNI_ABL);   // getEntryCrc == stored crc (log_file.go:141-143)
+      ok = ok && diff == 0u && (reg ^ KL) == ~crc;   // getEntryCrc == stored crc (log_file.go:141-143)
     }
-#ifdef LDB_UNI_OKALL   // A/B only (results wrong): every candidate accepted, K untouched
-    asm volatile("" ::"v"(reg), "v"(ok));   // the CRC and the check stay live
-    ok = true;
-#endif
     const uint64_t bad = __ballot((last && mine && !ok) ? 1 : 0);
     if (bad && lane == 0)
       atomicMin((unsigned long long*)F, (unsigned long long)(b * E + ((uint32_t)__builtin_ctzll(bad) >> lg)));
@@ -1345,9 +1266,6 @@ __device__ __forceinline__ void uni_waves(const Pipe& p, const UniRun& su, uint6
 // uni_finish's agent-scope release wrote them back before the last workgroup could go on. A fill wave writing the
 // slice while the other 15 verify -- K re-read every 4096 tuples -- was measured and rejected: config 4
 // k_uniform 0.897 ms against 0.84, 15 verifying waves per CU lose more than the overlap gains.)
-#ifndef LDB_UNI_NTFILL
-#define LDB_UNI_NTFILL 1   // the sweep's tuples as streaming stores (0: plain stores, A/B)
-#endif
 __device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniRuns& ru) {
   __syncthreads();
   const UniRun& rl = ru.r[ru.n - 1];
@@ -1366,8 +1284,7 @@ __device__ __forceinline__ void uni_post_fill(const Pipe& p, const UniRuns& ru) 
     z = z < hi ? z : hi;
     const uint64_t sz = q.m.sz, ya = q.y - q.gbase * sz;   // x of chain entry g: ya + g sz (mod 2^64)
     for (uint64_t g = a + threadIdx.x; g < z; g += blockDim.x) {
-      if (LDB_UNI_NTFILL) store_tuple_nt(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
-      else store_tuple(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
+      store_tuple_nt(out + g, uni_pos(q.m, ya + g * sz), q.m.k, q.m.v);
     }
   }
 }
@@ -1739,30 +1656,6 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     ldb_index_tuple* sc = p.scratch + r * (uint64_t)kRegionCap;
     const __amdgpu_buffer_rsrc_t sc_rs = rsrc_of(sc, (uint32_t)(kRegionCap * sizeof(ldb_index_tuple)));
     ChainPriv cq;
-#if LDB_ABLATE >= 16
-    {   // timing skeletons (results invalid): 16 = DMA only, 32 = + slice CRC, 64 = + lane scan
-      uint32_t acc = 0;
-      if (LDB_ABLATE >= 32) {
-        const SliceRows rows = load_rows(v, lane * kS);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        GpuWave::sync();
-        if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
-        cq.O = crc_slice_raw2(v.tab, rows);
-        if (LDB_ABLATE >= 64) lane_scan(wp, v.tab, [&](int) -> ChainPriv& { return cq; });
-        acc = wp.from(kLanes - 1, [&](int) { return cq.O; });
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        GpuWave::sync();
-        if (i + kNB < total) stage_dma(p.img, p.len, r00 + i + kNB, ring_lds + slot * kBuf, lane);
-      }
-      RegionSum s;
-      s.start = kNone64; s.exitp = 0; s.soff = 0; s.status = kCont; s.count = 0; s.rpre = acc; s.rout = 0;
-      s.scrc = 0; s.sflag = 0;
-      if (lane == 0) p.rs[r] = s;
-      n_fast += 1;
-      continue;
-    }
-#endif
     if (!st.on && zero_region(wp, v)) {
       // all-zero speculative region (a preallocated file tail, fileio.go:66-68): covered, raw register 0
       // (ldb_chain.h zero_region)
@@ -1797,7 +1690,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
     const bool fast = !skip && region_chained(
         wp, v, ring + slot * kBuf, wl->sh, st, [&](int) -> ChainPriv& { return cq; },
         [&](bool valid, uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
-          store16<LDB_ST_NT ? kNt : 0>(sc_rs, valid && !dry ? slot_ * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
+          store16(sc_rs, valid && !dry ? slot_ * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
         },
         [&] {   // the buffer's last read is behind us: stage the run's region i + kNB into it
           const uint64_t nx = i + kNB;
@@ -1836,7 +1729,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
       region_process(
           wp, v, wl->sh, enter, &wl->rs, [&](int) -> LanePriv& { return q; },
           [&](uint32_t slot_, uint64_t pos, uint32_t k, uint32_t vv) {
-            store16<LDB_ST_NT ? kNt : 0>(sc_rs, dry ? kDrop : slot_ * 16u, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
+            store16(sc_rs, dry ? kDrop : slot_ * 16u, (uint32_t)pos, (uint32_t)(pos >> 32), k, vv);
           },
           [] {});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1911,7 +1804,7 @@ struct CohRd {
 // 2. the last workgroup to finish (ctr[6]) re-checks every link over the summaries as they now are
 //    (the same flags, rewritten), and its first wave runs the serial repair() from those flags.
 // ctr[2] = regions re-run (both phases).
-constexpr int kRepWaves = LDB_LP2 ? 14 : 16;   // k_repair: as many waves as fit beside the table block
+constexpr int kRepWaves = 16;   // k_repair: as many waves as fit beside the table block
 template <bool kB>
 __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* __restrict__ pb) {
   LDB_PIPE_SELECT;
@@ -2315,7 +2208,6 @@ __device__ __forceinline__ void compact_body(const Pipe& p) {
     if (dst >= p.cap) break;
     const ldb_index_tuple t = p.scratch[(r0 + lo) * (uint64_t)kRegionCap + (j - s_off[lo])];
     if (p.kind == LDB_TUPLE_ENTRY) decode_entry_global(p, t.pos & 0xFFFFFFFFFFull, reinterpret_cast<ldb_entry*>(p.out) + dst);
-    else if (LDB_ST_NT) store_tuple_nt(reinterpret_cast<ldb_index_tuple*>(p.out) + dst, t.pos, t.k_size, t.v_size);
     else reinterpret_cast<ldb_index_tuple*>(p.out)[dst] = t;
   }
   __syncthreads();   // s_off / s_wsum / s_part are reused by the next block

@@ -269,6 +269,28 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         q.n0 = q.n1 = 0;
       }
     };
+    // The group registers (RG, 4 KiB = one quarter), four quarters at once: row t of rga holds quarter t's 16
+    // window registers (lane 16 t + m <- window m); a 4-level tree in each row (shifts by 256 .. 2048 B)
+    // leaves the group's register in the row's lane 15. One tree per four quarters instead of four levels
+    // per quarter with one active lane.
+    uint32_t rga = 0;
+    const uint32_t bpa = (4u * ((uint32_t)lane & 15u) + 3u) * 4u;   // ds_bpermute: from lane 4 (l mod 16) + 3
+    auto rg_tree = [&](uint32_t qo_last) {
+      uint32_t r = rga, y;
+      y = sw_dpp<0x111>(r);                                   // row_shr:1
+      if (lane & 1) r ^= sw_shift(sh + 2048, y);
+      y = sw_dpp<0x112>(r);                                   // row_shr:2
+      if ((lane & 3) == 3) r ^= sw_shift(sh + 3072, y);
+      y = sw_dpp<0x114>(r);                                   // row_shr:4
+      if ((lane & 7) == 7) r ^= sw_shift(sh + 4096, y);
+      y = sw_dpp<0x118>(r);                                   // row_shr:8
+      if ((lane & 15) == 15) {
+        r ^= sw_shift(sh + 5120, y);
+        if ((uint32_t)(lane >> 4) <= ((qo_last >> 12) & 3u) && !(LDB_SW_ABL & 8))
+          p.swrg[((A + (qo_last & ~0x3FFFu)) >> 12) + (uint32_t)(lane >> 4)] = r;
+      }
+      rga = 0;
+    };
     // one quarter: its candidates appended to the hit list (in file order), each lane's register over its
     // 64 bytes, the window (RW) and quarter (RG) registers. False when the run is too dense for the tier.
     auto proc_q = [&](const QB& q, uint32_t qo) -> bool {
@@ -299,7 +321,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         reg = sw_shift(sh + 8 * 1024, c[0]) ^ sw_shift(sh + 7 * 1024, c[1]) ^ sw_shift(sh + 6 * 1024, c[2]) ^ c[3];
       }
       // a tree over the lanes (DPP): level i joins runs of 2^i lanes with a shift by 64 2^i bytes. Lane 4m+3
-      // ends level 2 with window m's register (RW, 256 B), lane 63 level 6 with the quarter's (RG, 4 KiB)
+      // ends level 2 with window m's register (RW, 256 B); the quarter's 16 go to the group accumulator
       const uint64_t w0 = (A + qo) >> 8;
       uint32_t v = reg, y;
       y = sw_dpp<0x111>(v);                                   // row_shr:1
@@ -314,56 +336,37 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         v ^= sw_shift(sh + 1024, y);
         if (!(LDB_SW_ABL & 8)) p.swrw[w0 + (uint32_t)(lane >> 2)] = v;
       }
-      y = sw_dpp<0x114>(v);                                   // row_shr:4
-      if ((lane & 7) == 7) v ^= sw_shift(sh + 2048, y);
-      y = sw_dpp<0x118>(v);                                   // row_shr:8
-      if ((lane & 15) == 15) v ^= sw_shift(sh + 3072, y);
-      y = sw_dpp<0x142>(v);                                   // row_bcast:15
-      if ((lane & 31) == 31) v ^= sw_shift(sh + 4096, y);
-      y = sw_dpp<0x143>(v);                                   // row_bcast:31
-      if (lane == 63) {
-        v ^= sw_shift(sh + 5120, y);
-        if (!(LDB_SW_ABL & 8)) p.swrg[w0 >> 4] = v;
-        else asm volatile("" ::"v"(v));
+      {   // quarter t of its 16-KiB batch (the run starts on a batch): its RWs to row t of the accumulator
+        const uint32_t t = (qo >> 12) & 3u;
+        const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)bpa, (int)v);
+        if ((uint32_t)(lane >> 4) == t) rga = x;
+        if (t == 3u) rg_tree(qo);
       }
 #ifdef LDB_STAMPS
       asm volatile("" ::"v"(v), "v"(pre));
 #endif
       SW_T(tq2);
       SW_ADD(3, tq1, tq2);
-      // candidates: a 64-bit map of the lane's positions p = 4 i + j (sw_hits' three conditions, exact). The
-      // status condition for every dword first (4 VALU each); the rest only in 16-B rows where some lane of
-      // the wave has a status byte <= 2 (text values have none: most rows end there). A pair of dwords' masks
-      // packs to 8 bits with one multiply (bit 7 + 8 j of the even dword's mask and 4 + 8 j after the odd
-      // one's shift both move by 24 - 7 j: to bit 24 + j and 28 + j, no two partial products on one bit).
+      // candidates: a 64-bit map of the lane's positions p = 4 i + j whose Status byte p + 4 is <= 2
+      // (log_entry.go:9-16; 3 VALU per dword). The decode (flush: decode_lean_w) decides; this only has to
+      // keep every true start, and text values have no such byte. A lane window of zeros holds none whose
+      // status byte is its own (the crc before it would be zero, which the decode rejects). A pair of
+      // dwords' masks packs to 8 bits with one multiply (bit 7 + 8 j of the even dword's mask and 4 + 8 j
+      // after the odd one's shift both move by 24 - 7 j: to bit 24 + j and 28 + j, no two partial products
+      // on one bit).
       uint32_t mlo = 0, mhi = 0;
       if (!(LDB_SW_ABL & 2)) {
-        uint32_t sv[16], pk[8], ag[4] = {0u, 0u, 0u, 0u};
+        uint32_t orw = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) orw |= q.d[i];
+        const uint32_t zk = orw ? 0x80808080u : 0u;
+        uint32_t ce = 0, pk[8];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const uint32_t w = D(i + 1);
-          sv[i] = ~(((w & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | w) & 0x80808080u;   // bit 7: the status byte <= 2
-          ag[i >> 2] |= sv[i];
-        }
-#pragma unroll
-        for (int gi = 0; gi < 4; ++gi) {
-          pk[2 * gi] = pk[2 * gi + 1] = 0u;
-          if (__ballot(ag[gi] != 0u)) {
-            uint32_t zp = sw_zero(D(4 * gi)), ce = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int i = 4 * gi + k;
-              const uint32_t w = D(i + 1), wn = D(i + 2);
-              const uint32_t z = sw_zero(w);
-              const uint32_t nb = __builtin_amdgcn_alignbyte(wn, w, 1) << 7;    // bit 7: ExpiredAt's first byte odd
-              const uint32_t y1 = zp & __builtin_amdgcn_alignbyte(z, zp, 1);      // crc: bytes j, j+1 zero
-              const uint32_t q4 = y1 & __builtin_amdgcn_alignbyte(z & (z >> 8), y1, 2);   // bytes j..j+3 zero
-              const uint32_t c = sv[i] & ~(nb | q4);
-              zp = z;
-              if (k & 1) pk[i >> 1] = (((c >> 3) | (ce >> 7)) * 0x01020408u) >> 24;
-              else ce = c;
-            }
-          }
+          const uint32_t c = ~(((w & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | w) & (i < 15 ? zk : 0x80808080u);
+          if (i & 1) pk[i >> 1] = (((c >> 3) | (ce >> 7)) * 0x01020408u) >> 24;
+          else ce = c;
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -437,6 +440,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       if (i + 1 < nq && !proc_q(Q, (i + 1) * 4096u)) { decl = true; break; }
       drain();
     }
+    if (!decl && (nq & 3u)) rg_tree((nq - 1u) * 4096u);   // a final batch of fewer than four quarters
     SW_T(tl1);
     SW_ADD(5, tl0, tl1);
     if (!decl && npend) flush(npend);

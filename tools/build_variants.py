@@ -1,6 +1,7 @@
-"""Build tuning variants of liblazydb_gpu.so (waves per workgroup, LDS ring depth, stamps).
+"""Build tuning variants of liblazydb_gpu.so (waves per workgroup, LDS ring depth, stamps, -D switches,
+the library as of a git revision, backend scheduler options).
 
-Usage: python tools/build_variants.py w8n2 w12n1 stamps ...  -> lazydb_amd/_lib/var_<name>.so
+Usage: python tools/build_variants.py w8n2 w12n1 stamps git_<rev> def_NAME=V ...  -> lazydb_amd/_lib/var_<name>.so
 Select one at run time with LAZYDB_GPU_LIB=<path>.
 """
 import os
@@ -16,24 +17,9 @@ OUT = os.path.join(ROOT, "lazydb_amd", "_lib")
 
 def build(name: str) -> str:
     defs = []
-    m = re.fullmatch(r"(ab)?(nib)?w(\d+)n(\d+)", name)
+    m = re.fullmatch(r"w(\d+)n(\d+)", name)
     if m:
-        defs = [f"-DLDB_WPB={m.group(3)}", f"-DLDB_NB={m.group(4)}"] + (["-DLDB_CRC_AB=1"] if m.group(1) else []) + \
-               (["-DLDB_NIB_SHIFT=1"] if m.group(2) else [])
-    elif name == "nib":   # nibble-indexed chain shift tables (conflict-free, 31 KB less LDS)
-        defs = ["-DLDB_NIB_SHIFT=1"]
-    elif name == "bperm":
-        defs = ["-DLDB_SCAN_BPERM=1"]
-    elif name == "late":
-        defs = ["-DLDB_LATE_RELEASE=1"]
-    elif name == "bpermlate":
-        defs = ["-DLDB_SCAN_BPERM=1", "-DLDB_LATE_RELEASE=1"]
-    elif name.startswith("abl"):
-        defs = [f"-DLDB_ABLATE={int(name[3:])}"]
-    elif name == "stampsnoprobe":
-        defs = ["-DLDB_STAMPS=1", "-DLDB_UNI_NOPROBE=1"]
-    elif name == "nowin":
-        defs = ["-DLDB_NO_WINCHK=1"]
+        defs = [f"-DLDB_WPB={m.group(1)}", f"-DLDB_NB={m.group(2)}"]
     elif name.startswith("git_"):   # the library as of a commit (A/B timing on one box)
         import tempfile
         rev = name[4:]
