@@ -325,13 +325,8 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       const uint64_t w0 = (A + qo) >> 8;
       uint32_t v = reg, y;
       y = sw_dpp<0x111>(v);                                   // row_shr:1
-      const uint32_t y1 = y;                                  // the previous lane's register
       if (lane & 1) v ^= sw_shift(sh, y);
-      const uint32_t z = sw_dpp<0x111>(v);                    // lane 2 of a quad: lanes 0-1 joined
       y = sw_dpp<0x112>(v);                                   // row_shr:2
-      // the register of the lane's 256-B window before its own 64 bytes (lanes j < lane of its quad joined)
-      const uint32_t jq = (uint32_t)lane & 3u;
-      const uint32_t pre = jq == 0 ? 0u : (jq == 1 ? y1 : (jq == 2 ? z : sw_shift(sh, y) ^ y1));
       if ((lane & 3) == 3) {
         v ^= sw_shift(sh + 1024, y);
         if (!(LDB_SW_ABL & 8)) p.swrw[w0 + (uint32_t)(lane >> 2)] = v;
@@ -343,7 +338,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         if (t == 3u) rg_tree(qo);
       }
 #ifdef LDB_STAMPS
-      asm volatile("" ::"v"(v), "v"(pre));
+      asm volatile("" ::"v"(v));
 #endif
       SW_T(tq2);
       SW_ADD(3, tq1, tq2);
@@ -386,9 +381,11 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
       if (tot) {
         if (npend + tot > kSwList) return false;   // too dense for the tier: the region pipeline takes it
-        // a lane with a candidate keeps the register of its window's bytes before it (the 256-B window's
-        // prefix P at the lane's first byte), so k_sweep_fin gets P(x) of an entry start from <= 63 bytes
-        if (cnt && !(LDB_SW_ABL & 8)) p.swpl[(A + wo) >> 6] = pre;
+        // the lanes before a candidate's lane in its 256-B window keep their 64-B registers, so k_sweep_fin
+        // gets P(x) of an entry start from <= 3 of them and <= 63 bytes
+        const uint64_t cb = __ballot(cnt != 0u);
+        const uint32_t quad = (uint32_t)(cb >> ((uint32_t)lane & 60u)) & 0xFu;
+        if ((quad >> (((uint32_t)lane & 3u) + 1u)) && !(LDB_SW_ABL & 8)) p.swpl[(A + wo) >> 6] = reg;
         // the positions, in file order (lane-major: the windows are in lane order)
         uint32_t j = npend + inc - cnt;
         while (mlo) {
@@ -602,16 +599,23 @@ __device__ __forceinline__ uint32_t sw_prefix(const Pipe& p, const uint32_t* S, 
   return reg;
 }
 
-// P(x) from the lane capture of k_sweep: swpl[x >> 6] is P at x & ~63 (written by the lane whose 64 bytes
-// hold a candidate, so valid for every chain entry's start), then the <= 63 bytes [x & ~63, x)
-__device__ __forceinline__ uint32_t sw_prefix_pl(const Pipe& p, const uint32_t* S, uint64_t x) {
-  const uint64_t ws = x & ~63ull;
-  const uint32_t n = (uint32_t)(x - ws);
+// P(x) from the lane registers k_sweep kept: swpl[i] is the register of image bytes [64 i, 64 i + 64),
+// written for the lanes before a candidate's lane in its 256-B window (so for those of every chain entry's
+// start), folded with shifts by 64 B (T64), then the <= 63 bytes [x & ~63, x)
+__device__ __forceinline__ uint32_t sw_prefix_pl(const Pipe& p, const uint32_t* S, const uint32_t* T64, uint64_t x) {
+  const uint64_t ws = x & ~63ull, l = x >> 6;
+  const uint32_t n = (uint32_t)(x - ws), j = (uint32_t)l & 3u;
   const uint4* row = reinterpret_cast<const uint4*>(p.img + ws);
   uint4 q[4];
+  uint32_t lr[3];
 #pragma unroll
   for (int i = 0; i < 4; ++i) q[i] = 16u * i < n ? row[i] : make_uint4(0, 0, 0, 0);
-  uint32_t reg = p.swpl[x >> 6];
+#pragma unroll
+  for (uint32_t t = 0; t < 3; ++t) lr[t] = t < j ? p.swpl[(l & ~3ull) + t] : 0u;
+  uint32_t reg = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < 3; ++t)
+    if (t < j) reg = sw_shift(T64, reg) ^ lr[t];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const uint32_t lo = 16u * i;
@@ -648,16 +652,16 @@ __device__ __forceinline__ uint32_t sw_fold_win(const Pipe& p, const uint32_t* T
 // P(a) is P(s) stepped over the stored crc (restarting at a window edge); P(e) is the next chain entry's
 // P(s), except after the tier's last entry (e == xe), whose end need not hold a candidate.
 __device__ __forceinline__ bool sw_verify(const Pipe& p, const uint32_t* S, const uint32_t* T256, const uint32_t* T4096,
-                                          uint64_t s, uint64_t sz, uint64_t xe) {
+                                          const uint32_t* T64, uint64_t s, uint64_t sz, uint64_t xe) {
   const uint64_t a = s + 4, e = s + sz;
   const uint32_t crc = sw_word(p, s);
-  uint32_t Pa = sw_prefix_pl(p, S, s);
+  uint32_t Pa = sw_prefix_pl(p, S, T64, s);
 #pragma unroll
   for (uint32_t t = 0; t < 4; ++t) {
     Pa = S[(Pa ^ (crc >> (8 * t))) & 0xFFu] ^ (Pa >> 8);
     if (((s + t + 1) & (kSwW - 1)) == 0) Pa = 0;   // a window edge after the byte: P restarts there
   }
-  const uint32_t Pe = e == xe ? sw_prefix(p, S, e) : sw_prefix_pl(p, S, e);
+  const uint32_t Pe = e == xe ? sw_prefix(p, S, e) : sw_prefix_pl(p, S, T64, e);
   const uint64_t wa = a >> 8, we = e >> 8;
   uint32_t R;
   if (wa == we) {
@@ -769,21 +773,21 @@ __device__ __forceinline__ void sw_finish(const Pipe& p) {
                         // 8 no verify
 #endif
 __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
-  __shared__ __attribute__((aligned(16))) uint32_t st[2 * 1024 + 16 * 256];
+  __shared__ __attribute__((aligned(16))) uint32_t st[2 * 1024 + 16 * 256 + 1024];
   __shared__ int s_last;
   if (scan_done(p)) return;
   SwCtl* c = p.swctl;
   if (c->state != 1) return;
-  if (!(LDB_FIN_ABL & 4)) {   // shift by 256, shift by 4096, slicing-by-16: every load in flight before the stores
-    static_assert(64 * kSwFinWaves == 256, "k_sweep_fin: 256 threads copy 6144 words");
-    uint32_t v[24];
+  if (!(LDB_FIN_ABL & 4)) {   // shift by 256, 4096, slicing-by-16, shift by 64: every load in flight before the stores
+    static_assert(64 * kSwFinWaves == 256, "k_sweep_fin: 256 threads copy 7168 words");
+    uint32_t v[28];
 #pragma unroll
-    for (int k = 0; k < 24; ++k) {
+    for (int k = 0; k < 28; ++k) {
       const uint32_t i = threadIdx.x + 256u * k;
-      v[k] = p.swt[i < 1024 ? 2 * 1024 + i : (i < 2048 ? 6 * 1024 + i - 1024 : kSwSl16Off + i - 2048)];
+      v[k] = p.swt[i < 1024 ? 2 * 1024 + i : (i < 2048 ? 6 * 1024 + i - 1024 : (i < 6144 ? kSwSl16Off + i - 2048 : i - 6144))];
     }
 #pragma unroll
-    for (int k = 0; k < 24; ++k) st[threadIdx.x + 256u * k] = v[k];
+    for (int k = 0; k < 28; ++k) st[threadIdx.x + 256u * k] = v[k];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -807,7 +811,7 @@ __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
       if (!on) continue;
       const uint64_t s = t.pos & 0xFFFFFFFFFFull;
       const uint64_t sz = ((t.pos >> 40) & 0x3Fu) + (uint64_t)t.k_size + t.v_size;
-      if (!(LDB_FIN_ABL & 8) && !sw_verify(p, st + 2048, st, st + 1024, s, sz, xe)) atomicMin((unsigned long long*)&c->fail, (unsigned long long)my);
+      if (!(LDB_FIN_ABL & 8) && !sw_verify(p, st + 2048, st, st + 1024, st + 6144, s, sz, xe)) atomicMin((unsigned long long*)&c->fail, (unsigned long long)my);
       const uint64_t k = ks + my;
       if (k < p.cap) {
         if (p.kind == LDB_TUPLE_ENTRY) decode_entry_global(p, s, reinterpret_cast<ldb_entry*>(p.out) + k);
