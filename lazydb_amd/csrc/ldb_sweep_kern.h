@@ -182,7 +182,8 @@ __device__ uint64_t g_swstamps[16];
 #endif
 
 #ifndef LDB_SW_ABL
-#define LDB_SW_ABL 0   // attribution builds only (results invalid): 1 no CRC, 2 no candidates, 4 no walk, 8 no register
+#define LDB_SW_ABL 0   // attribution builds only (results invalid): 1 no CRC, 2 no candidates, 4 no walk, 16 no window
+                       // tree, 32 no decode, 8 no register
                        // stores
 #endif
 __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
@@ -324,6 +325,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       // ends level 2 with window m's register (RW, 256 B); the quarter's 16 go to the group accumulator
       const uint64_t w0 = (A + qo) >> 8;
       uint32_t v = reg, y;
+      if (!(LDB_SW_ABL & 16)) {
       y = sw_dpp<0x111>(v);                                   // row_shr:1
       if (lane & 1) v ^= sw_shift(sh, y);
       y = sw_dpp<0x112>(v);                                   // row_shr:2
@@ -331,7 +333,8 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         v ^= sw_shift(sh + 1024, y);
         if (!(LDB_SW_ABL & 8)) p.swrw[w0 + (uint32_t)(lane >> 2)] = v;
       }
-      {   // quarter t of its 16-KiB batch (the run starts on a batch): its RWs to row t of the accumulator
+      }
+      if (!(LDB_SW_ABL & 16)) {   // quarter t of its 16-KiB batch (the run starts on a batch): its RWs to row t of the accumulator
         const uint32_t t = (qo >> 12) & 3u;
         const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)bpa, (int)v);
         if ((uint32_t)(lane >> 4) == t) rga = x;
@@ -406,6 +409,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
     auto drain = [&] {   // decode while 64 or more candidates wait
       SW_T(td0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the hit list's stores, before other lanes read them
+      if (LDB_SW_ABL & 32) npend = 0;
       while (npend >= 64 && !decl) {
         flush(64);
         npend -= 64;
