@@ -68,6 +68,23 @@ __device__ __forceinline__ uint64_t sw_ld_sc1(const uint64_t* a) {
   return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup-wide inclusive scans for sw_link (1024 threads = 16 waves): within the wave by lane shifts
+// (ds_bpermute, 6 rounds, no barrier), then each wave adds the totals of the waves before it (one barrier).
+template <class Op, class T>
+__device__ __forceinline__ T sw_wg_scan(T v, T ident, Op op, T* s_wtot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(v, o);
+    if (lane >= o) v = op(v, y);
+  }
+  if (lane == 63) s_wtot[wave] = v;
+  __syncthreads();
+  T pre = ident;
+  for (int w = 0; w < wave; ++w) pre = op(pre, s_wtot[w]);
+  return op(pre, v);
+}
+
 // The links between runs (the last k_sweep workgroup, every thread). The tier's entries are the chain
 // from x_s through the runs in order. A run whose walk found a chain (E_r set; "active") continues it when
 // E_r is the exit of the last active run before it (x_s before run 0's); a run without one is passed when
@@ -75,11 +92,13 @@ __device__ __forceinline__ uint64_t sw_ld_sc1(const uint64_t* a) {
 // run that does neither -- declined, a chain that is not the previous exit's, or an entry start the
 // walk could not take -- at the true chain position entering it (the previous exit), or at the end of an
 // active run whose chain ended inside it. Fully parallel: the last active run before each run is a
-// prefix maximum over the runs, each thread checks a contiguous share.
+// prefix maximum over the runs, each thread checks a contiguous share; the runs' bases a prefix sum.
+// Both scans are wave-level lane shifts plus one pass over the 16 wave totals (four barriers in all).
 __device__ void sw_link(const Pipe& p, const SwGeo& g) {
   __shared__ unsigned long long s_ev;
-  __shared__ int32_t s_la[1024];
-  __shared__ uint64_t s_sum[1024];
+  __shared__ uint64_t s_x[1024];     // X of each thread's last active run
+  __shared__ int32_t s_wmax[16];
+  __shared__ uint64_t s_wsum[16];
   __shared__ uint64_t s_xe;
   constexpr int kPer = (kSwMaxRuns + 1023) / 1024;   // runs per thread (blockDim.x = 1024)
   static_assert(64 * kSwWaves == 1024, "sw_link: one 1024-thread workgroup");
@@ -100,21 +119,24 @@ __device__ void sw_link(const Pipe& p, const SwGeo& g) {
     n[k] = q->n;
     fl[k] = v ? q->flags : kSwDecl;
   }
-  int32_t la = -1;   // the last active run of this thread's share
+  int32_t la = -1;   // the last active run of this thread's share, and its exit
+  uint64_t lx = 0;
 #pragma unroll
   for (int k = 0; k < kPer; ++k)
-    if (!(fl[k] & kSwDecl) && E[k] != ~0ull) la = (int32_t)(r0 + k);
-  s_la[tid] = la;
+    if (!(fl[k] & kSwDecl) && E[k] != ~0ull) {
+      la = (int32_t)(r0 + k);
+      lx = X[k];
+    }
+  s_x[tid] = lx;
   if (tid == 0) s_ev = ~0ull;
-  __syncthreads();
-  for (uint32_t o = 1; o < nt; o <<= 1) {   // prefix maximum over the threads
-    const int32_t y = tid >= o ? s_la[tid - o] : -1;
-    __syncthreads();
-    if (y > s_la[tid]) s_la[tid] = y;
-    __syncthreads();
+  auto mx = [](int32_t a, int32_t b) { return a > b ? a : b; };
+  const int32_t incl = sw_wg_scan<decltype(mx), int32_t>(la, -1, mx, s_wmax);   // (its barrier publishes s_x)
+  int32_t prev0 = __shfl_up(incl, 1);   // the last active run before this share
+  if ((tid & 63u) == 0) {
+    prev0 = -1;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) prev0 = mx(prev0, s_wmax[w]);
   }
-  const int32_t prev0 = tid ? s_la[tid - 1] : -1;   // the last active run before this share
-  uint64_t T = prev0 >= 0 ? p.swrun[prev0].X : g.xs;   // the chain's position entering the share
+  uint64_t T = prev0 >= 0 ? s_x[(uint32_t)prev0 / kPer] : g.xs;   // the chain's position entering the share
   uint64_t ev = ~0ull, xe_mine = 0;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
@@ -133,22 +155,15 @@ __device__ void sw_link(const Pipe& p, const SwGeo& g) {
   __syncthreads();
   const uint64_t evm = s_ev;
   if (evm != ~0ull && ev == evm) s_xe = xe_mine;
-  if (evm == ~0ull && tid == nt - 1) s_xe = s_la[nt - 1] >= 0 ? p.swrun[s_la[nt - 1]].X : g.xs;
-  __syncthreads();
-  const uint64_t ncov = evm == ~0ull ? nrun : ((evm & 1) ? evm / 2 + 1 : evm / 2), xe = s_xe;
+  if (evm == ~0ull && tid == nt - 1) s_xe = incl >= 0 ? s_x[(uint32_t)incl / kPer] : g.xs;
   // bases: an exclusive prefix of the runs' entry counts (inactive runs count 0)
+  const uint64_t ncov = evm == ~0ull ? nrun : ((evm & 1) ? evm / 2 + 1 : evm / 2);
   uint64_t sum = 0;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) sum += r0 + k < ncov ? n[k] : 0;
-  s_sum[tid] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < nt; o <<= 1) {   // Hillis-Steele over the threads' sums
-    const uint64_t y = tid >= o ? s_sum[tid - o] : 0;
-    __syncthreads();
-    s_sum[tid] += y;
-    __syncthreads();
-  }
-  uint64_t b = s_sum[tid] - sum;
+  auto add = [](uint64_t a, uint64_t b) { return a + b; };
+  const uint64_t tot = sw_wg_scan<decltype(add), uint64_t>(sum, 0ull, add, s_wsum);   // (its barrier publishes s_xe)
+  uint64_t b = tot - sum;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     if (r0 + k < ncov) p.swrun[r0 + k].base = b;
@@ -157,8 +172,8 @@ __device__ void sw_link(const Pipe& p, const SwGeo& g) {
   if (tid == nt - 1) {
     c->xs = g.xs;
     c->ks = g.ks;
-    c->xe = xe;
-    c->ke = g.ks + s_sum[nt - 1];
+    c->xe = s_xe;
+    c->ke = g.ks + tot;
     c->ncov = ncov;
     c->nrun = nrun;
     c->stop = ~0ull;
@@ -325,6 +340,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       // ends level 2 with window m's register (RW, 256 B); the quarter's 16 go to the group accumulator
       const uint64_t w0 = (A + qo) >> 8;
       uint32_t v = reg, y;
+      if (LDB_SW_ABL & 16) asm volatile("" ::"v"(reg));   // (the rows stay loaded in attribution builds)
       if (!(LDB_SW_ABL & 16)) {
       y = sw_dpp<0x111>(v);                                   // row_shr:1
       if (lane & 1) v ^= sw_shift(sh, y);

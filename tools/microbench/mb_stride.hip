@@ -28,18 +28,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-template <int S, int LDSK>
+template <int S, int LDSK, int QB = 4>
 __global__ __launch_bounds__(1024) void k_stride(const uint8_t* img, uint64_t nbatch, uint32_t* sink) {
   __shared__ uint32_t pad[LDSK ? LDSK * 256 : 1];
   if (LDSK) pad[threadIdx.x] = threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int R = S / 16;             // rows per lane per quarter
-  constexpr int Q = 16384 / (64 * S);   // quarters per batch
+  constexpr int Q = QB * 4096 / (64 * S);   // quarters per batch (QB KiB-quarters in flight per wave)
   uint32_t acc = 0;
   const uint64_t gw = (uint64_t)blockIdx.x * 16 + wave, nw = (uint64_t)gridDim.x * 16;
   const uint64_t per = (nbatch + nw - 1) / nw;
   for (uint64_t b = gw * per; b < (gw + 1) * per && b < nbatch; ++b) {
-    const __amdgpu_buffer_rsrc_t rs = rsrc(img + b * 16384, 16384);
+    const __amdgpu_buffer_rsrc_t rs = rsrc(img + b * (QB * 4096), QB * 4096);
     uint32_t d[64];
 #pragma unroll
     for (int t = 0; t < Q; ++t)
@@ -50,22 +50,22 @@ __global__ __launch_bounds__(1024) void k_stride(const uint8_t* img, uint64_t nb
       }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < 64; ++i) acc = (acc << 1 | acc >> 31) ^ d[i];
+    for (int i = 0; i < QB * 16; ++i) acc = (acc << 1 | acc >> 31) ^ d[i];
   }
   if (LDSK) acc ^= pad[(threadIdx.x + 1) & 1023];
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
-template <int S, int LDSK>
+template <int S, int LDSK, int QB = 4>
 double run(const uint8_t* img, uint64_t bytes, uint32_t* sink, int ncu) {
-  const uint64_t nb = bytes / 16384;
+  const uint64_t nb = bytes / (QB * 4096);
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_stride<S, LDSK>), dim3(ncu), dim3(1024), 0, 0, img, nb, sink);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_stride<S, LDSK, QB>), dim3(ncu), dim3(1024), 0, 0, img, nb, sink);
   CK(hipEventRecord(a, 0));
   const int it = 20;
-  for (int i = 0; i < it; ++i) hipLaunchKernelGGL((k_stride<S, LDSK>), dim3(ncu), dim3(1024), 0, 0, img, nb, sink);
+  for (int i = 0; i < it; ++i) hipLaunchKernelGGL((k_stride<S, LDSK, QB>), dim3(ncu), dim3(1024), 0, 0, img, nb, sink);
   CK(hipEventRecord(b, 0));
   CK(hipEventSynchronize(b));
   float ms = 0;
@@ -83,6 +83,9 @@ int main() {
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
   const int ncu = prop.multiProcessorCount;
+  std::printf("stride 64, 1 quarter (4 KiB) per wave in flight: %.0f GB/s\n", run<64, 120, 1>(img, bytes, sink, ncu));
+  std::printf("stride 64, 2 quarters (8 KiB): %.0f GB/s\n", run<64, 120, 2>(img, bytes, sink, ncu));
+  std::printf("stride 64, 3 quarters (12 KiB): %.0f GB/s\n", run<64, 120, 3>(img, bytes, sink, ncu));
   std::printf("stride 16: %.0f GB/s\n", run<16, 120>(img, bytes, sink, ncu));
   std::printf("stride 32: %.0f GB/s\n", run<32, 120>(img, bytes, sink, ncu));
   std::printf("stride 64: %.0f GB/s\n", run<64, 120>(img, bytes, sink, ncu));
