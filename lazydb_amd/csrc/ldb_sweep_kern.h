@@ -198,7 +198,7 @@ __device__ uint64_t g_swstamps[16];
 
 #ifndef LDB_SW_ABL
 #define LDB_SW_ABL 0   // attribution builds only (results invalid): 1 no CRC, 2 no candidates, 4 no walk, 16 no window
-                       // tree, 32 no decode, 8 no register
+                       // tree, 32 no decode, 64 no streaming, 128 no stop poll, 256 no look-ahead load, 8 no register
                        // stores
 #endif
 __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         const uint4 x = ld16(irs, qo + 64u * (uint32_t)lane + 16u * k);
         q.d[4 * k] = x.x; q.d[4 * k + 1] = x.y; q.d[4 * k + 2] = x.z; q.d[4 * k + 3] = x.w;
       }
-      if (lane == 63) {   // one lane: the look-ahead costs one dwordx2 load of a single address
+      if (lane == 63 && !(LDB_SW_ABL & 256)) {   // one lane: the look-ahead costs one dwordx2 load of a single address
         const v2u32 x = __builtin_amdgcn_raw_buffer_load_b64(irs, qo + 4096u, 0, 0);
         q.n0 = x[0];
         q.n1 = x[1];
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       SW_T(td1);
       SW_ADD(4, td0, td1);
     };
-    const uint32_t nq = (uint32_t)((B - A + 4095) / 4096);
+    const uint32_t nq = (LDB_SW_ABL & 64) ? 0u : (uint32_t)((B - A + 4095) / 4096);
     SW_T(tl0);
     QB P, Q;
     if (nq > 0) load_q(P, 0);
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         if (stop < r) { decl = true; break; }
       }
       if (i + 1 < nq) load_q(Q, (i + 1) * 4096u);
-      kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
+      if (!(LDB_SW_ABL & 128)) kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
       __builtin_amdgcn_sched_barrier(0);
       if (!proc_q(P, i * 4096u)) { decl = true; break; }
       if (i + 2 < nq) load_q(P, (i + 2) * 4096u);
