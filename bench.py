@@ -261,15 +261,16 @@ def measure_traffic(img, cap, args, kernel):
     try:
         img.tofile(path)
         # the device path's instance only (k_uniform<false, false>, k_scan_main<false>): not k_uniform_fill
+        tag = kernel + ("(" if kernel == "k_sweep" else "<false")   # k_sweep is no template
         cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--pmc", "FETCH_SIZE", "--kernel-include-regex",
-               kernel + "<false", "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
+               kernel + ("\\(" if kernel == "k_sweep" else "<false"), "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", f"{path}:{cap}", "--io", str(args.io), "--kind", str(args.kind)]
         p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
         per = {}
         for f in glob.glob(os.path.join(tmp, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    if kernel + "<false" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+                    if tag in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
                         key = r.get("Dispatch_Id") or r.get("Dispatch_ID") or r.get("Correlation_Id")
                         per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
         if not per:
@@ -702,27 +703,30 @@ def timed_scans(eng, S, fid, args, steps, world, stream):
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
+    sw_ms, fin_ms = eng.timing_sweep()   # (before timing_split, which resets the accumulators)
     run_ms, main_ms, total_ms, _ = eng.timing_split(0)
+    timed_scans.sweep_ms, timed_scans.fin_ms = sw_ms, fin_ms
     timed_scans.median_ms = med_ms
     timed_scans.median_iters = len(evs)
     return t, run_ms, main_ms, total_ms
 
 
-def dominant_kernel(S, r, kind, run_ms, main_ms):
+def dominant_kernel(S, r, kind, run_ms, main_ms, sweep_ms=0.0):
     """The scan's dominant kernel and its algorithmic bytes per launch (the bytes of
     the accepted entries it verified). k_uniform (the run prefix) verified entries [0, n_run), i.e.
-    bytes [0, x0); k_scan_main (the region pipeline) the rest, [x0, end_off)."""
-    n_run, n, end = int(r.n_run), int(r.n_entries), int(r.end_off)
-    if n_run == 0:
-        x0 = 0
-    elif n_run >= n:
-        x0 = end
-    else:
-        tsz = 16 if kind == 0 else 48
-        x0 = int.from_bytes(S.out[n_run * tsz: n_run * tsz + 8].cpu().numpy().tobytes(), "little") & ((1 << 40) - 1)
-    if run_ms >= main_ms:
-        return "k_uniform", x0, run_ms
-    return "k_scan_main", end - x0, main_ms
+    bytes [0, x0); k_sweep (the sweep tier, ldb_sweep.h) the next n_sweep, bytes [x0, x1); k_scan_main
+    (the region pipeline) the rest, [x1, end_off)."""
+    n_run, n_sw, n, end = int(r.n_run), int(r.n_sweep), int(r.n_entries), int(r.end_off)
+    tsz = 16 if kind == 0 else 48
+
+    def start_of(k):   # image offset of entry k (end_off past the last one)
+        if k >= n:
+            return end
+        return int.from_bytes(S.out[k * tsz: k * tsz + 8].cpu().numpy().tobytes(), "little") & ((1 << 40) - 1)
+    x0 = start_of(n_run) if n_run else 0
+    x1 = start_of(n_run + n_sw) if n_sw else x0
+    best = max((run_ms, "k_uniform", x0), (sweep_ms, "k_sweep", x1 - x0), (main_ms, "k_scan_main", end - x1))
+    return best[1], best[2], best[0]
 
 
 def prepare(eng, cfg, rank, args, dev, verify: bool):
@@ -759,7 +763,8 @@ def run_leg(eng, cfg, args, dev):
     import torch
     img, S, r, verified, workload, _ = prepare(eng, cfg, 0, args, dev, not args.no_verify)
     t, run_ms, main_ms, total_ms = timed_scans(eng, S, 1, args, args.leg_steps, 1, torch.cuda.current_stream(dev))
-    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms)
+    sw_ms, fin_ms = timed_scans.sweep_ms, timed_scans.fin_ms
+    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms, sw_ms)
     step = t / args.leg_steps
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else None
     leg = {"config": cfg, "workload": workload, "file_bytes": int(img.size), "bytes_scanned": int(r.end_off),
@@ -768,8 +773,9 @@ def run_leg(eng, cfg, args, dev):
            "mentries_per_s": round(int(r.n_entries) / step / 1e6, 2),
            "median_event_ms": round(timed_scans.median_ms, 4),
            "GiB_per_s_median": round(int(r.end_off) / (timed_scans.median_ms * 1e-3) / 2**30, 3),
-           "k_uniform_ms": round(run_ms, 4), "k_scan_main_ms": round(main_ms, 4), "pipeline_ms": round(total_ms, 4),
-           "run_entries": int(r.n_run), "roofline_kernel": kname, "roofline_bytes": kbytes,
+           "k_uniform_ms": round(run_ms, 4), "k_sweep_ms": round(sw_ms, 4), "k_sweep_fin_ms": round(fin_ms, 4),
+           "k_scan_main_ms": round(main_ms, 4), "pipeline_ms": round(total_ms, 4),
+           "run_entries": int(r.n_run), "sweep_entries": int(r.n_sweep), "roofline_kernel": kname, "roofline_bytes": kbytes,
            "roofline_frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
            "status": int(r.status), "fast_regions": int(r.n_fast), "regions": int(r.n_regions),
            "regions_rerun": int(r.n_repairs), "io_type": "FileIO" if S.io == 0 else "Mmap",
@@ -810,7 +816,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     t, run_ms, main_ms, total_ms = timed_scans(eng, S, 1 + rank, args, args.steps, world, stream)
     med_ms, med_iters = timed_scans.median_ms, timed_scans.median_iters
-    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms)
+    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms, timed_scans.sweep_ms)
     # practical HBM-read ceiling on this box: a read-only reduction over the same image, after the
     # timed region
     ceiling = eng.read_ceiling(S.d, 20) if rank == 0 else None

@@ -3137,6 +3137,20 @@ int ldb_debug_ustamps(uint64_t* out, int reset) {
 }
 #endif
 
+// Diagnostics (not in the C ABI header): the sweep tier's run records and control block of the last scan of
+// length len on this context, after it completed (tools/sweep_debug.py).
+extern "C" int ldb_debug_sweep_state(ldb_ctx* c, uint64_t len, void* h_runs, uint64_t max_runs, void* h_ctl) {
+  if (!c || !h_runs || !h_ctl) return LDB_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
+  const WsLayout L = layout(len);
+  if (L.total > c->ws_bytes) return LDB_ERR_ARG;
+  const uint64_t n = max_runs < (uint64_t)kSwMaxRuns ? max_runs : (uint64_t)kSwMaxRuns;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h_runs, c->ws + L.o_swrun, n * sizeof(SwRun), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(h_ctl, c->ws + L.o_swctl, sizeof(SwCtl), hipMemcpyDeviceToHost) != hipSuccess)
+    return LDB_ERR_HIP;
+  return LDB_OK;
+}
+
 int ldb_read_ceiling(ldb_ctx* c, const uint8_t* d_image, uint64_t len, int iters, double* gbps) {
   if (!c || !gbps || (len && !d_image) || iters < 1 || (uintptr_t)d_image % 16) return LDB_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;

@@ -490,31 +490,44 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       if (r == 0) E = g.xs;
       else if (ncand) E = sw_readlane64(lp, 0);
       uint64_t x = E;
-      while (E != ~0ull) {
-        if (x >= B) { X = x; break; }
-        for (;;) {   // the block holding x, or the last
+      // the block holding x (or the last): blocks are searched forward from the current one
+      auto seek = [&](uint64_t xx) {
+        for (;;) {
           const uint32_t nv = ncand - bi * 64u < 64u ? ncand - bi * 64u : 64u;
           const uint64_t lastp = nv ? sw_readlane64(lp, (int)nv - 1) : 0;
-          if (nv == 0 || lastp >= x || (bi + 1) * 64u >= ncand) break;
+          if (nv == 0 || lastp >= xx || (bi + 1) * 64u >= ncand) break;
           if (dirty) write_blk(bi);
           dirty = false;
           load_blk(++bi);
         }
-        const uint64_t mt = __ballot(lp == x);
-        if (mt) {
-          const int L = __builtin_ctzll(mt);
-          if (lane == L) {
-            rec.y = (rec.y & 0x0FFFFFFFu) | (tag << 28);
-            dirty = true;
+      };
+      // A speculated chain that leaves the run after fewer than kSwTrust entries is weak: a false start
+      // inside a value can claim a size past the run's end. Later starts are tried, and the first weak
+      // chain is taken back (re-walked, so its records carry its tag again) only if none of them holds.
+      uint64_t wE = ~0ull;
+      uint32_t wtag = 0;
+      while (E != ~0ull) {
+        if (x >= B) {
+          if (r == 0 || cnt >= kSwTrust || tag == 15) { X = x; break; }
+          if (wE == ~0ull) { wE = E; wtag = tag; }
+        } else {
+          seek(x);
+          const uint64_t mt = __ballot(lp == x);
+          if (mt) {
+            const int L = __builtin_ctzll(mt);
+            if (lane == L) {
+              rec.y = (rec.y & 0x0FFFFFFFu) | (tag << 28);
+              dirty = true;
+            }
+            ++cnt;
+            x += (uint32_t)__builtin_amdgcn_readlane((int)lsz, L);
+            continue;
           }
-          ++cnt;
-          x += (uint32_t)__builtin_amdgcn_readlane((int)lsz, L);
-          continue;
+          // x is no candidate: the chain ends here (run 0's is the true chain from x_s; a speculated one
+          // that held kSwTrust entries is kept and its end checked by the links), or the speculated first
+          // entry was false and the next candidate is tried
+          if (r == 0 || cnt >= kSwTrust || tag == 15) { fl |= kSwDead; X = x; break; }
         }
-        // x is no candidate: the chain ends here (run 0's is the true chain from x_s; a speculated one
-        // that held kSwTrust entries is kept and its end checked by the links), or the speculated first
-        // entry was false and the next candidate is tried
-        if (r == 0 || cnt >= kSwTrust || tag == 15) { fl |= kSwDead; X = x; break; }
         ++si;
         ++tag;
         cnt = 0;
@@ -524,6 +537,27 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         bi = si / 64u;
         load_blk(bi);
         E = x = sw_readlane64(lp, (int)(si % 64u));
+      }
+      if (E == ~0ull && wE != ~0ull) {
+        if (dirty) write_blk(bi);
+        dirty = false;
+        bi = 0;
+        load_blk(0);
+        E = x = wE;
+        tag = wtag;
+        cnt = 0;
+        while (x < B) {
+          seek(x);
+          const uint64_t mt = __ballot(lp == x);
+          const int L = __builtin_ctzll(mt);   // (a record: this chain was walked before)
+          if (lane == L) {
+            rec.y = (rec.y & 0x0FFFFFFFu) | (tag << 28);
+            dirty = true;
+          }
+          ++cnt;
+          x += (uint32_t)__builtin_amdgcn_readlane((int)lsz, L);
+        }
+        X = x;
       }
       if (dirty) write_blk(bi);
     }
