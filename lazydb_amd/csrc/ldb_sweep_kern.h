@@ -373,12 +373,14 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         uint32_t orw = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) orw |= q.d[i];
-        const uint32_t zk = orw ? 0x80808080u : 0u;
+        // (the last dword's candidates, p = 60..63, need a nonzero crc byte: here or in the next window's first
+        // dword -- a zero tail would otherwise offer 4 per window and flood the list)
+        const uint32_t zk = orw ? 0x80808080u : 0u, zk16 = (orw | n0) ? 0x80808080u : 0u;
         uint32_t ce = 0, pk[8];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const uint32_t w = D(i + 1);
-          const uint32_t c = ~(((w & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | w) & (i < 15 ? zk : 0x80808080u);
+          const uint32_t c = ~(((w & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | w) & (i < 15 ? zk : zk16);
           if (i & 1) pk[i >> 1] = (((c >> 3) | (ce >> 7)) * 0x01020408u) >> 24;
           else ce = c;
         }
