@@ -7,24 +7,33 @@
 // Zipf values of 16 B - 64 KiB, 5.2 KB per entry on average), where the region pipeline spends its time
 // on per-region machinery around one or two entry starts. It splits the work by what it depends on:
 //
-//   k_sweep      one streaming pass over the image, 16-B rows straight into registers (the run
-//                prefix's load pattern): every lane CRC-32s its 256-B window from register 0 on the
-//                lane-private LP2 tables (RW: one raw register per window, RG: per 16 windows by a DPP
-//                tree), and tests every byte position as a header candidate by its first bytes
-//                (Status <= 2, ExpiredAt >= 0, crc != 0: SWAR masks). Candidates are decoded 64 at a
-//                time (decode_lean_w, the region pipeline's Go-exact decode of canonical headers, with
-//                the IOController bounds) into the wave's slab: index tuples in file order.
+//   k_sweep      one streaming pass over the image, 16-B rows straight into registers: lane l of a wave
+//                holds bytes [64 l, 64 l + 64) of a 4-KiB quarter (four row instructions per quarter, the
+//                next quarter in flight while one is processed). Every lane CRC-32s its 64 bytes from
+//                register 0 on the lane-private LP2 tables (four 16-B row chains joined by shifts); a
+//                2-level DPP tree gives each 256-B window's raw register (RW), and the windows of four
+//                quarters at a time go to one row of an accumulator (ds_bpermute) whose 4-level row tree
+//                gives each 4-KiB group's register (RG). Every byte position is a header candidate when
+//                its Status byte (p + 4) is <= 2 (three VALU per dword; a zero window offers none): the
+//                positions go to a per-wave list in LDS, in file order, and are decoded 64 at a time
+//                (decode_lean_w, the region pipeline's Go-exact decode of canonical headers, with the
+//                IOController bounds) into the wave's slab of index tuples. The lanes of a 256-B window
+//                before a candidate's lane keep their 64-B registers (LR, one word per 64 B), so the
+//                prefix of an entry start costs k_sweep_fin at most 3 registers and 63 bytes.
 //                Each wave owns a contiguous run of the image and then walks its slab: from the run's
 //                first candidate (run 0: the chain's entry point x_s), each entry's end must be the
-//                next candidate. The last workgroup checks the links between runs (a run's exit must
-//                be the next run's first entry) and fixes where the tier ends: at the first broken
-//                link, declined run (too many candidates, slab full) or chain end.
-//   k_sweep_fin  one lane per chain entry: its CRC from the window registers (a Horner fold over the
-//                RW / RG registers between its span's ends, the partial windows at both ends by
-//                slicing-by-16 over at most 255 bytes each, two GF(2) multiplies), the tuple written at
-//                its index. The last workgroup writes the result when the tier ends on a terminal
-//                (io.EOF, ErrLogEndOfFile, a failed CRC) or hands the rest to the region pipeline: K
-//                entries and position x, as the run prefix does (dyn[0], dyn[5]).
+//                next candidate; a speculated start whose chain leaves the run after fewer than
+//                kSwTrust entries is weak (a false start inside a binary value can claim a size past
+//                the run), and later starts are tried first. The last workgroup checks the links
+//                between runs (a run's exit must be the next run's first entry; wave-level scans) and
+//                fixes where the tier ends: at the first broken link, declined run (too many
+//                candidates, slab full) or chain end.
+//   k_sweep_fin  one lane per chain entry: its CRC from the registers (the start's prefix from LR and at
+//                most 63 bytes, the partial windows folded by RW, whole groups by RG, the end's prefix
+//                likewise, two GF(2) multiplies), the tuple written at its index. The last workgroup
+//                writes the result when the tier ends on a terminal (io.EOF, ErrLogEndOfFile, a failed
+//                CRC) or hands the rest to the region pipeline: K entries and position x, as the run
+//                prefix does (dyn[0], dyn[5]).
 //
 // Results are the serial scan's for every input: a candidate is decoded exactly as decodeHeader
 // would, a chain entry is accepted only when its header, bounds and CRC check, and wherever the tier
