@@ -369,6 +369,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       // after the odd one's shift both move by 24 - 7 j: to bit 24 + j and 28 + j, no two partial products
       // on one bit).
       uint32_t mlo = 0, mhi = 0;
+      bool has = false;
       if (!(LDB_SW_ABL & 2)) {
         uint32_t orw = 0;
 #pragma unroll
@@ -376,48 +377,55 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         // (the last dword's candidates, p = 60..63, need a nonzero crc byte: here or in the next window's first
         // dword -- a zero tail would otherwise offer 4 per window and flood the list)
         const uint32_t zk = orw ? 0x80808080u : 0u, zk16 = (orw | n0) ? 0x80808080u : 0u;
-        uint32_t ce = 0, pk[8];
+        uint32_t cm[16], any = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const uint32_t w = D(i + 1);
-          const uint32_t c = ~(((w & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | w) & (i < 15 ? zk : zk16);
-          if (i & 1) pk[i >> 1] = (((c >> 3) | (ce >> 7)) * 0x01020408u) >> 24;
-          else ce = c;
+          cm[i] = ~(((w & 0x7C7C7C7Cu) + 0x7F7F7F7Fu) | w) & (i < 15 ? zk : zk16);
+          any |= cm[i];
         }
+        has = __ballot(any != 0u) != 0;
+        if (has) {   // (text values: about half the quarters hold no header byte <= 2)
+          uint32_t pk[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          mlo |= pk[k] << (8 * k);
-          mhi |= pk[4 + k] << (8 * k);
+          for (int k = 0; k < 8; ++k) pk[k] = (((cm[2 * k + 1] >> 3) | (cm[2 * k] >> 7)) * 0x01020408u) >> 24;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            mlo |= pk[k] << (8 * k);
+            mhi |= pk[4 + k] << (8 * k);
+          }
         }
       }
-      const uint32_t cnt = (uint32_t)__builtin_popcount(mlo) + (uint32_t)__builtin_popcount(mhi);
-      // exclusive prefix of the counts over the lanes (DPP scan: rows, then row 15 / lane 31 broadcasts)
-      uint32_t inc = cnt;
-      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x111, 0xF, 0xF, true);
-      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x112, 0xF, 0xF, true);
-      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x114, 0xF, 0xF, true);
-      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x118, 0xF, 0xF, true);
-      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x142, 0xA, 0xF, false);
-      inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x143, 0xC, 0xF, false);
-      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-      if (tot) {
-        if (npend + tot > kSwList) return false;   // too dense for the tier: the region pipeline takes it
-        // the lanes before a candidate's lane in its 256-B window keep their 64-B registers, so k_sweep_fin
-        // gets P(x) of an entry start from <= 3 of them and <= 63 bytes
-        const uint64_t cb = __ballot(cnt != 0u);
-        const uint32_t quad = (uint32_t)(cb >> ((uint32_t)lane & 60u)) & 0xFu;
-        if ((quad >> (((uint32_t)lane & 3u) + 1u)) && !(LDB_SW_ABL & 8)) p.swpl[(A + wo) >> 6] = reg;
-        // the positions, in file order (lane-major: the windows are in lane order)
-        uint32_t j = npend + inc - cnt;
-        while (mlo) {
-          hl[j++] = wo + (uint32_t)__builtin_ctz(mlo);
-          mlo &= mlo - 1;
+      if (has) {
+        const uint32_t cnt = (uint32_t)__builtin_popcount(mlo) + (uint32_t)__builtin_popcount(mhi);
+        // exclusive prefix of the counts over the lanes (DPP scan: rows, then row 15 / lane 31 broadcasts)
+        uint32_t inc = cnt;
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x111, 0xF, 0xF, true);
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x112, 0xF, 0xF, true);
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x114, 0xF, 0xF, true);
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x118, 0xF, 0xF, true);
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x142, 0xA, 0xF, false);
+        inc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x143, 0xC, 0xF, false);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        if (tot) {
+          if (npend + tot > kSwList) return false;   // too dense for the tier: the region pipeline takes it
+          // the lanes before a candidate's lane in its 256-B window keep their 64-B registers, so k_sweep_fin
+          // gets P(x) of an entry start from <= 3 of them and <= 63 bytes
+          const uint64_t cb = __ballot(cnt != 0u);
+          const uint32_t quad = (uint32_t)(cb >> ((uint32_t)lane & 60u)) & 0xFu;
+          if ((quad >> (((uint32_t)lane & 3u) + 1u)) && !(LDB_SW_ABL & 8)) p.swpl[(A + wo) >> 6] = reg;
+          // the positions, in file order (lane-major: the windows are in lane order)
+          uint32_t j = npend + inc - cnt;
+          while (mlo) {
+            hl[j++] = wo + (uint32_t)__builtin_ctz(mlo);
+            mlo &= mlo - 1;
+          }
+          while (mhi) {
+            hl[j++] = wo + 32u + (uint32_t)__builtin_ctz(mhi);
+            mhi &= mhi - 1;
+          }
+          npend += tot;
         }
-        while (mhi) {
-          hl[j++] = wo + 32u + (uint32_t)__builtin_ctz(mhi);
-          mhi &= mhi - 1;
-        }
-        npend += tot;
       }
 
       SW_T(tq3);
