@@ -864,10 +864,12 @@ __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
     if (tag == 0) continue;   // a covered run (sw_link): no entry of the chain starts in it
     uint64_t rank = q.base;
     const ldb_index_tuple* slab = p.scratch + r * cap64;
+    ldb_index_tuple tn{};
+    if ((uint32_t)lane < q.ncand) tn = slab[lane];
     for (uint32_t b0 = 0; b0 < q.ncand; b0 += 64) {
       const uint32_t i = b0 + (uint32_t)lane;
-      ldb_index_tuple t{};
-      if (i < q.ncand) t = slab[i];
+      const ldb_index_tuple t = tn;
+      if (i + 64u < q.ncand) tn = slab[i + 64u];   // the next block's record in flight during this one's checks
       const bool on = i < q.ncand && (t.pos >> 60) == tag;
       const uint64_t bal = __ballot(on);
       const uint64_t my = rank + sw_rank(bal, lane);
