@@ -385,14 +385,27 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
           any |= cm[i];
         }
         has = __ballot(any != 0u) != 0;
-        if (has) {   // (text values: about half the quarters hold no header byte <= 2)
+        auto pack = [&] {
           uint32_t pk[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) pk[k] = (((cm[2 * k + 1] >> 3) | (cm[2 * k] >> 7)) * 0x01020408u) >> 24;
+          mlo = mhi = 0;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             mlo |= pk[k] << (8 * k);
             mhi |= pk[4 + k] << (8 * k);
+          }
+        };
+        if (has) {   // (text values: about half the quarters hold no header byte <= 2)
+          pack();
+          // a lane with many: zero runs inside values (every zero byte passes the Status test). Positions
+          // whose crc bytes are surely zero go (dword i zero and bytes 0-2 of dword i + 1 zero: the crc of
+          // every start in dword i + 1's status bytes); the decode would reject them, the list would fill
+          if (__ballot(__builtin_popcount(mlo) + __builtin_popcount(mhi) > 8)) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if ((D(i) | (D(i + 1) << 8)) == 0u) cm[i] = 0u;
+            pack();
           }
         }
       }
@@ -511,9 +524,10 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
           load_blk(++bi);
         }
       };
-      // A speculated chain that leaves the run after fewer than kSwTrust entries is weak: a false start
-      // inside a value can claim a size past the run's end. Later starts are tried, and the first weak
-      // chain is taken back (re-walked, so its records carry its tag again) only if none of them holds.
+      // A speculated chain of fewer than kSwTrust entries is weak, whether it leaves the run (a false start
+      // inside a value can claim a size past the run's end) or ends in it (the file's last run). Later
+      // starts are tried, and the first weak chain is taken back (re-walked, so its records carry its tag
+      // again) only if none of them holds; the links then check it like any other.
       uint64_t wE = ~0ull;
       uint32_t wtag = 0;
       while (E != ~0ull) {
@@ -537,6 +551,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
           // that held kSwTrust entries is kept and its end checked by the links), or the speculated first
           // entry was false and the next candidate is tried
           if (r == 0 || cnt >= kSwTrust || tag == 15) { fl |= kSwDead; X = x; break; }
+          if (wE == ~0ull) { wE = E; wtag = tag; }   // weak too: a short chain that ends (the file's last run)
         }
         ++si;
         ++tag;
@@ -559,7 +574,11 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         while (x < B) {
           seek(x);
           const uint64_t mt = __ballot(lp == x);
-          const int L = __builtin_ctzll(mt);   // (a record: this chain was walked before)
+          if (!mt) {   // the weak chain ended inside the run
+            fl |= kSwDead;
+            break;
+          }
+          const int L = __builtin_ctzll(mt);
           if (lane == L) {
             rec.y = (rec.y & 0x0FFFFFFFu) | (tag << 28);
             dirty = true;
@@ -715,17 +734,20 @@ __device__ __forceinline__ uint32_t sw_fold_win(const Pipe& p, const uint32_t* T
 // where P(x) is the raw register over [x & ~255, x) and shift by n bytes multiplies by x^(8n) mod P.
 // P(a) is P(s) stepped over the stored crc (restarting at a window edge); P(e) is the next chain entry's
 // P(s), except after the tier's last entry (e == xe), whose end need not hold a candidate.
+// Ps = P(s), this entry's start prefix; Pe = P(e) when the caller has it (the next chain entry's Ps from
+// another lane, have_pe), else computed here.
 __device__ __forceinline__ bool sw_verify(const Pipe& p, const uint32_t* S, const uint32_t* T256, const uint32_t* T4096,
-                                          const uint32_t* T64, uint64_t s, uint64_t sz, uint64_t xe) {
+                                          const uint32_t* T64, uint64_t s, uint64_t sz, uint64_t xe, uint32_t Ps,
+                                          bool have_pe, uint32_t Pe_in) {
   const uint64_t a = s + 4, e = s + sz;
   const uint32_t crc = sw_word(p, s);
-  uint32_t Pa = sw_prefix_pl(p, S, T64, s);
+  uint32_t Pa = Ps;
 #pragma unroll
   for (uint32_t t = 0; t < 4; ++t) {
     Pa = S[(Pa ^ (crc >> (8 * t))) & 0xFFu] ^ (Pa >> 8);
     if (((s + t + 1) & (kSwW - 1)) == 0) Pa = 0;   // a window edge after the byte: P restarts there
   }
-  const uint32_t Pe = e == xe ? sw_prefix(p, S, e) : sw_prefix_pl(p, S, T64, e);
+  const uint32_t Pe = have_pe ? Pe_in : (e == xe ? sw_prefix(p, S, e) : sw_prefix_pl(p, S, T64, e));
   const uint64_t wa = a >> 8, we = e >> 8;
   uint32_t R;
   if (wa == we) {
@@ -874,10 +896,17 @@ __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
       const uint64_t bal = __ballot(on);
       const uint64_t my = rank + sw_rank(bal, lane);
       rank += (uint64_t)__builtin_popcountll(bal);
-      if (!on) continue;
       const uint64_t s = t.pos & 0xFFFFFFFFFFull;
       const uint64_t sz = ((t.pos >> 40) & 0x3Fu) + (uint64_t)t.k_size + t.v_size;
-      if (!(LDB_FIN_ABL & 8) && !sw_verify(p, st + 2048, st, st + 1024, st + 6144, s, sz, xe)) atomicMin((unsigned long long*)&c->fail, (unsigned long long)my);
+      // each entry's start prefix once: the next chain entry (the next lane with a record of the chain,
+      // whose start is this one's end) hands its P to this lane
+      const uint32_t Ps = on ? sw_prefix_pl(p, st + 2048, st + 6144, s) : 0u;
+      const uint64_t after = lane < 63 ? bal & (~0ull << (lane + 1)) : 0ull;
+      const int nl = after ? (int)__builtin_ctzll(after) : lane;
+      const uint32_t Pn = (uint32_t)__shfl((int)Ps, nl);
+      if (!on) continue;
+      if (!(LDB_FIN_ABL & 8) && !sw_verify(p, st + 2048, st, st + 1024, st + 6144, s, sz, xe, Ps, after != 0ull, Pn))
+        atomicMin((unsigned long long*)&c->fail, (unsigned long long)my);
       const uint64_t k = ks + my;
       if (k < p.cap) {
         if (p.kind == LDB_TUPLE_ENTRY) decode_entry_global(p, s, reinterpret_cast<ldb_entry*>(p.out) + k);

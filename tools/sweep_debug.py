@@ -1,6 +1,6 @@
 """Where and why the sweep tier ended on a log (diagnostics): runs the scan on cuda:0, reads the run records
 and the control block (ldb_debug_sweep_state), and prints the runs around the tier's end beside the
-oracle's chain. usage: python tools/sweep_debug.py [writer|zipf] [mib] [seed]"""
+oracle's chain. usage: python tools/sweep_debug.py [writer|zipf|adv:<case>] [mib] [seed]"""
 import ctypes as C
 import os
 import sys
@@ -27,6 +27,12 @@ def main():
     seed = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     if kind == "writer":
         img, n, _ = coracle.gen_writer_log(mib << 20, seed)
+    elif kind.startswith("adv:"):   # a tools/adversarial.py case tiled to mib MiB
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import adversarial
+        b = adversarial.block(kind[4:])
+        img = np.concatenate([np.tile(b, max(1, (mib << 20) // len(b))), np.zeros(64, np.uint8)])
+        n = int(coracle.scan(img)[0].n_entries)
     else:
         img, n, _ = coracle.gen_log(mib << 20, seed, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
     ref, rt = coracle.scan(img, tuple_kind=1)
