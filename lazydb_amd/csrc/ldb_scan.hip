@@ -2434,12 +2434,14 @@ int fence_ws(ldb_ctx* c, hipStream_t s) {
 }
 // The workspace is free for stream s once the last pipeline enqueued on another stream has finished.
 // An event is recorded on the old stream only when the context owns it (h_stream lives as long as the
-// context); a caller's stream may have been destroyed since its last call (the C ABI allows that), and
-// recording on a dead handle is undefined, so a switch away from one drains the device instead. A
-// context used from one stream never switches; the merge's scan contexts keep to their own streams.
+// context) or is the null stream; a caller's stream may have been destroyed since its last call (the C ABI
+// allows that), and recording on a dead handle is undefined, so a switch away from one drains the device
+// instead. A context used from one stream never switches; the merge's scan contexts keep to their own
+// streams.
 int ws_wait(ldb_ctx* c, hipStream_t s) {
   if (!c->ws_ev_live || c->ws_stream == s) return LDB_OK;
-  if (c->ws_stream != c->h_stream || !c->h_stream) {
+  // (the null stream and the context's own stream always exist: an event on them is safe)
+  if (c->ws_stream != nullptr && (c->ws_stream != c->h_stream || !c->h_stream)) {
     LDB_HIP(hipDeviceSynchronize());
     c->ws_ev_live = false;
     return LDB_OK;
