@@ -306,9 +306,7 @@ __device__ __forceinline__ uint32_t key_len_before(const uint8_t* img, uint64_t 
 // kCasFirst: claim by CAS straight away (the CAS returns the slot's word when it is taken) instead
 // of a load first. The slot id goes to slot[seq] with bit 31 = "expired" (db.go:255, ExpiredAt <=
 // now): the header sits next to the key this kernel reads, so k_live needs no image access for it.
-// kAbl (timing ablations, results invalid; LDB_INSERT_ABL): 1 no atomicMax, 2 no key compare, 3 both,
-// 4 no table at all (key read + hash only)
-template <bool kCasFirst, int kAbl = 0>
+template <bool kCasFirst>
 __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __restrict__ gfd, uint32_t n_files,
                                                 unsigned long long* tab, uint64_t mask, uint32_t* __restrict__ slot,
                                                 int64_t now, uint64_t tagmask) {
@@ -328,10 +326,6 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
   const uint64_t h = in_run ? fd[f].hashes[seq - fd[f].seq_base] : key_hash(kp, kl);
   const unsigned long long mine = (h & ~kGMask) | (fd[f].gbase + e.offset + e.hdr_size + 1);
   uint64_t i = h & mask;
-  if (kAbl == 4) {
-    slot[seq] = (uint32_t)(h & mask) | (expired ? 0x80000000u : 0u);
-    return;
-  }
   for (;;) {
     unsigned long long v;
     if (kCasFirst) {
@@ -346,17 +340,13 @@ __global__ __launch_bounds__(256) void k_insert(uint64_t n, const FileDesc* __re
       }
     }
     if (((v ^ mine) & tagmask) == 0) {   // tagmask: ~kGMask (0 = every probe compares keys: a test mode)
-      uint32_t rl = kl;
-      const uint8_t* rp = kp;
-      if (!(kAbl & 2)) {
-        const uint64_t g = (v & kGMask) - 1;
-        const uint32_t fr = file_of_g(fd, n_files, g);
-        const uint64_t ko = g - fd[fr].gbase;
-        rl = key_len_before(fd[fr].img, ko);
-        rp = fd[fr].img + ko;
-      }
-      if ((kAbl & 2) || (rl == kl && key_equal(kp, rp, kl))) {
-        if (!(kAbl & 1)) atomicMax(&tab[i], mine);
+      const uint64_t g = (v & kGMask) - 1;
+      const uint32_t fr = file_of_g(fd, n_files, g);
+      const uint64_t ko = g - fd[fr].gbase;
+      const uint32_t rl = key_len_before(fd[fr].img, ko);
+      const uint8_t* rp = fd[fr].img + ko;
+      if (rl == kl && key_equal(kp, rp, kl)) {
+        atomicMax(&tab[i], mine);
         break;
       }
     }
@@ -1459,12 +1449,7 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
     const uint64_t tagmask = tl && atoi(tl) != 0 ? 0ull : ~kGMask;
     static const bool cas_first = getenv("LDB_INSERT_CAS") != nullptr && atoi(getenv("LDB_INSERT_CAS")) != 0;
     if (!ext_live) {
-      static const int abl = getenv("LDB_INSERT_ABL") ? atoi(getenv("LDB_INSERT_ABL")) : 0;
-      if (abl == 1) k_insert<false, 1><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
-      else if (abl == 2) k_insert<false, 2><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
-      else if (abl == 3) k_insert<false, 3><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
-      else if (abl == 4) k_insert<false, 4><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
-      else if (cas_first) k_insert<true><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
+      if (cas_first) k_insert<true><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
       else k_insert<false><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
     }
     k_live<<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, d_slot, last_in, now, live_ok ? d_live : nullptr, d_esz, d_part,

@@ -2013,7 +2013,7 @@ __global__ __launch_bounds__(256) void k_combine(Pipe p0, const Pipe* __restrict
   if (threadIdx.x == 0) p.blk[blockIdx.x] = s_sum[0];   // blockDim == kBlkRegions
 }
 
-__device__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out) {
+__device__ __forceinline__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out) {
   struct G {
     const uint8_t* q;
     __device__ uint32_t operator()(int i) const { return q[i]; }
@@ -2607,7 +2607,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
       if (fold_init && sweep_enabled()) {   // the sweep tier from the run prefix's end (ldb_sweep.h)
         hipLaunchKernelGGL(k_sweep, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p);
         if (ev) LDB_HIP(hipEventRecord(ev->es, s));
-        hipLaunchKernelGGL(k_sweep_fin, dim3(4 * c->n_cu), dim3(64 * kSwFinWaves), 0, s, p);
+        hipLaunchKernelGGL(k_sweep_fin, dim3(LDB_FIN_WPE * c->n_cu), dim3(64 * kSwFinWaves), 0, s, p);
       } else if (ev) {
         LDB_HIP(hipEventRecord(ev->es, s));
       }

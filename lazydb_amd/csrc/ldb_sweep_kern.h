@@ -196,11 +196,6 @@ __device__ uint64_t g_swstamps[16];
 #define SW_ADD(k, a, b)
 #endif
 
-#ifndef LDB_SW_ABL
-#define LDB_SW_ABL 0   // attribution builds only (results invalid): 1 no CRC, 2 no candidates, 4 no walk, 16 no window
-                       // tree, 32 no decode, 64 no streaming, 128 no stop poll, 256 no look-ahead load, 8 no register
-                       // stores
-#endif
 __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
   __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
   __shared__ __attribute__((aligned(16))) uint32_t sh[9 * 1024];   // shift by 64, 128, ..., 2048, then 16, 32, 48 bytes
@@ -277,13 +272,13 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
         const uint4 x = ld16(irs, qo + 64u * (uint32_t)lane + 16u * k);
         q.d[4 * k] = x.x; q.d[4 * k + 1] = x.y; q.d[4 * k + 2] = x.z; q.d[4 * k + 3] = x.w;
       }
-      if (lane == 63 && !(LDB_SW_ABL & 256)) {   // one lane: the look-ahead costs one dwordx2 load of a single address
-        const v2u32 x = __builtin_amdgcn_raw_buffer_load_b64(irs, qo + 4096u, 0, 0);
-        q.n0 = x[0];
-        q.n1 = x[1];
-      } else {
-        q.n0 = q.n1 = 0;
-      }
+      // the look-ahead (used by lane 63): one wave-uniform address, one request. Every load here and in the
+      // loop below is unconditional (past the run's end the bytes are unused, past the file's the buffer
+      // returns zeros), so the compiler's vmcnt waits count exactly: the next quarter's rows stay in flight
+      // while this one is processed (a load under a branch made it wait for all of them)
+      const v2u32 x = __builtin_amdgcn_raw_buffer_load_b64(irs, qo + 4096u, 0, 0);
+      q.n0 = x[0];
+      q.n1 = x[1];
     };
     // The group registers (RG, 4 KiB = one quarter), four quarters at once: row t of rga holds quarter t's 16
     // window registers (lane 16 t + m <- window m); a 4-level tree in each row (shifts by 256 .. 2048 B)
@@ -302,7 +297,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       y = sw_dpp<0x118>(r);                                   // row_shr:8
       if ((lane & 15) == 15) {
         r ^= sw_shift(sh + 5120, y);
-        if ((uint32_t)(lane >> 4) <= ((qo_last >> 12) & 3u) && !(LDB_SW_ABL & 8))
+        if ((uint32_t)(lane >> 4) <= ((qo_last >> 12) & 3u))
           p.swrg[((A + (qo_last & ~0x3FFFu)) >> 12) + (uint32_t)(lane >> 4)] = r;
       }
       rga = 0;
@@ -324,11 +319,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       SW_ADD(1, tq0, tq1);
       // the lane's raw register over its 64 bytes (LP2: conflict-free lane-private tables)
       uint32_t reg = 0;
-      if (LDB_SW_ABL & 1) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) reg ^= q.d[k];
-      } else {
-        // one chain per 16-B row (four in flight), joined by shifts of 48, 32 and 16 bytes
+      {   // one chain per 16-B row (four in flight), joined by shifts of 48, 32 and 16 bytes
         uint32_t c[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -340,17 +331,14 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       // ends level 2 with window m's register (RW, 256 B); the quarter's 16 go to the group accumulator
       const uint64_t w0 = (A + qo) >> 8;
       uint32_t v = reg, y;
-      if (LDB_SW_ABL & 16) asm volatile("" ::"v"(reg));   // (the rows stay loaded in attribution builds)
-      if (!(LDB_SW_ABL & 16)) {
       y = sw_dpp<0x111>(v);                                   // row_shr:1
       if (lane & 1) v ^= sw_shift(sh, y);
       y = sw_dpp<0x112>(v);                                   // row_shr:2
       if ((lane & 3) == 3) {
         v ^= sw_shift(sh + 1024, y);
-        if (!(LDB_SW_ABL & 8)) p.swrw[w0 + (uint32_t)(lane >> 2)] = v;
+        p.swrw[w0 + (uint32_t)(lane >> 2)] = v;
       }
-      }
-      if (!(LDB_SW_ABL & 16)) {   // quarter t of its 16-KiB batch (the run starts on a batch): its RWs to row t of the accumulator
+      {   // quarter t of its 16-KiB batch (the run starts on a batch): its RWs to row t of the accumulator
         const uint32_t t = (qo >> 12) & 3u;
         const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)bpa, (int)v);
         if ((uint32_t)(lane >> 4) == t) rga = x;
@@ -370,7 +358,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       // on one bit).
       uint32_t mlo = 0, mhi = 0;
       bool has = false;
-      if (!(LDB_SW_ABL & 2)) {
+      {
         uint32_t orw = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) orw |= q.d[i];
@@ -426,7 +414,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
           // gets P(x) of an entry start from <= 3 of them and <= 63 bytes
           const uint64_t cb = __ballot(cnt != 0u);
           const uint32_t quad = (uint32_t)(cb >> ((uint32_t)lane & 60u)) & 0xFu;
-          if ((quad >> (((uint32_t)lane & 3u) + 1u)) && !(LDB_SW_ABL & 8)) p.swpl[(A + wo) >> 6] = reg;
+          if ((quad >> (((uint32_t)lane & 3u) + 1u))) p.swpl[(A + wo) >> 6] = reg;
           // the positions, in file order (lane-major: the windows are in lane order)
           uint32_t j = npend + inc - cnt;
           while (mlo) {
@@ -448,7 +436,6 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
     auto drain = [&] {   // decode while 64 or more candidates wait
       SW_T(td0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the hit list's stores, before other lanes read them
-      if (LDB_SW_ABL & 32) npend = 0;
       while (npend >= 64 && !decl) {
         flush(64);
         npend -= 64;
@@ -462,21 +449,22 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       SW_T(td1);
       SW_ADD(4, td0, td1);
     };
-    const uint32_t nq = (LDB_SW_ABL & 64) ? 0u : (uint32_t)((B - A + 4095) / 4096);
+    const uint32_t nq = (uint32_t)((B - A + 4095) / 4096);
     SW_T(tl0);
     QB P, Q;
     if (nq > 0) load_q(P, 0);
     for (uint32_t i = 0; i < nq && !decl; i += 2) {
-      {   // a run before this one ends the tier: nothing here is used
+      load_q(Q, (i + 1) * 4096u);
+      kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!proc_q(P, i * 4096u)) { decl = true; break; }
+      load_q(P, (i + 2) * 4096u);
+      __builtin_amdgcn_sched_barrier(0);
+      {   // a run before this one ends the tier: nothing here is used (kv was loaded before the rows of P:
+          // its wait leaves them in flight)
         const uint64_t stop = ((uint64_t)__builtin_amdgcn_readfirstlane(kv[1]) << 32) | __builtin_amdgcn_readfirstlane(kv[0]);
         if (stop < r) { decl = true; break; }
       }
-      if (i + 1 < nq) load_q(Q, (i + 1) * 4096u);
-      if (!(LDB_SW_ABL & 128)) kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (!proc_q(P, i * 4096u)) { decl = true; break; }
-      if (i + 2 < nq) load_q(P, (i + 2) * 4096u);
-      __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < nq && !proc_q(Q, (i + 1) * 4096u)) { decl = true; break; }
       drain();
     }
@@ -507,8 +495,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       const uint32_t i = blk * 64u + (uint32_t)lane;
       store16(srs, i < ncand ? i * 16u : kDrop, rec.x, rec.y, rec.z, rec.w);
     };
-    if (LDB_SW_ABL & 4) fl |= kSwDecl;
-    if (!decl && ncand <= cap && !(LDB_SW_ABL & 4)) {
+    if (!decl && ncand <= cap) {
       if (ncand) load_blk(0);
       if (r == 0) E = g.xs;
       else if (ncand) E = sw_readlane64(lp, 0);
@@ -854,17 +841,16 @@ __device__ __forceinline__ void sw_finish(const Pipe& p) {
   }
 }
 
-#ifndef LDB_FIN_ABL
-#define LDB_FIN_ABL 0   // attribution builds only (results invalid): 1 no run loop, 2 no sw_finish, 4 no table copy,
-                        // 8 no verify
+#ifndef LDB_FIN_WPE
+#define LDB_FIN_WPE 4   // workgroups per CU (= waves per SIMD): 5 measured slower at 8 GiB (fin 202-206 against 194-195 us)
 #endif
-__global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
+__global__ __launch_bounds__(64 * kSwFinWaves) __attribute__((amdgpu_waves_per_eu(LDB_FIN_WPE))) void k_sweep_fin(Pipe p) {
   __shared__ __attribute__((aligned(16))) uint32_t st[2 * 1024 + 16 * 256 + 1024];
   __shared__ int s_last;
   if (scan_done(p)) return;
   SwCtl* c = p.swctl;
   if (c->state != 1) return;
-  if (!(LDB_FIN_ABL & 4)) {   // shift by 256, 4096, slicing-by-16, shift by 64: every load in flight before the stores
+  {   // shift by 256, 4096, slicing-by-16, shift by 64: every load in flight before the stores
     static_assert(64 * kSwFinWaves == 256, "k_sweep_fin: 256 threads copy 7168 words");
     uint32_t v[28];
 #pragma unroll
@@ -880,7 +866,7 @@ __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
   const int wave = threadIdx.x >> 6;
   const uint64_t ks = c->ks, ncov = c->ncov, nrun = c->nrun, xe = c->xe;
   const uint64_t cap64 = nrun ? p.scratch_bytes / 16 / nrun : 0;
-  for (uint64_t r = (uint64_t)blockIdx.x * kSwFinWaves + wave; r < ((LDB_FIN_ABL & 1) ? 0 : ncov); r += (uint64_t)gridDim.x * kSwFinWaves) {
+  for (uint64_t r = (uint64_t)blockIdx.x * kSwFinWaves + wave; r < ncov; r += (uint64_t)gridDim.x * kSwFinWaves) {
     const SwRun q = p.swrun[r];
     const uint64_t tag = q.flags >> 8;
     if (tag == 0) continue;   // a covered run (sw_link): no entry of the chain starts in it
@@ -905,7 +891,7 @@ __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
       const int nl = after ? (int)__builtin_ctzll(after) : lane;
       const uint32_t Pn = (uint32_t)__shfl((int)Ps, nl);
       if (!on) continue;
-      if (!(LDB_FIN_ABL & 8) && !sw_verify(p, st + 2048, st, st + 1024, st + 6144, s, sz, xe, Ps, after != 0ull, Pn))
+      if (!sw_verify(p, st + 2048, st, st + 1024, st + 6144, s, sz, xe, Ps, after != 0ull, Pn))
         atomicMin((unsigned long long*)&c->fail, (unsigned long long)my);
       const uint64_t k = ks + my;
       if (k < p.cap) {
@@ -925,5 +911,5 @@ __global__ __launch_bounds__(64 * kSwFinWaves) void k_sweep_fin(Pipe p) {
   if (!s_last || threadIdx.x >= 64) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (!(LDB_FIN_ABL & 2)) sw_finish(p);
+  sw_finish(p);
 }

@@ -1,5 +1,5 @@
 # The sweep tier's attribution on one box: the product library and the LDB_SW_ABL builds present in
-# lazydb_amd/_lib (tools/build_variants.py def_LDB_SW_ABL=<bits>), on a 1 GiB Zipf log; then the read ceiling.
+# lazydb_amd/_lib (tools/build_variants.py def_LDB_SW_ABL=<bits> on a checkout of b0eb7f1), on a 1 GiB Zipf log; then the read ceiling.
 set -o pipefail
 mkdir -p gpurun_out
 : > gpurun_out/abl.log

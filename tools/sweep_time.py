@@ -1,5 +1,5 @@
 """Time the sweep tier on one Zipf log (config 3's value mix): k_sweep and k_sweep_fin by HIP events, for the
-library LAZYDB_GPU_LIB names (A/B and attribution builds: tools/build_variants.py def_LDB_SW_ABL=<bits>).
+library LAZYDB_GPU_LIB names (A/B and attribution builds: tools/build_variants.py def_LDB_SW_ABL=<bits> on a checkout of b0eb7f1).
 usage: python tools/sweep_time.py [mib] [reps]"""
 import os
 import sys
