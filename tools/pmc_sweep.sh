@@ -1,6 +1,6 @@
 # PMC passes on the sweep tier's kernels (k_sweep, k_sweep_fin) over a 1 GiB Zipf log (tools/sweep_time.py),
 # one counter set per rocprofv3 run (never combined with other traces), summarised per kernel.
-# usage: bash tools/pmc_sweep.sh <tag>   -> gpurun_out/pmcsw_<tag>/
+# usage: [MIB=..] [KIND=zipf|writer] bash tools/pmc_sweep.sh <tag>   -> gpurun_out/pmcsw_<tag>/
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-x}
@@ -11,7 +11,7 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
            "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $set --kernel-include-regex 'k_sweep' -d $OUT/pmc$i -o pmc -f csv -- python3 tools/sweep_time.py ${MIB:-1024} 5 > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 1; }
+  timeout -k 10 120 rocprofv3 --pmc $set --kernel-include-regex 'k_sweep' -d $OUT/pmc$i -o pmc -f csv -- python3 tools/sweep_time.py ${MIB:-1024} 5 ${KIND:-zipf} > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 1; }
 done
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections

@@ -1,6 +1,6 @@
 """Time the sweep tier on one Zipf log (config 3's value mix): k_sweep and k_sweep_fin by HIP events, for the
 library LAZYDB_GPU_LIB names (A/B and attribution builds: tools/build_variants.py def_LDB_SW_ABL=<bits> on a checkout of b0eb7f1).
-usage: python tools/sweep_time.py [mib] [reps]"""
+usage: python tools/sweep_time.py [mib] [reps] [zipf|writer]"""
 import os
 import sys
 import time
@@ -15,7 +15,11 @@ def main():
     from oracle import coracle
     mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    img, n, end = coracle.gen_log(mib << 20, 11, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
+    kind = sys.argv[3] if len(sys.argv) > 3 else "zipf"
+    if kind == "writer":   # bench leg w's log (gen_writer_log, seed 30)
+        img, n, end = coracle.gen_writer_log(mib << 20, 30)
+    else:
+        img, n, end = coracle.gen_log(mib << 20, 11, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
     eng = Engine(0)
     d = torch.from_numpy(img).to("cuda:0")
     res, _ = eng.scan_dev(d, cap=n + 1024)
