@@ -23,9 +23,16 @@ def build_lib(force: bool = False) -> str:
     deps = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include", "lazydb_gpu.h")]
     if force or _stale(OUT, deps):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
-        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-               "-Wno-unused-function", "-o", OUT, *SRCS]
-        subprocess.run(cmd, check=True)
+        # the translation units in parallel (each carries its own code object), then one link
+        flags = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+        objs = [os.path.join(os.path.dirname(OUT), os.path.basename(s) + ".o") for s in SRCS]
+        procs = [subprocess.Popen([*flags, "-c", "-o", o, s]) for s, o in zip(SRCS, objs)]
+        rcs = [pr.wait() for pr in procs]
+        if any(rcs):
+            raise subprocess.CalledProcessError(max(rcs, key=abs), "hipcc")
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-o", OUT, *objs], check=True)
+        for o in objs:
+            os.remove(o)
     return OUT
 
 

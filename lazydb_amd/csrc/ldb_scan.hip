@@ -1408,7 +1408,6 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
     if (threadIdx.x == 5) p.dyn[5] = ~0ull;
     if (p.swctl && threadIdx.x == 0) {   // the sweep tier's control words (k_sweep, k_sweep_fin follow)
       p.swctl->fail = ~0ull;
-      p.swctl->stop = ~0ull;
       p.swctl->done0 = 0;
       p.swctl->done1 = 0;
       p.swctl->state = 0;
@@ -2604,6 +2603,18 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
     } else {
       launch(0, len);   // its workgroups also write the runs' INDEX tuples (uni_post_fill)
       if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+#ifdef LDB_TAIL_ABL   // attribution builds only (results wrong unless the run prefix covers the file): 1 no tail, 2 one launch
+      if (LDB_TAIL_ABL == 2)
+        hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)std::min<uint64_t>(L.nblk, 4ull * c->n_cu)), dim3(kBlkRegions), 0, s,
+                           p, nullptr);
+      if (ev) {
+        LDB_HIP(hipEventRecord(ev->es, s));
+        LDB_HIP(hipEventRecord(ev->ef, s));
+        LDB_HIP(hipEventRecord(ev->e1, s));
+        LDB_HIP(hipEventRecord(ev->e2, s));
+      }
+      return fence_ws(c, s);
+#endif
       if (fold_init && sweep_enabled()) {   // the sweep tier from the run prefix's end (ldb_sweep.h)
         hipLaunchKernelGGL(k_sweep, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p);
         if (ev) LDB_HIP(hipEventRecord(ev->es, s));

@@ -87,8 +87,9 @@ __device__ __forceinline__ T sw_wg_scan(T v, T ident, Op op, T* s_wtot) {
 
 // The links between runs (the last k_sweep workgroup, every thread). The tier's entries are the chain
 // from x_s through the runs in order. A run whose walk found a chain (E_r set; "active") continues it when
-// E_r is the exit of the last active run before it (x_s before run 0's); a run without one is passed when
-// that exit lies at or past its end (an entry longer than the run covers it). The tier ends at the first
+// E_r is the exit of the last active run before it (x_s before run 0's); a run without one (declined, or no
+// walk) is passed when that exit lies at or past its end (an entry longer than the run covers it; its CRC
+// is then checked from this run's registers, which every run computes to its end). The tier ends at the first
 // run that does neither -- declined, a chain that is not the previous exit's, or an entry start the
 // walk could not take -- at the true chain position entering it (the previous exit), or at the end of an
 // active run whose chain ended inside it. Fully parallel: the last active run before each run is a
@@ -176,7 +177,6 @@ __device__ void sw_link(const Pipe& p, const SwGeo& g) {
     c->ke = g.ks + tot;
     c->ncov = ncov;
     c->nrun = nrun;
-    c->stop = ~0ull;
     c->done0 = 0;
     c->state = 1;
   }
@@ -235,7 +235,6 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
     const __amdgpu_buffer_rsrc_t srs = rsrc_of(slab, cap * 16u);
     const uint64_t ib = (p.len - A + 3) & ~3ull;   // (a ternary: min() on 64-bit unsigned is HIP's double overload)
     const __amdgpu_buffer_rsrc_t irs = rsrc_of(p.img + A, (uint32_t)(ib < 0xFFFFFFFFull ? ib : 0xFFFFFFFFull));
-    const __amdgpu_buffer_rsrc_t krs = rsrc_of(&p.swctl->stop, 8);
     uint32_t npend = 0, ncand = 0;
     bool decl = false;
     // decode hl[0, nf) (one candidate per lane) and append the entries decode_lean accepts to the slab
@@ -258,7 +257,6 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       ncand += (uint32_t)__builtin_popcountll(bal);
       if (ncand > cap) decl = true;
     };
-    v2u32 kv = {0xFFFFFFFFu, 0xFFFFFFFFu};
     // The run in quarters of 4 KiB: lane l holds the quarter's bytes [64 l, 64 l + 64) as 4 rows (a row
     // instruction reads 4 KiB in 64-B steps; the lane's bytes stay contiguous for its CRC), lane 63 also the
     // next quarter's first 8 bytes. The next quarter's rows are in flight while one is processed.
@@ -405,7 +403,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
           }
         }
       }
-      if (has) {
+      if (has && !decl) {   // (a declined run keeps its registers, not its candidates)
         const uint32_t cnt = (uint32_t)__builtin_popcount(mlo) + (uint32_t)__builtin_popcount(mhi);
         // exclusive prefix of the counts over the lanes (DPP scan: rows, then row 15 / lane 31 broadcasts)
         uint32_t inc = cnt;
@@ -461,26 +459,24 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
     SW_T(tl0);
     QB P, Q;
     if (nq > 0) load_q(P, 0);
-    for (uint32_t i = 0; i < nq && !decl; i += 2) {
+    // Every run streams to its end, declined or not: a declined run (too many candidates) ends the tier
+    // unless an entry from an earlier run covers it whole (sw_link), and that entry's CRC is then checked
+    // from this run's window and group registers, so they are always complete. (Round 5 broke out of the
+    // loop at a decline and polled a stop word per pair of quarters; an entry spanning a declined run was
+    // then verified from stale registers.)
+    for (uint32_t i = 0; i < nq; i += 2) {
       load_q(Q, (i + 1) * 4096u);
-      kv = __builtin_amdgcn_raw_buffer_load_b64(krs, 0, 0, kSc1);
       __builtin_amdgcn_sched_barrier(0);
-      if (!proc_q(P, i * 4096u)) { decl = true; break; }
+      if (!proc_q(P, i * 4096u)) decl = true;
       load_q(P, (i + 2) * 4096u);
       __builtin_amdgcn_sched_barrier(0);
-      {   // a run before this one ends the tier: nothing here is used (kv was loaded before the rows of P:
-          // its wait leaves them in flight)
-        const uint64_t stop = ((uint64_t)__builtin_amdgcn_readfirstlane(kv[1]) << 32) | __builtin_amdgcn_readfirstlane(kv[0]);
-        if (stop < r) { decl = true; break; }
-      }
-      if (i + 1 < nq && !proc_q(Q, (i + 1) * 4096u)) { decl = true; break; }
+      if (i + 1 < nq && !proc_q(Q, (i + 1) * 4096u)) decl = true;
       drain();
     }
-    if (!decl && (nq & 3u)) rg_tree((nq - 1u) * 4096u);   // a final batch of fewer than four quarters
+    if (nq & 3u) rg_tree((nq - 1u) * 4096u);   // a final batch of fewer than four quarters
     SW_T(tl1);
     SW_ADD(5, tl0, tl1);
     if (!decl && npend) flush(npend);
-    if (decl) atomicMin((unsigned long long*)&p.swctl->stop, (unsigned long long)r);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slab's stores, before the walk reads them
     // ---- the walk: from the run's first entry, each entry's end is the next candidate
     uint64_t E = ~0ull, X = 0, cnt = 0;

@@ -132,3 +132,50 @@ def test_sweep_dense_candidates(eng):
 def test_sweep_writer_mix(eng):
     w, nw, _ = coracle.gen_writer_log(32 << 20, 17, vmax=65536)
     check(eng, w)
+
+
+def _text_fill(rng, G, upto):
+    """Text-value entries that end exactly at byte `upto` (the last one's value sized to land there)."""
+    parts, used = [], 0
+    while True:
+        rest = upto - used
+        if rest < 400:
+            break
+        e = G.ent(key=G.alpha(rng, 16), value=G.alpha(rng, rng.randrange(40, min(3000, rest - 200))))
+        parts.append(e)
+        used += len(e)
+    base = len(G.ent(key=b"k" * 16, value=b""))
+    v = rest - base
+    while len(G.ent(key=b"k" * 16, value=b"v" * v)) > rest:
+        v -= 1
+    e = G.ent(key=G.alpha(rng, 16), value=G.alpha(rng, v))
+    assert len(e) == rest, (len(e), rest)
+    parts.append(e)
+    return parts
+
+
+@pytest.mark.parametrize("vlen,d", [(40000, 8), (33000, 0), (64000, 300), (50000, -60)])
+def test_sweep_entry_spanning_declined_runs(eng, vlen, d):
+    """an entry whose 0x02-byte value covers whole runs that decline (every position a
+    candidate). Its CRC is checked from those runs' window and group registers, so a declined run must
+    still compute them; round 5 stopped streaming at the decline and verified the entry from stale ones.
+    The header sits in the run before (its value starts d bytes into a 16-KiB run of a 1 MiB file)."""
+    from tests.golden import make_golden as G
+    rng = random.Random(vlen + d)
+    size = 1 << 20
+    # another log of the same size first, so the workspace's registers hold someone else's values
+    w, _, _ = coracle.gen_writer_log(size, 3)
+    check(eng, w, kinds=(0,), ios=(0,))
+    R = 8 * 16384
+    big = G.ent(key=G.alpha(rng, 16), value=bytes([2]) * vlen)
+    hs_k = len(big) - vlen
+    h = R + d - hs_k
+    parts = _text_fill(rng, G, h) + [big]
+    used = sum(len(x) for x in parts)
+    while used < size - 8192:
+        e = G.ent(key=G.alpha(rng, 16), value=G.alpha(rng, rng.randrange(40, 3000)))
+        parts.append(e)
+        used += len(e)
+    img = np.frombuffer(G.image(parts, size), np.uint8).copy()
+    res = check(eng, img)
+    assert res.status == 2 and res.n_entries == len(parts), res.as_dict()
