@@ -282,10 +282,10 @@ def measure_traffic(img, cap, args, kernel):
     path = os.path.join(shm, f"ldb_pmc_{os.getpid()}.bin")
     try:
         img.tofile(path)
-        # the device path's instance only (k_uniform<false, false>, k_scan_main<false>): not k_uniform_fill
-        tag = kernel + ("(" if kernel == "k_sweep" else "<false")   # k_sweep is no template
+        # the device path's instance only (k_uniform<false, false>, k_sweep<false>, k_region<false>): not k_uniform_fill
+        tag = kernel + "<false"
         cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--pmc", "FETCH_SIZE", "--kernel-include-regex",
-               kernel + ("\\(" if kernel == "k_sweep" else "<false"), "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
+               kernel + "<false", "-d", tmp, "-o", "pmc", "-f", "csv", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", f"{path}:{cap}", "--io", str(args.io), "--kind", str(args.kind)]
         p = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
         per = {}
@@ -696,7 +696,8 @@ def timed_scans(eng, S, fid, args, steps, world, stream):
     with no instrumentation inside the pipelines. Then K more with HIP events recorded around the
     kernels on the scan stream, for the per-kernel split (an event record between two kernels adds a
     few microseconds of gap, so it stays out of the headline pass). Returns (wall seconds, avg
-    k_uniform ms, avg k_scan_main ms, avg pipeline ms)."""
+    k_uniform ms, avg k_region ms, avg pipeline ms); timed_scans.sweep_ms: avg k_sweep ms; timed_scans.phases:
+    the phases after the run prefix (device clock)."""
     import torch
     import torch.distributed as dist
 
@@ -731,18 +732,22 @@ def timed_scans(eng, S, fid, args, steps, world, stream):
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    sw_ms, fin_ms = eng.timing_sweep()   # (before timing_split, which resets the accumulators)
+    ph = eng.timing_tail()   # (before timing_split, which resets the accumulators)
+    timed_scans.sweep_ms = eng.timing_sweep()[0]
     run_ms, main_ms, total_ms, _ = eng.timing_split(0)
-    timed_scans.sweep_ms, timed_scans.fin_ms = sw_ms, fin_ms
+    timed_scans.phases = {k: round(v, 4) for k, v in zip(TAIL_PHASES, ph)}
     timed_scans.median_ms = med_ms
     timed_scans.median_iters = len(evs)
     return t, run_ms, main_ms, total_ms
 
 
+TAIL_PHASES = ("sweep", "sweep_check", "regions", "links", "repair", "combine", "compact")
+
+
 def dominant_kernel(S, r, kind, run_ms, main_ms, sweep_ms=0.0):
     """The scan's dominant kernel and its algorithmic bytes per launch (the bytes of
     the accepted entries it verified). k_uniform (the run prefix) verified entries [0, n_run), i.e.
-    bytes [0, x0); k_sweep (the sweep tier, ldb_sweep.h) the next n_sweep, bytes [x0, x1); k_scan_main
+    bytes [0, x0); k_sweep (the sweep tier, ldb_sweep.h) the next n_sweep, bytes [x0, x1); k_region
     (the region pipeline) the rest, [x1, end_off)."""
     n_run, n_sw, n, end = int(r.n_run), int(r.n_sweep), int(r.n_entries), int(r.end_off)
     tsz = 16 if kind == 0 else 48
@@ -753,7 +758,7 @@ def dominant_kernel(S, r, kind, run_ms, main_ms, sweep_ms=0.0):
         return int.from_bytes(S.out[k * tsz: k * tsz + 8].cpu().numpy().tobytes(), "little") & ((1 << 40) - 1)
     x0 = start_of(n_run) if n_run else 0
     x1 = start_of(n_run + n_sw) if n_sw else x0
-    best = max((run_ms, "k_uniform", x0), (sweep_ms, "k_sweep", x1 - x0), (main_ms, "k_scan_main", end - x1))
+    best = max((run_ms, "k_uniform", x0), (sweep_ms, "k_sweep", x1 - x0), (main_ms, "k_region", end - x1))
     return best[1], best[2], best[0]
 
 
@@ -791,8 +796,7 @@ def run_leg(eng, cfg, args, dev):
     import torch
     img, S, r, verified, workload, _ = prepare(eng, cfg, 0, args, dev, not args.no_verify)
     t, run_ms, main_ms, total_ms = timed_scans(eng, S, 1, args, args.leg_steps, 1, torch.cuda.current_stream(dev))
-    sw_ms, fin_ms = timed_scans.sweep_ms, timed_scans.fin_ms
-    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms, sw_ms)
+    kname, kbytes, kms = dominant_kernel(S, r, args.kind, run_ms, main_ms, timed_scans.sweep_ms)
     step = t / args.leg_steps
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else None
     leg = {"config": cfg, "workload": workload, "file_bytes": int(img.size), "bytes_scanned": int(r.end_off),
@@ -801,8 +805,9 @@ def run_leg(eng, cfg, args, dev):
            "mentries_per_s": round(int(r.n_entries) / step / 1e6, 2),
            "median_event_ms": round(timed_scans.median_ms, 4),
            "GiB_per_s_median": round(int(r.end_off) / (timed_scans.median_ms * 1e-3) / 2**30, 3),
-           "k_uniform_ms": round(run_ms, 4), "k_sweep_ms": round(sw_ms, 4), "k_sweep_fin_ms": round(fin_ms, 4),
-           "k_scan_main_ms": round(main_ms, 4), "pipeline_ms": round(total_ms, 4),
+           "k_uniform_ms": round(run_ms, 4), "k_sweep_ms": round(timed_scans.sweep_ms, 4), "k_region_ms": round(main_ms, 4),
+           "tail_phases_ms": timed_scans.phases,
+           "pipeline_ms": round(total_ms, 4),
            "run_entries": int(r.n_run), "sweep_entries": int(r.n_sweep), "roofline_kernel": kname, "roofline_bytes": kbytes,
            "roofline_frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
            "status": int(r.status), "fast_regions": int(r.n_fast), "regions": int(r.n_regions),
@@ -966,7 +971,9 @@ def main():
                 "traffic_source": traffic_src,
                 "avg_kernel_ms": round(kms, 4),
                 "avg_k_uniform_ms": round(run_ms, 4),
-                "avg_k_scan_main_ms": round(main_ms, 4),
+                "avg_k_sweep_ms": round(timed_scans.sweep_ms, 4),
+                "avg_k_region_ms": round(main_ms, 4),
+                "tail_phases_ms": timed_scans.phases,
                 "run_entries": int(r.n_run),
                 "avg_pipeline_ms": round(total_ms, 4),
                 "algorithmic_bytes_per_launch": kbytes,
@@ -992,7 +999,7 @@ def main():
                 {"rank": i, "kernel": kname, "avg_kernel_ms": round(v[1], 4),
                  "achieved": round(v[0] / (v[1] * 1e-3) / 1e9, 1) if v[1] > 0 else None,
                  "frac": round(v[0] / (v[1] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if v[1] > 0 else None,
-                 "avg_k_uniform_ms": round(v[2], 4), "avg_k_scan_main_ms": round(v[3], 4),
+                 "avg_k_uniform_ms": round(v[2], 4), "avg_k_region_ms": round(v[3], 4),
                  "avg_pipeline_ms": round(v[4], 4), "wall_ms_per_step": round(v[5], 4)} for i, v in enumerate(per_rank)]
         if gather:
             line["gather"] = gather

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define LDB_ABI_VERSION 3
+#define LDB_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------
  * Normal terminations of the replay loop (index.go:86-88 `break`) are > 0;
@@ -181,22 +181,22 @@ int ldb_scan_file_dev_serial(ldb_ctx* ctx, const uint8_t* d_image, uint64_t len,
                              int tuple_kind, void* d_out, uint64_t cap, ldb_scan_result* d_result,
                              void* stream);
 
-/* Timing hook for bench.py: average device time (ms) of the main decode+CRC kernel and of the
- * whole pipeline over the launches since the last reset, measured with HIP events recorded on
- * the scan stream around each launch (no host synchronisation while enabled; the query waits
+/* Timing hook for bench.py: average device time (ms) of the region pipeline (avg_main_ms: the k_region
+ * launch, ABI 4) and of the whole pipeline over the scans since the last reset, measured with HIP events
+ * recorded on the scan stream around the launches (no host synchronisation while enabled; the query waits
  * for the recorded events). enable: 1 on + reset, 0 off + reset, -1 query only. */
 int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg_total_ms, uint64_t* n);
-/* The same with the run-prefix kernel (k_uniform, the equal-sized entries at the file start) timed on
- * its own: avg_run_ms; avg_main_ms is then the region pipeline's main kernel after it. */
+/* The same with the run prefix (k_uniform, the equal-sized entries at the file start, and on a chunked host
+ * scan its per-chunk fills) timed on its own: avg_run_ms; avg_main_ms is k_region. */
 int ldb_kernel_timing_split(ldb_ctx* ctx, int enable, double* avg_run_ms, double* avg_main_ms, double* avg_total_ms,
                             uint64_t* n);
-/* The run prefix's tuple fill (k_uniform_fill: the run's INDEX tuples written as one dense sweep after
- * k_uniform verified them) over the same launches: avg_fill_ms. Query only; the reset is
- * ldb_kernel_timing's / ldb_kernel_timing_split's. */
-int ldb_kernel_timing_fill(ldb_ctx* ctx, double* avg_fill_ms);
-/* The sweep tier (variable-length entries after the run prefix, ABI 3) over the same launches: its
- * streaming kernel (k_sweep: window CRCs, candidate decode, run walks and links) and its verify/emit
- * kernel (k_sweep_fin), each averaged over the timed scans (0 where the tier did not run). */
+/* The phases after the run prefix over the same scans, from the device's constant clock (first item claimed
+ * to the phase published, 0 where a phase did not run): k_sweep's [0] stream and links, [1] CRC checks and
+ * tuples; k_region's [2] regions, [3] their links, [4] the repair, [5] the cross-region CRCs, [6] the
+ * compaction. n_phases entries are written (7 are defined, the rest 0). Query only; the reset is
+ * ldb_kernel_timing's / ldb_kernel_timing_split's. (ABI 4: replaces ldb_kernel_timing_fill.) */
+int ldb_kernel_timing_tail(ldb_ctx* ctx, double* avg_phase_ms, int n_phases);
+/* The sweep tier: avg_sweep_ms the k_sweep launch (events), avg_fin_ms its check phase (ldb_kernel_timing_tail's [1]). */
 int ldb_kernel_timing_sweep(ldb_ctx* ctx, double* avg_sweep_ms, double* avg_fin_ms);
 
 /* Practical HBM-read ceiling for the roofline report: a read-only XOR

@@ -97,9 +97,9 @@ def lib():
         L.ldb_kernel_timing_split.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                               C.POINTER(C.c_double), C.POINTER(u64)]
         L.ldb_kernel_timing_split.restype = i32
-        if hasattr(L, "ldb_kernel_timing_fill"):   # absent from A/B builds of older revisions
-            L.ldb_kernel_timing_fill.argtypes = [vp, C.POINTER(C.c_double)]
-            L.ldb_kernel_timing_fill.restype = i32
+        if hasattr(L, "ldb_kernel_timing_tail"):   # absent from A/B builds of older revisions
+            L.ldb_kernel_timing_tail.argtypes = [vp, C.POINTER(C.c_double), i32]
+            L.ldb_kernel_timing_tail.restype = i32
         if hasattr(L, "ldb_kernel_timing_sweep"):
             L.ldb_kernel_timing_sweep.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
             L.ldb_kernel_timing_sweep.restype = i32
@@ -135,7 +135,8 @@ def lib():
             L.ldb_encode_entries_dev.argtypes = [vp, u64, vp, vp, u32, u64, u64, vp, u64, vp, u64, vp, u32,
                                                  C.POINTER(MergeResult), vp]
             L.ldb_encode_entries_dev.restype = i32
-        if L.ldb_abi_version() != 3:
+        # (an A/B build of an older revision, LAZYDB_GPU_LIB, may be one ABI behind)
+        if L.ldb_abi_version() != 4 and not (os.environ.get("LAZYDB_GPU_LIB") and L.ldb_abi_version() == 3):
             raise LdbError("liblazydb_gpu ABI version mismatch")
         _lib = L
     return _lib
@@ -144,7 +145,7 @@ def lib():
 EXPORTS = ("ldb_abi_version", "ldb_status_str", "ldb_ctx_create", "ldb_ctx_destroy", "ldb_ctx_reserve",
            "ldb_workspace_bytes", "ldb_scan_file_dev", "ldb_scan_file", "ldb_scan_file_count", "ldb_scan_copy_out",
            "ldb_scan_files_dev",
-           "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_kernel_timing_split", "ldb_kernel_timing_fill",
+           "ldb_scan_file_dev_serial", "ldb_kernel_timing", "ldb_kernel_timing_split", "ldb_kernel_timing_tail",
            "ldb_kernel_timing_sweep",
            "ldb_read_ceiling", "ldb_merge_files_dev",
            "ldb_merge_timing", "ldb_encode_entries_dev", "ldb_merge_repack_dev", "ldb_host_register", "ldb_host_unregister",

@@ -54,9 +54,16 @@ struct Pipe {
   SwCtl* swctl;
   const uint32_t* swt;
   uint64_t scratch_bytes;
+  // k_sweep and k_region (ldb_scan.hip): their control words (tickets, items done, published phases, phase stamps; 256 B,
+  // zeroed where the pipeline starts), the per-phase time accumulators (null unless ldb_kernel_timing is
+  // on) and whether the sweep tier runs
+  uint32_t* tail;
+  uint64_t* tacc;
+  uint32_t sweep;
 };
 
-constexpr int kBlkRegions = 256;   // regions per k_combine / k_compact workgroup
+constexpr uint32_t kTailCtlBytes = 256;   // Pipe::tail
+constexpr int kBlkRegions = 1024;   // regions per block of the count prefix (k_region phases C and K: one thread each)
 
 // ---------------------------------------------------------------- the run prefix (k_uniform)
 // k_uniform verifies, in parallel, that the log starts with K entries that all have entry 0's header

@@ -42,7 +42,9 @@ namespace {
 #ifndef LDB_NB
 #define LDB_NB 1
 #endif
-constexpr int kWPB = LDB_WPB;  // wavefronts per workgroup in k_scan_main
+constexpr int kWPB = LDB_WPB;  // wavefronts per workgroup of k_sweep and k_region (1024 threads)
+// what a k_sweep / k_region workgroup's LDS holds (its phases copy their tables once per workgroup, not per item)
+constexpr int kLdsNone = 0, kLdsSweep = 1, kLdsFin = 2, kLdsRegion = 3;
 constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
 #ifndef LDB_BLOCKS_PER_CU
 #define LDB_BLOCKS_PER_CU 0   // 0: as many as fit in a CU's 160 KiB of LDS
@@ -1406,13 +1408,12 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
     p.ctr[threadIdx.x] = 0u;
     if (threadIdx.x == 3 || threadIdx.x == 4 || threadIdx.x == 7) p.dyn[threadIdx.x] = 0;
     if (threadIdx.x == 5) p.dyn[5] = ~0ull;
-    if (p.swctl && threadIdx.x == 0) {   // the sweep tier's control words (k_sweep, k_sweep_fin follow)
+    if (p.swctl && threadIdx.x == 0) {   // the sweep tier's control words (k_sweep follows)
       p.swctl->fail = ~0ull;
-      p.swctl->done0 = 0;
-      p.swctl->done1 = 0;
       p.swctl->state = 0;
     }
   }
+  if (kMulti && LDB_FOLD_INIT && blockIdx.x == 0 && threadIdx.x < kTailCtlBytes / 4) p.tail[threadIdx.x] = 0u;
   // (workgroup 0 of a kMulti launch finds the runs first: its LP2 block afterwards, off that chain)
   if (!kMulti || blockIdx.x != 0) lp2_build(lp2, p.gtab);
 #ifdef LDB_STAMPS
@@ -1569,25 +1570,26 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uni_run<false, false, true, kUniWaves>(p, ru.r[0], p.dyn, lp2, comb, lane, wave, 0, p.len, bound);
 }
-// ---------------------------------------------------------------- k_scan_main
-template <bool kB>
-__global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
-  // CRC tables in a static LDS array: its address is a link-time constant, so every table read
-  // folds the table base into the ds_read offset field
-  __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  if (scan_done(p)) return;   // the run prefix ended on the chain's terminal (uni_finish)
+// ---------------------------------------------------------------- the region pipeline's main phase
+// (k_region phase M; rounds 1-5 the k_scan_main kernel). Item vb of vg: its kWPB waves each scan a contiguous
+// run of regions, the runs dealt as if vg workgroups were launched. tab: the CRC table block in LDS (a
+// static array of k_region: its address is a link-time constant, so every table read folds the table base
+// into the ds_read offset field), copied once per workgroup (tabs); smem: the waves' rings after it.
+__device__ __forceinline__ void main_item(const Pipe& p, uint32_t vb, uint32_t vg, uint32_t* tab, uint8_t* smem,
+                                          int& tabs) {
   // ctr[] was zeroed by k_init, which opens every pipeline (enqueue_scan), or on a run-prefix scan by
-  // k_uniform's workgroup 0 (LDB_FOLD_INIT); the terminal words start
-  // at "none" (read only by the later kernels, stream-ordered after this one)
-  if (blockIdx.x == 0 && threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
-  {   // a workgroup whose waves have no region (the run prefix took them) leaves before the table copy
-    const uint64_t rf0 = first_region(p), nr0 = p.nreg - rf0, nw0 = (uint64_t)gridDim.x * kWPB;
-    if (rf0 + (uint64_t)blockIdx.x * kWPB * ((nr0 + nw0 - 1) / nw0) >= p.nreg) return;
+  // k_uniform's workgroup 0 (LDB_FOLD_INIT); the terminal words start at "none" (read only by the later
+  // phases, after this one completes)
+  if (vb == 0 && threadIdx.x < 2) p.tpos[threadIdx.x] = ~0ull;
+  {   // an item whose waves have no region (the run prefix took them) is done before the table copy
+    const uint64_t rf0 = first_region(p), nr0 = p.nreg - rf0, nw0 = (uint64_t)vg * kWPB;
+    if (rf0 + (uint64_t)vb * kWPB * ((nr0 + nw0 - 1) / nw0) >= p.nreg) return;
   }
-  copy_tables(tab, p.gtab);
-  __syncthreads();
+  if (tabs != kLdsRegion) {
+    copy_tables(tab, p.gtab);
+    __syncthreads();
+    tabs = kLdsRegion;
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* wbase = smem + wave * (sizeof(WaveLds) + kNB * kBuf);
@@ -1598,7 +1600,7 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
   // region (ldb_chain.h) carries into the next
   // the replay covers regions [rf, nreg): the run prefix (k_uniform) took everything before x0
   const uint64_t rf = first_region(p), nr = p.nreg - rf;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWPB + wave, nw = (uint64_t)gridDim.x * kWPB;
+  const uint64_t gw = (uint64_t)vb * kWPB + wave, nw = (uint64_t)vg * kWPB;
   const uint64_t per = (nr + nw - 1) / nw;
   const uint64_t rb = rf + gw * per;
   const uint64_t count = rb < p.nreg ? (p.nreg - rb < per ? p.nreg - rb : per) : 0;
@@ -1763,22 +1765,21 @@ __global__ __launch_bounds__(64 * kWPB) void k_scan_main(Pipe p0, const Pipe* __
 // One thread per region: its outgoing link's flag (ldb_pipeline.h fail_flags; every flag of the
 // pipeline is written, the first region's also for the virtual source rf - 1) and its walker claim
 // cleared. ctr[0] counts the broken links.
-template <bool kB>
-__global__ void k_link(Pipe p0, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
-  if (scan_done(p)) return;
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// (k_region phase L; item vb of vg strides over the regions [rf, nreg) in pieces of blockDim)
+__device__ __forceinline__ void link_item(const Pipe& p, uint32_t vb, uint32_t vg) {
   const uint64_t rf = first_region(p);
-  if (r >= p.nreg || r < rf) return;
   uint8_t* fl = fail_flags(p);
-  const bool bad = link_broken(p, r);
-  fl[r - rf + 1] = bad ? 1 : 0;
-  repair_claims(p)[r] = 0;
-  uint32_t nb = bad ? 1u : 0u;
-  if (r == rf) {
-    const bool b0 = p.rs[rf].start != chain_x0(p);
-    fl[0] = b0 ? 1 : 0;
-    nb += b0 ? 1u : 0u;
+  uint32_t nb = 0;
+  for (uint64_t r = rf + (uint64_t)vb * blockDim.x + threadIdx.x; r < p.nreg; r += (uint64_t)vg * blockDim.x) {
+    const bool bad = link_broken(p, r);
+    fl[r - rf + 1] = bad ? 1 : 0;
+    repair_claims(p)[r] = 0;
+    nb += bad ? 1u : 0u;
+    if (r == rf) {
+      const bool b0 = p.rs[rf].start != chain_x0(p);
+      fl[0] = b0 ? 1 : 0;
+      nb += b0 ? 1u : 0u;
+    }
   }
   if (nb) atomicAdd(&p.ctr[0], nb);
 }
@@ -1804,21 +1805,21 @@ struct CohRd {
 //    (the same flags, rewritten), and its first wave runs the serial repair() from those flags.
 // ctr[2] = regions re-run (both phases).
 constexpr int kRepWaves = 16;   // k_repair: as many waves as fit beside the table block
-template <bool kB>
-__global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
-  if (p.ctr[0] == 0 || scan_done(p)) return;
-  // CRC tables in a static LDS array: its address is a link-time constant, so every table read
-  // folds the table base into the ds_read offset field
-  __shared__ __attribute__((aligned(16))) uint32_t tab[kTabWords];
-  __shared__ int s_last;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  copy_tables(tab, p.gtab);
+// (k_region phase R, run only when phase L flagged a broken link: ctr[0]. Item vb of vg: the walkers of
+// phase 1; the workgroup that completes the last item then runs phase 2, repair_item(..., true).)
+static_assert(kRepWaves == kWPB && sizeof(WaveLds) + kBuf <= sizeof(WaveLds) + kNB * kBuf,
+              "k_region: the repair waves use the main phase's per-wave LDS");
+__device__ __forceinline__ void repair_item(const Pipe& p, uint32_t vb, uint32_t vg, uint32_t* tab, uint8_t* smem,
+                                            int& tabs, bool phase2) {
+  if (tabs != kLdsRegion) {
+    copy_tables(tab, p.gtab);
+    __syncthreads();
+    tabs = kLdsRegion;
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  WaveLds* wl = reinterpret_cast<WaveLds*>(smem + wave * (sizeof(WaveLds) + kBuf));
-  uint8_t* buf = smem + wave * (sizeof(WaveLds) + kBuf) + sizeof(WaveLds);
-  __syncthreads();
+  WaveLds* wl = reinterpret_cast<WaveLds*>(smem + wave * (sizeof(WaveLds) + kNB * kBuf));
+  uint8_t* buf = smem + wave * (sizeof(WaveLds) + kNB * kBuf) + sizeof(WaveLds);
   GpuWave wp{lane};
   CohRd rd{&p};
   const int64_t rf = (int64_t)first_region(p);
@@ -1871,8 +1872,9 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
   // one window to several waves measured 4-40x slower: walkers from stale exits walk garbage). Windows
   // are dealt across the CUs first (wave-major), so a file with few windows still gets one CU each.
   uint32_t runs = 0;
-  const uint64_t nwave = (uint64_t)gridDim.x * kRepWaves;
-  for (uint64_t w = (uint64_t)wave * gridDim.x + blockIdx.x; w * 64 < nflag; w += nwave) {
+  const uint64_t nwave = (uint64_t)vg * kRepWaves;
+  if (!phase2)
+  for (uint64_t w = (uint64_t)wave * vg + vb; w * 64 < nflag; w += nwave) {
     const uint64_t b = w * 64;
     uint64_t m = __ballot(b + lane < nflag && fl[b + lane] != 0);
     while (m) {
@@ -1902,16 +1904,9 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
     }
   }
   if (lane == 0 && runs) atomicAdd(&p.ctr[2], runs);
-  // ---- 2. the last workgroup: links again, then the serial repair
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {   // the workgroup's summaries and tuples, released once
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    s_last = atomicAdd(&p.ctr[6], 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (!phase2) return;
+  // ---- 2. the workgroup that completed the last item (every item's summaries and tuples released, then
+  // acquired by k_region): links again, then the serial repair
   uint32_t nb = 0;
   // the flags again, 64 to a thread, with their bitmap word; then the terminal bits (flag_bits)
   uint64_t* fb = flag_bits(p);
@@ -1979,12 +1974,13 @@ __global__ __launch_bounds__(64 * kRepWaves) void k_repair(Pipe p0, const Pipe* 
 }
 
 // ---------------------------------------------------------------- k_combine
-template <bool kB>
-__global__ __launch_bounds__(256) void k_combine(Pipe p0, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
-  if ((uint64_t)blockIdx.x * blockDim.x >= p.nreg || scan_done(p)) return;   // (a batched grid sized for a longer file)
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ uint64_t s_sum[256];
+// (k_region phase C; item vb of vg strides over the kBlkRegions-region blocks, one thread per region)
+static_assert(kBlkRegions == 64 * kWPB, "k_region: one thread per region of a block");
+__device__ __forceinline__ void combine_item(const Pipe& p, uint32_t vb, uint32_t vg, uint64_t* s_sum) {
+  const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint64_t b = vb; b < nblk; b += vg) {
+  const uint64_t r = b * kBlkRegions + threadIdx.x;
   uint64_t cnt = 0;
   if (r < p.nreg && r >= first_region(p)) {
     const int32_t st = p.rs[r].status;
@@ -2003,13 +1999,17 @@ __global__ __launch_bounds__(256) void k_combine(Pipe p0, const Pipe* __restrict
       }
     }
   }
-  s_sum[threadIdx.x] = cnt;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (lane == 0) s_sum[wave] = cnt;
   __syncthreads();
-  for (int o = 128; o; o >>= 1) {
-    if (threadIdx.x < o) s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kBlkRegions / 64; ++w) t += s_sum[w];
+    p.blk[b] = t;
   }
-  if (threadIdx.x == 0) p.blk[blockIdx.x] = s_sum[0];   // blockDim == kBlkRegions
+  __syncthreads();   // (s_sum is reused by the next block)
+  }
 }
 
 __device__ __forceinline__ void decode_entry_global(const Pipe& p, uint64_t off, ldb_entry* out) {
@@ -2097,21 +2097,14 @@ __global__ __launch_bounds__(64) void k_serial(Pipe p0, int only_on_overflow, co
 // counts (k_combine), its regions are scanned in LDS, and tuples are copied flat (thread j of
 // the block's output range finds its region by binary search). The block holding the terminal
 // region writes the ldb_scan_result.
-__device__ __forceinline__ void compact_body(const Pipe& p);
-template <bool kB>
-__global__ __launch_bounds__(kBlkRegions) void k_compact(Pipe p0, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
-  compact_body(p);
-}
-__device__ __forceinline__ void compact_body(const Pipe& p) {
-  if (scan_done(p)) return;   // uni_finish wrote the result
-  if (p.ctr[1]) {   // a region overflowed its tuple slots (k_combine): the serial walker redoes the scan
-    if (blockIdx.x == 0 && threadIdx.x == 0) serial_walk(p);
+// (k_region phase K; item vb of vg strides over the blocks. LDS: s_off kBlkRegions + 1 words, s_wsum and s_part
+// one word per wave)
+__device__ __forceinline__ void compact_item(const Pipe& p, uint32_t vb, uint32_t vg, uint32_t* s_off, uint32_t* s_wsum,
+                                             uint64_t* s_part) {
+  if (p.ctr[1]) {   // a region overflowed its tuple slots (phase C): the serial walker redoes the scan
+    if (vb == 0 && threadIdx.x == 0) serial_walk(p);
     return;
   }
-  __shared__ uint32_t s_off[kBlkRegions + 1];
-  __shared__ uint32_t s_wsum[kBlkRegions / 64];
-  __shared__ uint64_t s_part[kBlkRegions / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t T = p.tpos[0];
   uint64_t tp = term_pos(T);
@@ -2119,7 +2112,7 @@ __device__ __forceinline__ void compact_body(const Pipe& p) {
   if (T == ~0ull) { tp = p.len; ts = LDB_ERR_MALFORMED; }  // unreachable: the chain always stops
   const uint64_t rf = first_region(p), K = run_k(p);      // the run prefix's tuples are out[0, K)
   if (rf >= p.nreg) {   // the replay stops right after the run: io.EOF at x0 (log_file.go:117-122)
-    if (blockIdx.x == 0 && tid == 0) {
+    if (vb == 0 && tid == 0) {
       ldb_scan_result res;
       res.status = LDB_EOF_WINDOW;
       res.fid = p.fid;
@@ -2140,7 +2133,7 @@ __device__ __forceinline__ void compact_body(const Pipe& p) {
   const uint64_t lastR = regT < p.nreg ? regT : p.nreg - 1;
   // a capped grid strides over the blocks (a file the run prefix took whole launches few workgroups)
   const uint64_t nblk = (p.nreg + kBlkRegions - 1) / kBlkRegions;
-  for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+  for (uint64_t b = vb; b < nblk; b += vg) {
   const uint64_t r0 = b * kBlkRegions;
   if (r0 > lastR) break;
   // base = sum of the counts of every earlier block (all their regions precede the terminal)
@@ -2238,9 +2231,227 @@ __global__ __launch_bounds__(256) void k_read_reduce(const uint4* __restrict__ p
 
 #include "ldb_sweep_kern.h"
 
-size_t main_lds_bytes() { return kWPB * (sizeof(WaveLds) + kNB * kBuf); }   // dynamic part (tables are static)
-size_t repair_lds_bytes() { return kRepWaves * (sizeof(WaveLds) + kBuf); }
-static_assert(kRepWaves * (sizeof(WaveLds) + kBuf) + kTabBytes + 64 <= 160 * 1024, "k_repair: LDS per workgroup");
+// ---------------------------------------------------------------- k_sweep, k_region
+// Everything after the run prefix, in two launches (rounds 1-5: seven, k_sweep, k_sweep_fin, k_scan_main,
+// k_link, k_repair, k_combine, k_compact; on a file the run prefix covers each returned at its first
+// instruction, ~10-14 us of every config-2/4 step, profiles/r06_tail_ab.txt):
+//   k_sweep   the sweep tier (ldb_sweep.h): S its stream (sweep_item), then the links between its runs
+//             (sweep_last); F its per-entry CRC checks and tuples (fin_item), then where it ends (sw_finish)
+//   k_region  the region pipeline from where the run prefix and the sweep tier stopped: M the regions
+//             (main_item), L their links (link_item), R the repair when a link broke (repair_item), C the
+//             cross-region CRCs and block counts (combine_item), K the compaction (compact_item)
+// The scan may end after any phase (the run prefix's uni_finish or sw_finish writes the result and the done
+// word): every workgroup then returns. Each phase is a number of items, the workgroups of the launch that
+// kernel used to have, claimed one at a time from a ticket counter by the workgroups that are running; the
+// workgroup that completes a phase's last item runs its follow-up (links, finish, serial repair) and
+// publishes the phase, and every workgroup waits for that before its next phase. A workgroup only ever waits
+// after the phase's tickets are all taken, i.e. for items that running workgroups hold, so a launch cannot
+// deadlock however few of its workgroups are resident (another stream's kernels, a smaller chip).
+// Completion releases at agent scope and the wait acquires, as the kernel boundaries did (L2 write-back
+// across the XCDs). One launch for all seven phases was measured and rejected: the region code's register
+// pressure spilled every phase's values to scratch (224-272 B per lane, and a wave's first scratch access
+// costs at launch scale, tools/microbench/mb_scratch.hip): the sweep's stream 5-7 % and its checks 45 us
+// slower (profiles/r06_tail_fused_ab.txt). The sweep tier alone spills nothing on its usual path.
+constexpr int kPhS = 0, kPhF = 1, kPhM = 2, kPhL = 3, kPhR = 4, kPhC = 5, kPhK = 6, kNPh = 7;
+constexpr uint32_t kMainLds = kWPB * (sizeof(WaveLds) + kNB * kBuf);
+constexpr uint32_t kCompactWsum = (4 * (kBlkRegions + 1) + 15) & ~15u, kCompactPart = kCompactWsum + 4 * kWPB;
+constexpr uint32_t kCompactLds = kCompactPart + 8 * kWPB;
+constexpr uint32_t cmax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+constexpr uint32_t kSweepLds = cmax(cmax(kSwLds, kSwLinkLds), kSwFinLds);
+constexpr uint32_t kRegionLds = cmax(kTabBytes + kMainLds, kCompactLds);
+static_assert(kTabBytes % 16 == 0 && kLp2Bytes % 256 == 0, "LDS carve alignment");
+static_assert(kSweepLds + 64 <= 160 * 1024 && kRegionLds + 64 <= 160 * 1024, "LDS per workgroup");
+static_assert(kRepWaves == kWPB && kSwWaves == kWPB, "every phase runs kWPB waves");
+
+// item counts: the grids the kernels had (every phase has at least one item: its last one runs the
+// follow-up and publishes it)
+__device__ __forceinline__ uint32_t tail_items(uint64_t want, uint32_t ncu) {
+  return (uint32_t)(want < 1 ? 1 : (want < ncu ? want : ncu));
+}
+
+// the pipe, fetched again in every phase through a pointer the compiler cannot see through (the kernel
+// argument itself, p0 at the kernarg segment's offset 0; a batched launch's device array), so no phase holds
+// another's Pipe fields in registers. Made in the kernel's own body (the kernarg segment pointer exists only
+// there), every use inlined.
+typedef __attribute__((address_space(4))) const Pipe* CPipe;
+template <bool kB>
+struct PipeSrc {
+  const Pipe* pb;
+  CPipe ka;
+  __device__ __forceinline__ const Pipe& get() const {
+    if constexpr (kB) {
+      const Pipe* q = pb + blockIdx.y;
+      asm volatile("" : "+s"(q));
+      return *q;
+    } else {
+      CPipe q = ka;
+      asm volatile("" : "+s"(q));
+      return *(const Pipe*)q;
+    }
+  }
+};
+#define LDB_PIPE_SRC(kB) const PipeSrc<kB> src{pb, (CPipe)__builtin_amdgcn_kernarg_segment_ptr()}
+
+// The phase protocol over Pipe::tail: [0, 8) tickets, [8, 16) items done, [16, 24) published, then the phases'
+// start stamps (u64 [16, 24)). s_tail_tk / s_tail_fl: the workgroup's broadcast words.
+__shared__ uint32_t s_tail_tk;
+__shared__ int s_tail_fl;
+struct TailSync {
+  __device__ __forceinline__ uint32_t claim(const Pipe& p, int ph) const {
+    __syncthreads();   // (every thread has read the previous ticket)
+    if (threadIdx.x == 0) {
+      s_tail_tk = atomicAdd(&p.tail[ph], 1u);
+      if (s_tail_tk == 0) reinterpret_cast<uint64_t*>(p.tail + 32)[ph] = __builtin_amdgcn_s_memrealtime();
+    }
+    __syncthreads();
+    return s_tail_tk;
+  }
+  __device__ __forceinline__ bool complete(const Pipe& p, int ph, uint32_t n) const {   // true in the workgroup that completed the last item
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      s_tail_fl = atomicAdd(&p.tail[8 + ph], 1u) == n - 1;
+    }
+    __syncthreads();
+    const bool last = s_tail_fl != 0;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return last;
+  }
+  __device__ __forceinline__ void publish(const Pipe& p, int ph) const {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (p.tacc) {
+        const uint64_t t0 = __hip_atomic_load(reinterpret_cast<uint64_t*>(p.tail + 32) + ph, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd((unsigned long long*)&p.tacc[ph], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&p.tail[16 + ph], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __device__ __forceinline__ void wait(const Pipe& p, int ph) const {
+    if (threadIdx.x == 0)
+      while (__hip_atomic_load(&p.tail[16 + ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(4);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  // a phase whose items are cheap or rare: the plain claim loop
+  template <class Body, class Last>
+  __device__ __forceinline__ void loop(const Pipe& p, int ph, uint32_t n, Body body, Last last) const {
+    for (uint32_t t; (t = claim(p, ph)) < n;) {
+      body(t);
+      if (complete(p, ph, n)) {
+        last(t);
+        publish(p, ph);
+      }
+    }
+    wait(p, ph);
+  }
+  // the first item peeled off the claim loop (a workgroup's usual share is one item): what the compiler
+  // hoists out of a loop and holds across it then stays in the loop's copy, and the usual path holds nothing
+  // over the item (k_sweep: no scratch access outside the loop copy)
+  template <class Body, class Last>
+  __device__ __forceinline__ void peeled(const Pipe& p, int ph, uint32_t n, Body body, Last last) const {
+    uint32_t t = claim(p, ph);
+    if (t < n) {
+      body(t);
+      if (complete(p, ph, n)) {
+        last(t);
+        publish(p, ph);
+      }
+      loop(p, ph, n, body, last);
+    } else {
+      wait(p, ph);
+    }
+  }
+};
+__device__ __forceinline__ bool tail_done(const Pipe& p) {   // after a wait: the scan ended in the phase just published
+  return __builtin_amdgcn_readfirstlane((uint32_t)(__hip_atomic_load(&p.dyn[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                                   kUniDone)) != 0u;
+}
+
+template <bool kB>
+__global__ __launch_bounds__(64 * kWPB) void k_sweep(Pipe p0, const Pipe* __restrict__ pb, uint32_t ncu) {
+  __shared__ __attribute__((aligned(256))) uint8_t lds[kSweepLds];
+  (void)p0;   // (read through src)
+  LDB_PIPE_SRC(kB);
+  if (!src.get().sweep || scan_done(src.get())) return;   // (uni_finish ended the scan)
+  const TailSync ts;
+  int tabs = kLdsNone;
+  {
+    const Pipe& p = src.get();
+    const uint32_t nS = tail_items((p.len / kSwBatch + 2 + kSwWaves - 1) / kSwWaves, ncu);
+    ts.peeled(
+        p, kPhS, nS,
+        [&](uint32_t t) __attribute__((always_inline)) {
+          sweep_item(src.get(), t, nS, lds, reinterpret_cast<uint32_t*>(lds + kLp2Bytes),
+                     reinterpret_cast<uint32_t*>(lds + kLp2Bytes + 9 * 1024 * 4), tabs);
+        },
+        [&](uint32_t) __attribute__((always_inline)) {
+          sweep_last(src.get(), nS, lds);
+          tabs = kLdsNone;
+        });
+  }
+  {
+    const Pipe& p = src.get();
+    const uint64_t ncov = __hip_atomic_load(&p.swctl->ncov, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t nF = tail_items((ncov + kSwWaves - 1) / kSwWaves, ncu);
+    ts.peeled(
+        p, kPhF, nF, [&](uint32_t t) __attribute__((always_inline)) { fin_item(src.get(), t, nF, reinterpret_cast<uint32_t*>(lds), tabs); },
+        [&](uint32_t) __attribute__((always_inline)) {
+          if (threadIdx.x < 64) sw_finish(src.get());
+        });
+  }
+}
+
+template <bool kB>
+__global__ __launch_bounds__(64 * kWPB) void k_region(Pipe p0, const Pipe* __restrict__ pb, uint32_t ncu) {
+  __shared__ __attribute__((aligned(256))) uint8_t lds[kRegionLds];
+  (void)p0;   // (read through src)
+  LDB_PIPE_SRC(kB);
+  if (scan_done(src.get())) return;   // the run prefix or the sweep tier ended the scan
+  const TailSync ts;
+  int tabs = kLdsNone;
+  uint32_t* const tab = reinterpret_cast<uint32_t*>(lds);
+  uint8_t* const smem = lds + kTabBytes;
+  auto none = [](uint32_t) __attribute__((always_inline)) {};
+  {
+    const Pipe& p = src.get();
+    const uint32_t nM = tail_items((p.nreg + kWPB - 1) / kWPB, ncu);
+    ts.loop(p, kPhM, nM, [&](uint32_t t) __attribute__((always_inline)) { main_item(src.get(), t, nM, tab, smem, tabs); }, none);
+  }
+  {
+    const Pipe& p = src.get();
+    const uint32_t nL = tail_items((p.nreg - first_region(p) + blockDim.x - 1) / blockDim.x, ncu);
+    ts.loop(p, kPhL, nL, [&](uint32_t t) __attribute__((always_inline)) { link_item(src.get(), t, nL); }, none);
+  }
+  {
+    const Pipe& p = src.get();
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&p.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u) {
+      const uint32_t nR = tail_items((p.nreg + 1 + 63) / 64, ncu);
+      ts.loop(
+          p, kPhR, nR, [&](uint32_t t) __attribute__((always_inline)) { repair_item(src.get(), t, nR, tab, smem, tabs, false); },
+          [&](uint32_t t) __attribute__((always_inline)) { repair_item(src.get(), t, nR, tab, smem, tabs, true); });
+    }
+  }
+  tabs = kLdsNone;   // (phases C and K use the LDS as scratch)
+  {
+    const Pipe& p = src.get();
+    const uint32_t nC = tail_items((p.nreg + kBlkRegions - 1) / kBlkRegions, ncu);
+    ts.loop(p, kPhC, nC, [&](uint32_t t) __attribute__((always_inline)) { combine_item(src.get(), t, nC, reinterpret_cast<uint64_t*>(lds)); }, none);
+  }
+  {
+    const Pipe& p = src.get();
+    const uint32_t nK = tail_items((p.nreg + kBlkRegions - 1) / kBlkRegions, ncu);
+    for (uint32_t t; (t = ts.claim(p, kPhK)) < nK;) {   // (the last phase: nothing waits for it)
+      compact_item(src.get(), t, nK, reinterpret_cast<uint32_t*>(lds), reinterpret_cast<uint32_t*>(lds + kCompactWsum),
+                   reinterpret_cast<uint64_t*>(lds + kCompactPart));
+      if (ts.complete(p, kPhK, nK)) ts.publish(p, kPhK);
+    }
+  }
+}
 
 }  // namespace
 
@@ -2252,6 +2463,7 @@ struct ldb_ctx {
   uint32_t* d_xw = nullptr;    // kW + 1
   uint32_t* d_gsh = nullptr;   // kGsWords register-shift tables (k_combine)
   uint32_t* d_swt = nullptr;   // kSwTabWords: the sweep tier's shift and slicing-by-16 tables (ldb_sweep.h)
+  uint64_t* d_tacc = nullptr;  // the tail kernels' per-phase time accumulators (s_memrealtime ticks), read by ldb_kernel_timing_tail
   uint8_t* ws = nullptr;       // workspace
   uint64_t ws_bytes = 0;
   // Workspace fence: the event recorded after the last pipeline enqueued on this context, and the
@@ -2264,9 +2476,8 @@ struct ldb_ctx {
   uint32_t scan_epoch = 0;   // device scans enqueued on this context (Pipe::epoch)
   // kernel timing: one event triple per timed launch, recorded without host synchronisation and
   // resolved when the timing is queried (or when the pool is full)
-  // start, after k_uniform, after its fill (device path: after the sweep tier), after k_scan_main, end; es:
-  // between k_sweep and k_sweep_fin (recorded only where the sweep tier runs, else = ef)
-  struct EvTriple { hipEvent_t e0, eu, ef, e1, e2, es; };
+  // start, after the run prefix (k_uniform, and a chunked scan's fills), after k_sweep, after k_region (the end)
+  struct EvTriple { hipEvent_t e0, eu, es, e2; };
   std::vector<EvTriple> evs;
   size_t ev_used = 0;
   bool timing = false;
@@ -2284,7 +2495,9 @@ struct ldb_ctx {
   int n_cp = 0;
   hipStream_t cp[kMaxCp] = {};
   std::vector<hipEvent_t> chunk_ev;
-  double t_run = 0, t_fill = 0, t_main = 0, t_total = 0, t_sweep = 0;
+  double t_run = 0, t_sweep = 0, t_main = 0, t_total = 0;
+  double t_ph[8] = {};   // k_sweep's and k_region's phases (device clock, d_tacc), summed over the timed scans
+  double rt_khz = 100000.0;   // the device's constant clock (s_memrealtime)
   uint64_t t_n = 0;
   // batched scans (enqueue_scan_batch): page-locked staging of the per-file Pipes, reused once the
   // copy of the previous batch has completed (pipes_ev)
@@ -2313,23 +2526,27 @@ __attribute__((visibility("hidden"))) int ldb_ctx_device_(ldb_ctx* c) { return c
 __attribute__((visibility("hidden"))) void** ldb_ctx_merge_slot_(ldb_ctx* c) { return &c->merge; }
 
 static int resolve_timing(ldb_ctx* c) {
+  if (!c->ev_used) return LDB_OK;
   for (size_t i = 0; i < c->ev_used; ++i) {
     const ldb_ctx::EvTriple& t = c->evs[i];
     if (hipEventSynchronize(t.e2) != hipSuccess) return LDB_ERR_HIP;
-    float u = 0, f = 0, a = 0, b = 0;
-    if (hipEventElapsedTime(&u, t.e0, t.eu) != hipSuccess || hipEventElapsedTime(&f, t.eu, t.ef) != hipSuccess ||
-        hipEventElapsedTime(&a, t.ef, t.e1) != hipSuccess || hipEventElapsedTime(&b, t.e0, t.e2) != hipSuccess)
+    float u = 0, w = 0, a = 0, b = 0;
+    if (hipEventElapsedTime(&u, t.e0, t.eu) != hipSuccess || hipEventElapsedTime(&w, t.eu, t.es) != hipSuccess ||
+        hipEventElapsedTime(&a, t.es, t.e2) != hipSuccess || hipEventElapsedTime(&b, t.e0, t.e2) != hipSuccess)
       return LDB_ERR_HIP;
     c->t_run += u;
-    c->t_fill += f;
-    float sw = 0;
-    if (hipEventElapsedTime(&sw, t.eu, t.es) != hipSuccess) return LDB_ERR_HIP;
-    c->t_sweep += sw;
+    c->t_sweep += w;
     c->t_main += a;
     c->t_total += b;
     c->t_n += 1;
   }
   c->ev_used = 0;
+  // the tail kernels' phase accumulators (every timed scan has completed: its e2 fired)
+  uint64_t acc[8];
+  if (hipMemcpy(acc, c->d_tacc, sizeof(acc), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemset(c->d_tacc, 0, sizeof(acc)) != hipSuccess)
+    return LDB_ERR_HIP;
+  for (int k = 0; k < 8; ++k) c->t_ph[k] += (double)acc[k] / c->rt_khz;
   return LDB_OK;
 }
 
@@ -2337,7 +2554,7 @@ namespace {
 
 struct WsLayout {
   uint64_t nreg, nblk;
-  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_dyn, o_uni, o_blk, o_swrw, o_swrg, o_swpl, o_swrun, o_swctl, total;
+  uint64_t o_rs, o_scratch, o_fail, o_ctr, o_tpos, o_dyn, o_uni, o_blk, o_swrw, o_swrg, o_swpl, o_swrun, o_swctl, o_tail, total;
 };
 
 WsLayout layout(uint64_t len) {
@@ -2368,6 +2585,7 @@ WsLayout layout(uint64_t len) {
   L.o_swpl = take(4 * ((len + kSwBatch) / 64 + 1));
   L.o_swrun = take(sizeof(SwRun) * (uint64_t)kSwMaxRuns);
   L.o_swctl = take(sizeof(SwCtl));
+  L.o_tail = take(kTailCtlBytes);   // the tail kernels' control words
   L.total = o;
   return L;
 }
@@ -2387,6 +2605,12 @@ int ensure_ws(ldb_ctx* c, uint64_t bytes) {
   if (hipMalloc(&c->ws, bytes) != hipSuccess) return LDB_ERR_NOMEM;
   c->ws_bytes = bytes;
   return LDB_OK;
+}
+
+// LDB_SWEEP=0 turns the sweep tier off (A/B: the region pipeline from the run prefix's end, rounds 1-4)
+bool sweep_enabled() {
+  static const bool on = getenv("LDB_SWEEP") == nullptr || atoi(getenv("LDB_SWEEP")) != 0;
+  return on;
 }
 
 Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, uint32_t fid, int io, int kind,
@@ -2421,6 +2645,9 @@ Pipe make_pipe(ldb_ctx* c, const WsLayout& L, const uint8_t* img, uint64_t len, 
   p.swctl = reinterpret_cast<SwCtl*>(w + L.o_swctl);
   p.swt = c->d_swt;
   p.scratch_bytes = sizeof(ldb_index_tuple) * (uint64_t)kRegionCap * L.nreg;
+  p.tail = reinterpret_cast<uint32_t*>(w + L.o_tail);
+  p.tacc = c->timing ? c->d_tacc : nullptr;
+  p.sweep = sweep_enabled() ? 1u : 0u;
   return p;
 }
 
@@ -2461,9 +2688,7 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
       ldb_ctx::EvTriple t{};
       LDB_HIP(hipEventCreate(&t.e0));
       LDB_HIP(hipEventCreate(&t.eu));
-      LDB_HIP(hipEventCreate(&t.ef));
       LDB_HIP(hipEventCreate(&t.es));
-      LDB_HIP(hipEventCreate(&t.e1));
       LDB_HIP(hipEventCreate(&t.e2));
       c->evs.push_back(t);
     } else {
@@ -2480,25 +2705,30 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
 // the control words every region pipeline starts from (enqueue_scan)
 // dyn: [0] K (dyn_val: ~0 = no failure seen, 0 = no run), [1] entry size, [2] setup flag, [3] done
 // flag (uni_finish), [4] k_uniform's done counter, [5] x0 (uni_finish), [6] runs published (uni_discover)
-__global__ __launch_bounds__(64) void k_init(uint32_t* ctr, uint64_t* dyn, uint64_t dyn_val) {
-  if (threadIdx.x < 8) ctr[threadIdx.x] = 0u;
-  if (threadIdx.x < 3) dyn[threadIdx.x] = dyn_val;
-  if (threadIdx.x == 3 || threadIdx.x == 4 || threadIdx.x == 6 || threadIdx.x == 7) dyn[threadIdx.x] = 0;
-  if (threadIdx.x == 5) dyn[5] = ~0ull;   // x0 not finished: K sz (no run: 0)
+// the tail kernels' control words and the sweep tier's (every path but the device path's run prefix, which sets
+// them in k_uniform's workgroup 0)
+__device__ __forceinline__ void tail_init(const Pipe& p, uint32_t t) {
+  if (t < kTailCtlBytes / 4) p.tail[t] = 0u;
+  if (t == 0) {
+    p.swctl->fail = ~0ull;
+    p.swctl->state = 0;
+  }
+}
+__global__ __launch_bounds__(64) void k_init(Pipe p, uint64_t dyn_val) {
+  if (threadIdx.x < 8) p.ctr[threadIdx.x] = 0u;
+  if (threadIdx.x < 3) p.dyn[threadIdx.x] = dyn_val;
+  if (threadIdx.x == 3 || threadIdx.x == 4 || threadIdx.x == 6 || threadIdx.x == 7) p.dyn[threadIdx.x] = 0;
+  if (threadIdx.x == 5) p.dyn[5] = ~0ull;   // x0 not finished: K sz (no run: 0)
+  tail_init(p, threadIdx.x);
 }
 
-// persistent k_scan_main workgroups: exactly those resident at once (LDS-limited), so no second
-// dispatch round leaves a tail
-int scan_main_grid(const ldb_ctx* c, uint64_t nreg) {
-  const int per_cu = LDB_BLOCKS_PER_CU > 0 ? LDB_BLOCKS_PER_CU
-                                           : std::max(1, (int)(163840 / (main_lds_bytes() + kTabBytes)));
-  return (int)std::min<uint64_t>((nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu * per_cu);
+// k_sweep, k_region: one workgroup per CU (their LDS), fewer for a file whose phases have fewer items
+// (tail_items: the sweep's stream, the region pipeline's main phase)
+int sweep_grid(const ldb_ctx* c, uint64_t len) {
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((len / kSwBatch + 2 + kSwWaves - 1) / kSwWaves, (uint64_t)c->n_cu));
 }
-
-// k_repair's workgroups: one per CU (fewer for tiny files; they exit at once when k_link found no
-// broken link), so the walkers of a file with many failures spread over the whole chip
-int repair_grid(const ldb_ctx* c, uint64_t nreg) {
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>((nreg + 1 + 63) / 64, (uint64_t)c->n_cu));
+int region_grid(const ldb_ctx* c, uint64_t nreg) {
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((nreg + kWPB - 1) / kWPB, (uint64_t)c->n_cu));
 }
 
 int uniform_grid(const ldb_ctx* c, uint64_t bytes) {
@@ -2511,16 +2741,6 @@ int fill_grid(const ldb_ctx* c, uint64_t bytes) {
   return std::max(1, (int)std::min<uint64_t>(bytes / 16 / kFillThreads + 1, (uint64_t)c->n_cu * 2));
 }
 
-// k_sweep: one workgroup of kSwWaves per CU (the LP2 block), fewer for a file of few batches
-int sweep_grid(const ldb_ctx* c, uint64_t len) {
-  const uint64_t batches = len / kSwBatch + 2;
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>((batches + kSwWaves - 1) / kSwWaves, (uint64_t)c->n_cu));
-}
-// LDB_SWEEP=0 turns the sweep tier off (A/B: the region pipeline from the run prefix's end, rounds 1-4)
-bool sweep_enabled() {
-  static const bool on = getenv("LDB_SWEEP") == nullptr || atoi(getenv("LDB_SWEEP")) != 0;
-  return on;
-}
 
 // An image that is still being copied in: bytes [0, avail[i]) are in place once ev[i] has fired
 // (avail ascending, the last = len). The run prefix then verifies its candidates chunk by chunk,
@@ -2576,7 +2796,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   // launch fewer, ~4.5 us of every such scan
   p.epoch = ++c->scan_epoch;
   const bool fold_init = !no_run && !chunked && !p.hash_out && LDB_FOLD_INIT;
-  if (!fold_init) hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, s, p.ctr, p.dyn, no_run ? 0ull : ~0ull);
+  if (!fold_init) hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, s, p, no_run ? 0ull : ~0ull);
   if (!no_run) {
     auto launch = [&](uint64_t lo, uint64_t hi) {
       const int ug = uniform_grid(c, hi - lo);
@@ -2597,47 +2817,20 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
           hipLaunchKernelGGL(k_uniform_fill<true>, dim3(fill_grid(c, hi - lo)), dim3(kFillThreads), 0, s, p, lo, hi);
         lo = hi;
       }
-      if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-      if (ev) LDB_HIP(hipEventRecord(ev->es, s));
-      if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     } else {
       launch(0, len);   // its workgroups also write the runs' INDEX tuples (uni_post_fill)
-      if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-#ifdef LDB_TAIL_ABL   // attribution builds only (results wrong unless the run prefix covers the file): 1 no tail, 2 one launch
-      if (LDB_TAIL_ABL == 2)
-        hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)std::min<uint64_t>(L.nblk, 4ull * c->n_cu)), dim3(kBlkRegions), 0, s,
-                           p, nullptr);
-      if (ev) {
-        LDB_HIP(hipEventRecord(ev->es, s));
-        LDB_HIP(hipEventRecord(ev->ef, s));
-        LDB_HIP(hipEventRecord(ev->e1, s));
-        LDB_HIP(hipEventRecord(ev->e2, s));
-      }
-      return fence_ws(c, s);
-#endif
-      if (fold_init && sweep_enabled()) {   // the sweep tier from the run prefix's end (ldb_sweep.h)
-        hipLaunchKernelGGL(k_sweep, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p);
-        if (ev) LDB_HIP(hipEventRecord(ev->es, s));
-        hipLaunchKernelGGL(k_sweep_fin, dim3(LDB_FIN_WPE * c->n_cu), dim3(64 * kSwFinWaves), 0, s, p);
-      } else if (ev) {
-        LDB_HIP(hipEventRecord(ev->es, s));
-      }
-      if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
     }
-  } else if (ev) {
-    LDB_HIP(hipEventRecord(ev->eu, s));
-    LDB_HIP(hipEventRecord(ev->es, s));
-    LDB_HIP(hipEventRecord(ev->ef, s));
   }
-  hipLaunchKernelGGL(k_scan_main<false>, dim3(scan_main_grid(c, L.nreg)), dim3(64 * kWPB), main_lds_bytes(), s, p, nullptr);
-  if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
-  const int g256 = (int)((L.nreg + 255) / 256);
-  hipLaunchKernelGGL(k_link<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
-  hipLaunchKernelGGL(k_repair<false>, dim3(repair_grid(c, L.nreg)), dim3(64 * kRepWaves), repair_lds_bytes(), s, p,
-                     nullptr);
-  hipLaunchKernelGGL(k_combine<false>, dim3(g256), dim3(256), 0, s, p, nullptr);
-  hipLaunchKernelGGL(k_compact<false>, dim3((unsigned)std::min<uint64_t>(L.nblk, 4ull * c->n_cu)), dim3(kBlkRegions), 0, s, p,
-                     nullptr);
+  if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+#ifdef LDB_TAIL_ABL   // attribution builds only (results wrong unless the run prefix covers the file): no tail
+  if (ev) LDB_HIP(hipEventRecord(ev->es, s));
+  if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
+  return fence_ws(c, s);
+#endif
+  // everything after the run prefix: the sweep tier (k_sweep), then the region pipeline (k_region)
+  hipLaunchKernelGGL(k_sweep<false>, dim3(sweep_grid(c, len)), dim3(64 * kWPB), 0, s, p, nullptr, (uint32_t)c->n_cu);
+  if (ev) LDB_HIP(hipEventRecord(ev->es, s));
+  hipLaunchKernelGGL(k_region<false>, dim3(region_grid(c, L.nreg)), dim3(64 * kWPB), 0, s, p, nullptr, (uint32_t)c->n_cu);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
@@ -2670,6 +2863,7 @@ __global__ __launch_bounds__(64) void k_batch_init(const Pipe* __restrict__ pb) 
   if (threadIdx.x < 8) p.ctr[threadIdx.x] = 0u;
   if (threadIdx.x < 4 || threadIdx.x == 5) p.dyn[threadIdx.x] = ~0ull;   // [3]: not done; [5]: x0 = K sz
   if (threadIdx.x == 4 || threadIdx.x == 6 || threadIdx.x == 7) p.dyn[threadIdx.x] = 0;
+  tail_init(p, threadIdx.x);
 }
 
 int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s) {
@@ -2681,8 +2875,8 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   std::vector<WsLayout> Ls(nf);
   std::vector<uint64_t> off(nf);
   uint64_t o = (sizeof(Pipe) * (uint64_t)nf + 255) & ~255ull;
-  int ug = 1, mg = 1;
-  uint64_t nblk = 1, max_nreg = 1;
+  int ug = 1;
+  uint64_t max_len = 0, max_nreg = 1;
   for (int i = 0; i < nf; ++i) {
     if (!batch_eligible(f[i].img, f[i].len) || !f[i].res || (f[i].cap && !f[i].out) ||
         (f[i].hash_out != nullptr) != hashed)
@@ -2691,8 +2885,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     off[i] = o;
     o += Ls[i].total;
     ug = std::max(ug, uniform_grid(c, f[i].len));
-    mg = std::max(mg, scan_main_grid(c, Ls[i].nreg));
-    nblk = std::max(nblk, Ls[i].nblk);
+    max_len = std::max(max_len, f[i].len);
     max_nreg = std::max(max_nreg, Ls[i].nreg);
   }
   int rc = ensure_ws(c, o);
@@ -2715,15 +2908,10 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   }
   const Pipe* d_pipes = reinterpret_cast<const Pipe*>(c->ws);
   const Pipe p0{};   // unused by the kB instances
-  // the region pipeline and the repair walkers: the chip's resident workgroups dealt over the files,
-  // not one file's grid per file (16 files of 256 MiB launched 16 x 256 k_scan_main workgroups that
-  // queue behind each other even when every run prefix covered its file; LDB_BATCH_SPREAD=0: A/B)
-  static const bool spread = getenv("LDB_BATCH_SPREAD") == nullptr || atoi(getenv("LDB_BATCH_SPREAD")) != 0;
-  int rg = repair_grid(c, max_nreg);
-  if (spread) {
-    mg = std::min(mg, std::max(1, (scan_main_grid(c, ~0ull >> 8) + nf - 1) / nf));
-    rg = std::min(rg, std::max(1, (c->n_cu + nf - 1) / nf));
-  }
+  // k_sweep, k_region: the chip's workgroups dealt over the files, not one file's grid per file (round 3: 16 files of
+  // 256 MiB launched 16 x 256 k_scan_main workgroups that queued behind each other even when every run
+  // prefix covered its file; profiles/r03_s35_merge_spread_ab.json, r04_batch_spread_writer_mix_ab.txt)
+  const int tg = std::max(1, (c->n_cu + nf - 1) / nf);
   rc = ws_wait(c, s);
   if (rc != LDB_OK) return rc;
   LDB_HIP(hipMemcpyAsync(const_cast<Pipe*>(d_pipes), c->h_pipes, sizeof(Pipe) * (size_t)nf, hipMemcpyHostToDevice, s));
@@ -2754,16 +2942,11 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
+  hipLaunchKernelGGL(k_sweep<true>, dim3(std::min(tg, sweep_grid(c, max_len)), n), dim3(64 * kWPB), 0, s, p0, d_pipes,
+                     (uint32_t)c->n_cu);
   if (ev) LDB_HIP(hipEventRecord(ev->es, s));
-  if (ev) LDB_HIP(hipEventRecord(ev->ef, s));
-  hipLaunchKernelGGL(k_scan_main<true>, dim3(mg, n), dim3(64 * kWPB), main_lds_bytes(), s, p0, d_pipes);
-  if (ev) LDB_HIP(hipEventRecord(ev->e1, s));
-  hipLaunchKernelGGL(k_link<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
-  hipLaunchKernelGGL(k_repair<true>, dim3(rg, n), dim3(64 * kRepWaves), repair_lds_bytes(), s,
-                     p0, d_pipes);
-  hipLaunchKernelGGL(k_combine<true>, dim3((unsigned)nblk, n), dim3(256), 0, s, p0, d_pipes);
-  hipLaunchKernelGGL(k_compact<true>, dim3((unsigned)std::min<uint64_t>(nblk, 4ull * c->n_cu), n), dim3(kBlkRegions), 0, s,
-                     p0, d_pipes);
+  hipLaunchKernelGGL(k_region<true>, dim3(std::min(tg, region_grid(c, max_nreg)), n), dim3(64 * kWPB), 0, s, p0, d_pipes,
+                     (uint32_t)c->n_cu);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
@@ -2841,6 +3024,8 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
   c->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0) c->rt_khz = khz;
   std::vector<uint32_t> tab(kTabWords), xw(kW + 1), gsh(kGsWords), swt(kSwTabWords);
   build_tables(tab.data());
   for (int n = 0; n <= kW; ++n) xw[n] = x8n_modp((uint64_t)n);
@@ -2858,16 +3043,9 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }
-  if (hipFuncSetAttribute((const void*)k_scan_main<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)main_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_scan_main<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)main_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_repair<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)repair_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_repair<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)repair_lds_bytes()) != hipSuccess) {
+  if (hipMalloc(&c->d_tacc, 8 * 8) != hipSuccess || hipMemset(c->d_tacc, 0, 8 * 8) != hipSuccess) {
     ldb_ctx_destroy(c);
-    return LDB_ERR_HIP;
+    return LDB_ERR_NOMEM;
   }
   *out = c;
   return LDB_OK;
@@ -2881,6 +3059,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   if (c->d_xw) (void)hipFree(c->d_xw);
   if (c->d_gsh) (void)hipFree(c->d_gsh);
   if (c->d_swt) (void)hipFree(c->d_swt);
+  if (c->d_tacc) (void)hipFree(c->d_tacc);
   if (c->ws) (void)hipFree(c->ws);
   if (c->h_img) (void)hipFree(c->h_img);
   if (c->h_out) (void)hipFree(c->h_out);
@@ -2896,9 +3075,7 @@ int ldb_ctx_destroy(ldb_ctx* c) {
   for (const ldb_ctx::EvTriple& t : c->evs) {
     (void)hipEventDestroy(t.e0);
     (void)hipEventDestroy(t.eu);
-    (void)hipEventDestroy(t.ef);
     (void)hipEventDestroy(t.es);
-    (void)hipEventDestroy(t.e1);
     (void)hipEventDestroy(t.e2);
   }
   delete c;
@@ -3205,7 +3382,8 @@ int ldb_kernel_timing(ldb_ctx* c, int enable, double* avg_main_ms, double* avg_t
   if (n) *n = c->t_n;
   if (enable >= 0) {
     c->timing = enable != 0;
-    c->t_run = c->t_fill = c->t_main = c->t_total = c->t_sweep = 0;
+    c->t_run = c->t_sweep = c->t_main = c->t_total = 0;
+    for (double& x : c->t_ph) x = 0;
     c->t_n = 0;
   }
   return LDB_OK;
@@ -3221,22 +3399,22 @@ int ldb_kernel_timing_split(ldb_ctx* c, int enable, double* avg_run_ms, double* 
   return ldb_kernel_timing(c, enable, avg_main_ms, avg_total_ms, n);
 }
 
-int ldb_kernel_timing_fill(ldb_ctx* c, double* avg_fill_ms) {
-  if (!c || !avg_fill_ms) return LDB_ERR_ARG;
+int ldb_kernel_timing_tail(ldb_ctx* c, double* avg_phase_ms, int n_phases) {
+  if (!c || !avg_phase_ms || n_phases < 0) return LDB_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
   const int rc = resolve_timing(c);
   if (rc != LDB_OK) return rc;
-  *avg_fill_ms = c->t_n ? c->t_fill / c->t_n : 0.0;
+  for (int k = 0; k < n_phases; ++k) avg_phase_ms[k] = k < kNPh && c->t_n ? c->t_ph[k] / c->t_n : 0.0;
   return LDB_OK;
 }
 
 int ldb_kernel_timing_sweep(ldb_ctx* c, double* avg_sweep_ms, double* avg_fin_ms) {
   if (!c || !avg_sweep_ms || !avg_fin_ms) return LDB_ERR_ARG;
-  const int rc = resolve_timing(c);
-  if (rc != LDB_OK) return rc;
+  double ph[2];
+  const int rc = ldb_kernel_timing_tail(c, ph, 2);
   *avg_sweep_ms = c->t_n ? c->t_sweep / c->t_n : 0.0;
-  *avg_fin_ms = c->t_n ? (c->t_fill - c->t_sweep) / c->t_n : 0.0;
-  return LDB_OK;
+  *avg_fin_ms = ph[1];
+  return rc;
 }
 
 }  // extern "C"

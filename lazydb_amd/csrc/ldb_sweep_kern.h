@@ -95,12 +95,15 @@ __device__ __forceinline__ T sw_wg_scan(T v, T ident, Op op, T* s_wtot) {
 // active run whose chain ended inside it. Fully parallel: the last active run before each run is a
 // prefix maximum over the runs, each thread checks a contiguous share; the runs' bases a prefix sum.
 // Both scans are wave-level lane shifts plus one pass over the 16 wave totals (four barriers in all).
-__device__ void sw_link(const Pipe& p, const SwGeo& g) {
-  __shared__ unsigned long long s_ev;
-  __shared__ uint64_t s_x[1024];     // X of each thread's last active run
-  __shared__ int32_t s_wmax[16];
-  __shared__ uint64_t s_wsum[16];
-  __shared__ uint64_t s_xe;
+// LDS (the caller's, kSwLinkLds bytes): X of each thread's last active run, the wave totals of both scans,
+// the first event and the tier's end
+constexpr uint32_t kSwLinkLds = 8 * 1024 + 8 * 16 + 4 * 16 + 8 + 8;
+__device__ __forceinline__ void sw_link(const Pipe& p, const SwGeo& g, uint8_t* lds) {
+  uint64_t* s_x = reinterpret_cast<uint64_t*>(lds);
+  uint64_t* s_wsum = s_x + 1024;
+  int32_t* s_wmax = reinterpret_cast<int32_t*>(s_wsum + 16);
+  unsigned long long& s_ev = *reinterpret_cast<unsigned long long*>(s_wmax + 16);
+  uint64_t& s_xe = *(reinterpret_cast<uint64_t*>(s_wmax + 16) + 1);
   constexpr int kPer = (kSwMaxRuns + 1023) / 1024;   // runs per thread (blockDim.x = 1024)
   static_assert(64 * kSwWaves == 1024, "sw_link: one 1024-thread workgroup");
   SwCtl* c = p.swctl;
@@ -177,7 +180,6 @@ __device__ void sw_link(const Pipe& p, const SwGeo& g) {
     c->ke = g.ks + tot;
     c->ncov = ncov;
     c->nrun = nrun;
-    c->done0 = 0;
     c->state = 1;
   }
 }
@@ -196,22 +198,27 @@ __device__ uint64_t g_swstamps[16];
 #define SW_ADD(k, a, b)
 #endif
 
-__global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
-  __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
-  __shared__ __attribute__((aligned(16))) uint32_t sh[9 * 1024];   // shift by 64, 128, ..., 2048, then 16, 32, 48 bytes
-  __shared__ uint32_t hits[kSwWaves][kSwList];
-  __shared__ int s_last;
-  if (scan_done(p)) return;   // the run prefix ended the scan
+// k_sweep phase S, item vb of vg (rounds 1-5 the k_sweep kernel): waves run vb kSwWaves + wave of the
+// geometry of vg workgroups. LDS (k_sweep's): lp2 the LP2 block, sh shift by 64, 128, ..., 2048, then 16, 32,
+// 48 bytes (9 x 1024 words), hits each wave's candidate list (kSwWaves x kSwList words); built once per
+// workgroup (tabs).
+constexpr uint32_t kSwLds = kLp2Bytes + 9 * 1024 * 4 + kSwWaves * kSwList * 4;
+__device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t vg, uint8_t* lp2, uint32_t* sh,
+                                           uint32_t* hits, int& tabs) {
 #ifdef LDB_STAMPS
   uint64_t swacc[9] = {};
 #endif
   SW_T(ts0);
-  const SwGeo g = sw_geo(p, (uint64_t)gridDim.x * kSwWaves);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t r = (uint64_t)blockIdx.x * kSwWaves + wave;
+  const SwGeo g = sw_geo(p, (uint64_t)vg * kSwWaves);
+  // the lane numbers through an opaque per-item copy: what derives from them is computed in the item, not
+  // hoisted over k_sweep's claim loop and held (spilled) across it
+  uint32_t tid = threadIdx.x;
+  asm volatile("" : "+v"(tid) : "s"(vb));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t r = (uint64_t)vb * kSwWaves + wave;
   const bool mine = g.active && r < g.nrun;
-  if (__syncthreads_or(mine ? 1 : 0)) {
+  if (__syncthreads_or(mine ? 1 : 0) && tabs != kLdsSweep) {
     lp2_build(lp2, p.gtab);
     for (uint32_t i = threadIdx.x; i < 6 * 1024; i += blockDim.x) {
       const uint32_t a = p.swt[i], b = i < 3 * 1024 ? p.swt[kSwRowOff + i] : 0u;
@@ -219,6 +226,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
       if (i < 3 * 1024) sh[6 * 1024 + i] = b;
     }
     __syncthreads();
+    tabs = kLdsSweep;
   }
   SW_T(ts1);
   SW_ADD(0, ts0, ts1);
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
     const uint64_t B = A + g.rl < p.len ? A + g.rl : p.len;
     const uint64_t lo = r == 0 ? g.xs : A;
     const uint32_t lb = ((uint32_t)lane & 31u) * 4u;
-    uint32_t* hl = hits[wave];
+    uint32_t* hl = hits + wave * kSwList;
     // the run's slab: an equal share of the scratch tuples
     const uint64_t cap64 = p.scratch_bytes / 16 / g.nrun;
     const uint32_t cap = (uint32_t)(cap64 < 0x7FFFFFFFull ? cap64 : 0x7FFFFFFFull);
@@ -600,21 +608,13 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p) {
   if (lane == 0)
     for (int k = 0; k < 9; ++k) atomicAdd((unsigned long long*)&g_swstamps[k], (unsigned long long)swacc[k]);
 #endif
-  // the last workgroup resolves the links
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = atomicAdd((unsigned long long*)&p.swctl->done0, 1ull) == (unsigned long long)gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+}
+
+// after the last phase-S item, in the workgroup that completed it (every item released, then acquired by
+// k_sweep): the links between runs, with the geometry every item used
+__device__ __forceinline__ void sweep_last(const Pipe& p, uint32_t vg, uint8_t* lds) {
   SW_T(tk0);
-  sw_link(p, g);
+  sw_link(p, sw_geo(p, (uint64_t)vg * kSwWaves), lds);
   SW_T(tk1);
 #ifdef LDB_STAMPS
   if (threadIdx.x == 0) atomicAdd((unsigned long long*)&g_swstamps[7], (unsigned long long)(tk1 - tk0));
@@ -840,37 +840,35 @@ __device__ __forceinline__ void sw_finish(const Pipe& p) {
       p.dyn[3] = kUniDone;
     }
     c->fail = ~0ull;
-    c->done1 = 0;
     c->state = 0;
   }
 }
 
-#ifndef LDB_FIN_WPE
-#define LDB_FIN_WPE 4   // workgroups per CU (= waves per SIMD): 5 measured slower at 8 GiB (fin 202-206 against 194-195 us)
-#endif
-__global__ __launch_bounds__(64 * kSwFinWaves) __attribute__((amdgpu_waves_per_eu(LDB_FIN_WPE))) void k_sweep_fin(Pipe p) {
-  __shared__ __attribute__((aligned(16))) uint32_t st[2 * 1024 + 16 * 256 + 1024];
-  __shared__ int s_last;
-  if (scan_done(p)) return;
+// k_sweep phase F, item vb of vg (rounds 1-5 the k_sweep_fin kernel): wave w takes runs vb kSwWaves + w, stepping
+// by vg kSwWaves, one lane per chain entry. st: the shift by 256 and 4096 bytes, the slicing-by-16 tables and
+// the shift by 64 (kSwFinLds bytes of k_sweep's LDS), copied once per workgroup (tabs)
+constexpr uint32_t kSwFinLds = (2 * 1024 + 16 * 256 + 1024) * 4;
+__device__ __forceinline__ void fin_item(const Pipe& p, uint32_t vb, uint32_t vg, uint32_t* st, int& tabs) {
   SwCtl* c = p.swctl;
-  if (c->state != 1) return;
-  {   // shift by 256, 4096, slicing-by-16, shift by 64: every load in flight before the stores
-    static_assert(64 * kSwFinWaves == 256, "k_sweep_fin: 256 threads copy 7168 words");
-    uint32_t v[28];
+  if (tabs != kLdsFin) {   // every load in flight before the stores
+    static_assert(kSwFinLds / 4 % (64 * kSwWaves) == 0, "fin_item: the workgroup copies whole rounds of words");
+    constexpr int kR = kSwFinLds / 4 / (64 * kSwWaves);
+    uint32_t v[kR];
 #pragma unroll
-    for (int k = 0; k < 28; ++k) {
-      const uint32_t i = threadIdx.x + 256u * k;
+    for (int k = 0; k < kR; ++k) {
+      const uint32_t i = threadIdx.x + 64u * kSwWaves * k;
       v[k] = p.swt[i < 1024 ? 2 * 1024 + i : (i < 2048 ? 6 * 1024 + i - 1024 : (i < 6144 ? kSwSl16Off + i - 2048 : i - 6144))];
     }
 #pragma unroll
-    for (int k = 0; k < 28; ++k) st[threadIdx.x + 256u * k] = v[k];
+    for (int k = 0; k < kR; ++k) st[threadIdx.x + 64u * kSwWaves * k] = v[k];
+    __syncthreads();
+    tabs = kLdsFin;
   }
-  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const uint64_t ks = c->ks, ncov = c->ncov, nrun = c->nrun, xe = c->xe;
   const uint64_t cap64 = nrun ? p.scratch_bytes / 16 / nrun : 0;
-  for (uint64_t r = (uint64_t)blockIdx.x * kSwFinWaves + wave; r < ncov; r += (uint64_t)gridDim.x * kSwFinWaves) {
+  for (uint64_t r = (uint64_t)vb * kSwWaves + wave; r < ncov; r += (uint64_t)vg * kSwWaves) {
     const SwRun q = p.swrun[r];
     const uint64_t tag = q.flags >> 8;
     if (tag == 0) continue;   // a covered run (sw_link): no entry of the chain starts in it
@@ -904,16 +902,4 @@ __global__ __launch_bounds__(64 * kSwFinWaves) __attribute__((amdgpu_waves_per_e
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = atomicAdd((unsigned long long*)&c->done1, 1ull) == (unsigned long long)gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last || threadIdx.x >= 64) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  sw_finish(p);
 }

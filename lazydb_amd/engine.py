@@ -311,11 +311,14 @@ class Engine:
                 "timing_split")
         return u.value, a.value, b.value, n.value
 
-    def timing_fill(self) -> float:
-        """avg k_uniform_fill ms over the timed launches (query; reset with timing/timing_split)."""
-        f = C.c_double()
-        N.check(N.lib().ldb_kernel_timing_fill(self.ctx, C.byref(f)), "timing_fill")
-        return f.value
+    def timing_tail(self):
+        """k_tail's per-phase averages (ms, device clock) over the timed scans: sweep stream, sweep checks,
+        regions, links, repair, cross-region CRCs, compaction (ldb_kernel_timing_tail)."""
+        a = (C.c_double * 7)()
+        if not hasattr(N.lib(), "ldb_kernel_timing_tail"):   # an A/B build of an older revision
+            return list(a)
+        N.check(N.lib().ldb_kernel_timing_tail(self.ctx, a, 7), "timing_tail")
+        return list(a)
 
     def timing_sweep(self):
         """(avg k_sweep ms, avg k_sweep_fin ms) over the timed launches: the sweep tier (query)."""

@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
     for sym in declared:
         assert hasattr(L, sym), sym
     assert set(N.EXPORTS) == declared
-    assert L.ldb_abi_version() == 3
+    assert L.ldb_abi_version() == 4
     assert N.status_str(-1) == "invalid crc"
 
 

@@ -11,6 +11,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
       --legs= --pmc 0 $ARGS > gpurun_out/${TAG}_${v}_$r.json 2> gpurun_out/${TAG}_${v}_$r.err || { tail -5 gpurun_out/${TAG}_${v}_$r.err; exit 1; }
     python3 -c "
 import json; d=json.loads(open('gpurun_out/${TAG}_${v}_$r.json').read().strip().splitlines()[-1]); ro=d['roofline']
-print('$v', 'round $r', d['value'], 'GiB/s', d['ms_per_step'], 'ms/step', 'median', d['median_step']['ms'], 'uni', ro['avg_k_uniform_ms'], 'main', ro['avg_k_scan_main_ms'], 'pipe', ro['avg_pipeline_ms'], 'frac', ro['frac'], 'verified', d['verified_vs_oracle'])"
+print('$v', 'round $r', d['value'], 'GiB/s', d['ms_per_step'], 'ms/step', 'median', d['median_step']['ms'], 'uni', ro['avg_k_uniform_ms'], 'sweep', ro.get('avg_k_sweep_ms'), 'region', ro.get('avg_k_region_ms', ro.get('avg_k_scan_main_ms')), 'pipe', ro['avg_pipeline_ms'], 'frac', ro['frac'], 'verified', d['verified_vs_oracle'])"
   done
 done

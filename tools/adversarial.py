@@ -95,12 +95,15 @@ def main() -> None:
         for _ in range(args.reps):
             eng.scan_dev_async(d, out=out, cap=cap, result=res)
         torch.cuda.synchronize()
+        ph = eng.timing_tail()
+        sw = eng.timing_sweep()[0]
         u, a, p, nl = eng.timing_split(0)
         print(json.dumps({"case": case, "bytes": int(ref.end_off), "entries": int(ref.n_entries),
                           "avg_entry_B": round(ref.end_off / max(1, ref.n_entries), 1), "verified": bool(ok),
                           "ms": round(ms, 3), "GiB_per_s": round(ref.end_off / (ms * 1e-3) / 2**30, 1),
                           "n_regions": int(r.n_regions), "n_fast": int(r.n_fast), "n_repairs": int(r.n_repairs),
-                          "n_broken_after_walk": int(r.n_broken), "k_uniform_ms": round(u, 4), "k_scan_main_ms": round(a, 4), "pipeline_ms": round(p, 4)}),
+                          "n_broken_after_walk": int(r.n_broken), "k_uniform_ms": round(u, 4), "k_sweep_ms": round(sw, 4), "k_region_ms": round(a, 4), "pipeline_ms": round(p, 4),
+                          "n_sweep": int(r.n_sweep), "tail_phases_ms": [round(x, 4) for x in ph]}),
               flush=True)
         del d, out, res
         torch.cuda.empty_cache()

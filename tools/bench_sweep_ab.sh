@@ -6,6 +6,6 @@ for sw in 1 0 1 0; do
 import json,sys
 d=json.loads(open('gpurun_out/bsw_$sw.json').read().strip().splitlines()[-1])
 print('sweep=$sw', 'cfg4 ms', d['ms_per_step'], 'median', d['median_step']['ms'], 'pipe', d['roofline']['avg_pipeline_ms'])
-for l in d['legs']: print('   leg', l['config'], 'ms', l['ms_per_step'], 'median', l['median_event_ms'], 'pipe', l['pipeline_ms'], 'sweep', l.get('k_sweep_ms'), l.get('k_sweep_fin_ms'), 'main', l['k_scan_main_ms'], 'n_sweep', l.get('sweep_entries'))
+for l in d['legs']: print('   leg', l['config'], 'ms', l['ms_per_step'], 'median', l['median_event_ms'], 'pipe', l['pipeline_ms'], 'sweep', l.get('k_sweep_ms'), 'region', l.get('k_region_ms'), l.get('tail_phases_ms'), 'n_sweep', l.get('sweep_entries'))
 "
 done

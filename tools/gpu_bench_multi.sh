@@ -12,7 +12,7 @@ for l in d.get("legs", []):
     if l["config"] == 5:
         print(" leg 5", l["GiB_per_s"], l["phases_ms"], l["roofline"]["frac"], l["verified_vs_oracle"], l["cpu_baseline"])
     else:
-        print(" leg", l["config"], l["GiB_per_s"], l["roofline_kernel"], l["roofline_frac"], "uni", l["k_uniform_ms"], "main", l["k_scan_main_ms"], "pipe", l["pipeline_ms"], "run", l["run_entries"], "/", l["entries"], "rerun", l["regions_rerun"], l["verified_vs_oracle"])
+        print(" leg", l["config"], l["GiB_per_s"], l["roofline_kernel"], l["roofline_frac"], "uni", l["k_uniform_ms"], "sweep", l.get("k_sweep_ms"), "region", l.get("k_region_ms"), l.get("tail_phases_ms"), "pipe", l["pipeline_ms"], "run", l["run_entries"], "/", l["entries"], "rerun", l["regions_rerun"], l["verified_vs_oracle"])
 PY
 LDB_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu --e2e 0 > gpurun_out/${TAG}_gloo2.json 2> gpurun_out/${TAG}_gloo2.err || { tail -20 gpurun_out/${TAG}_gloo2.err; exit 1; }
 python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_gloo2.json').read().strip().splitlines()[-1]);print('gloo2', d['value'], d['n_gpus'], d['verified_vs_oracle'], d.get('gather'))"

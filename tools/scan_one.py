@@ -31,10 +31,12 @@ def main():
         res, _ = eng.scan_dev(d, io_type=io, cap=n + 1024)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
+    ph = eng.timing_tail()
+    sw = eng.timing_sweep()[0]
     u, m, tot, k = eng.timing_split(0)
-    print(f"{wl}: status {res.status} entries {res.n_entries} end {res.end_off} run {res.n_run} fast {res.n_fast}/"
-          f"{res.n_regions} repairs {res.n_repairs} broken {res.n_broken} | {dt * 1e3:.3f} ms/scan wall, k_uniform "
-          f"{u:.4f} k_scan_main {m:.4f} pipeline {tot:.4f} ms")
+    print(f"{wl}: status {res.status} entries {res.n_entries} end {res.end_off} run {res.n_run} sweep {res.n_sweep} "
+          f"fast {res.n_fast}/{res.n_regions} repairs {res.n_repairs} broken {res.n_broken} | {dt * 1e3:.3f} ms/scan wall, "
+          f"k_uniform {u:.4f} k_sweep {sw:.4f} k_region {m:.4f} pipeline {tot:.4f} ms; phases " + " ".join(f"{x:.4f}" for x in ph))
     eng.close()
 
 
