@@ -191,10 +191,11 @@ int ldb_kernel_timing(ldb_ctx* ctx, int enable, double* avg_main_ms, double* avg
 int ldb_kernel_timing_split(ldb_ctx* ctx, int enable, double* avg_run_ms, double* avg_main_ms, double* avg_total_ms,
                             uint64_t* n);
 /* The phases after the run prefix over the same scans, from the device's constant clock (first item claimed
- * to the phase published, 0 where a phase did not run): k_sweep's [0] stream and links, [1] CRC checks and
- * tuples; k_region's [2] regions, [3] their links, [4] the repair, [5] the cross-region CRCs, [6] the
- * compaction. n_phases entries are written (7 are defined, the rest 0). Query only; the reset is
- * ldb_kernel_timing's / ldb_kernel_timing_split's. (ABI 4: replaces ldb_kernel_timing_fill.) */
+ * to the phase published, 0 where a phase did not run): [0] 0 (the sweep tier's stream is the k_sweep launch:
+ * ldb_kernel_timing_sweep), k_region's [1] the sweep tier's CRC checks and tuples, [2] the regions, [3] their
+ * links, [4] the repair, [5] the cross-region CRCs, [6] the compaction. n_phases entries are written (7 are
+ * defined, the rest 0). Query only; the reset is ldb_kernel_timing's / ldb_kernel_timing_split's. (ABI 4:
+ * replaces ldb_kernel_timing_fill.) */
 int ldb_kernel_timing_tail(ldb_ctx* ctx, double* avg_phase_ms, int n_phases);
 /* The sweep tier: avg_sweep_ms the k_sweep launch (events), avg_fin_ms its check phase (ldb_kernel_timing_tail's [1]). */
 int ldb_kernel_timing_sweep(ldb_ctx* ctx, double* avg_sweep_ms, double* avg_fin_ms);

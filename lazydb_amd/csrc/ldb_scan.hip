@@ -1413,7 +1413,8 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
       p.swctl->state = 0;
     }
   }
-  if (kMulti && LDB_FOLD_INIT && blockIdx.x == 0 && threadIdx.x < kTailCtlBytes / 4) p.tail[threadIdx.x] = 0u;
+  if (kMulti && LDB_FOLD_INIT && blockIdx.x == 0 && threadIdx.x < kTailCtlBytes / 4)
+    p.tail[threadIdx.x] = threadIdx.x >= kTailCtlBytes / 4 - 2 ? ~0u : 0u;   // (k_sweep's tail_init)
   // (workgroup 0 of a kMulti launch finds the runs first: its LP2 block afterwards, off that chain)
   if (!kMulti || blockIdx.x != 0) lp2_build(lp2, p.gtab);
 #ifdef LDB_STAMPS
@@ -2235,32 +2236,32 @@ __global__ __launch_bounds__(256) void k_read_reduce(const uint4* __restrict__ p
 // Everything after the run prefix, in two launches (rounds 1-5: seven, k_sweep, k_sweep_fin, k_scan_main,
 // k_link, k_repair, k_combine, k_compact; on a file the run prefix covers each returned at its first
 // instruction, ~10-14 us of every config-2/4 step, profiles/r06_tail_ab.txt):
-//   k_sweep   the sweep tier (ldb_sweep.h): S its stream (sweep_item), then the links between its runs
-//             (sweep_last); F its per-entry CRC checks and tuples (fin_item), then where it ends (sw_finish)
-//   k_region  the region pipeline from where the run prefix and the sweep tier stopped: M the regions
+//   k_sweep   the sweep tier's stream (phase S, sweep_item: one item per workgroup), then the links between
+//             its runs (sweep_last, the last workgroup to finish)
+//   k_region  F the sweep tier's per-entry CRC checks and tuples (fin_item), then where it ends (sw_finish);
+//             then the region pipeline from where the run prefix and the sweep tier stopped: M the regions
 //             (main_item), L their links (link_item), R the repair when a link broke (repair_item), C the
 //             cross-region CRCs and block counts (combine_item), K the compaction (compact_item)
 // The scan may end after any phase (the run prefix's uni_finish or sw_finish writes the result and the done
-// word): every workgroup then returns. Each phase is a number of items, the workgroups of the launch that
-// kernel used to have, claimed one at a time from a ticket counter by the workgroups that are running; the
-// workgroup that completes a phase's last item runs its follow-up (links, finish, serial repair) and
+// word): every workgroup then returns. In k_region each phase is a number of items, the workgroups of the
+// launch that kernel used to have, claimed one at a time from a ticket counter by the workgroups that are
+// running; the workgroup that completes a phase's last item runs its follow-up (finish, serial repair) and
 // publishes the phase, and every workgroup waits for that before its next phase. A workgroup only ever waits
-// after the phase's tickets are all taken, i.e. for items that running workgroups hold, so a launch cannot
-// deadlock however few of its workgroups are resident (another stream's kernels, a smaller chip).
-// Completion releases at agent scope and the wait acquires, as the kernel boundaries did (L2 write-back
-// across the XCDs). One launch for all seven phases was measured and rejected: the region code's register
-// pressure spilled every phase's values to scratch (224-272 B per lane, and a wave's first scratch access
-// costs at launch scale, tools/microbench/mb_scratch.hip): the sweep's stream 5-7 % and its checks 45 us
-// slower (profiles/r06_tail_fused_ab.txt). The sweep tier alone spills nothing on its usual path.
+// after the phase's tickets are all taken, i.e. for items that running workgroups hold, so the launch cannot
+// deadlock however few of its workgroups are resident (another stream's kernels, a smaller chip). Completion
+// releases at agent scope and the wait acquires, as the kernel boundaries did (L2 write-back across the XCDs).
+// Measured and rejected (profiles/r06_tail_fused_ab.txt): all seven phases in one launch (the region code's
+// register pressure spilled every phase's values to scratch, 224-272 B per lane, and a wave's first scratch
+// access costs tens of us at launch scale, tools/microbench/mb_scratch.hip: the sweep 5-7 % slower); S and F
+// in one launch (S's stream loop then held the protocol's values in SGPRs and spilled them into the loop: 3 %).
 constexpr int kPhS = 0, kPhF = 1, kPhM = 2, kPhL = 3, kPhR = 4, kPhC = 5, kPhK = 6, kNPh = 7;
 constexpr uint32_t kMainLds = kWPB * (sizeof(WaveLds) + kNB * kBuf);
 constexpr uint32_t kCompactWsum = (4 * (kBlkRegions + 1) + 15) & ~15u, kCompactPart = kCompactWsum + 4 * kWPB;
 constexpr uint32_t kCompactLds = kCompactPart + 8 * kWPB;
 constexpr uint32_t cmax(uint32_t a, uint32_t b) { return a > b ? a : b; }
-constexpr uint32_t kSweepLds = cmax(cmax(kSwLds, kSwLinkLds), kSwFinLds);
-constexpr uint32_t kRegionLds = cmax(kTabBytes + kMainLds, kCompactLds);
+constexpr uint32_t kRegionLds = cmax(cmax(kTabBytes + kMainLds, kCompactLds), kSwFinLds);
 static_assert(kTabBytes % 16 == 0 && kLp2Bytes % 256 == 0, "LDS carve alignment");
-static_assert(kSweepLds + 64 <= 160 * 1024 && kRegionLds + 64 <= 160 * 1024, "LDS per workgroup");
+static_assert(cmax(kSwLds, kSwLinkLds) + 64 <= 160 * 1024 && kRegionLds + 64 <= 160 * 1024, "LDS per workgroup");
 static_assert(kRepWaves == kWPB && kSwWaves == kWPB, "every phase runs kWPB waves");
 
 // item counts: the grids the kernels had (every phase has at least one item: its last one runs the
@@ -2312,11 +2313,10 @@ struct TailSync {
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       s_tail_fl = atomicAdd(&p.tail[8 + ph], 1u) == n - 1;
+      if (s_tail_fl) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-    __syncthreads();
-    const bool last = s_tail_fl != 0;
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    return last;
+    __syncthreads();   // (the workgroup's other threads are ordered after thread 0's acquire by the barrier)
+    return s_tail_fl != 0;
   }
   __device__ __forceinline__ void publish(const Pipe& p, int ph) const {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2332,10 +2332,13 @@ struct TailSync {
     }
   }
   __device__ __forceinline__ void wait(const Pipe& p, int ph) const {
-    if (threadIdx.x == 0)
+    // Thread 0 polls and acquires; the barrier orders the workgroup's other threads after it. (Every thread's
+    // own agent-scope acquire, 16 waves per workgroup each invalidating, cost ~30 us per phase boundary.)
+    if (threadIdx.x == 0) {
       while (__hip_atomic_load(&p.tail[16 + ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(4);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   // a phase whose items are cheap or rare: the plain claim loop
   template <class Body, class Last>
@@ -2372,38 +2375,29 @@ __device__ __forceinline__ bool tail_done(const Pipe& p) {   // after a wait: th
                                                    kUniDone)) != 0u;
 }
 
+// The sweep tier's stream (phase S): one item per workgroup, the workgroups of the launch (the round-5 kernel,
+// whose code it keeps: no phase protocol inside, so nothing is held across its stream loop -- the same body
+// behind k_region's tickets spilled SGPRs into that loop, 3 % slower), then the links by the last workgroup to
+// finish (a done counter, no waiting).
 template <bool kB>
-__global__ __launch_bounds__(64 * kWPB) void k_sweep(Pipe p0, const Pipe* __restrict__ pb, uint32_t ncu) {
-  __shared__ __attribute__((aligned(256))) uint8_t lds[kSweepLds];
-  (void)p0;   // (read through src)
-  LDB_PIPE_SRC(kB);
-  if (!src.get().sweep || scan_done(src.get())) return;   // (uni_finish ended the scan)
-  const TailSync ts;
+__global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p0, const Pipe* __restrict__ pb) {
+  __shared__ __attribute__((aligned(256))) uint8_t lds[cmax(kSwLds, kSwLinkLds)];
+  __shared__ int s_last;
+  LDB_PIPE_SELECT;
+  if (!p.sweep || scan_done(p)) return;   // (uni_finish ended the scan)
   int tabs = kLdsNone;
-  {
-    const Pipe& p = src.get();
-    const uint32_t nS = tail_items((p.len / kSwBatch + 2 + kSwWaves - 1) / kSwWaves, ncu);
-    ts.peeled(
-        p, kPhS, nS,
-        [&](uint32_t t) __attribute__((always_inline)) {
-          sweep_item(src.get(), t, nS, lds, reinterpret_cast<uint32_t*>(lds + kLp2Bytes),
-                     reinterpret_cast<uint32_t*>(lds + kLp2Bytes + 9 * 1024 * 4), tabs);
-        },
-        [&](uint32_t) __attribute__((always_inline)) {
-          sweep_last(src.get(), nS, lds);
-          tabs = kLdsNone;
-        });
+  sweep_item(p, blockIdx.x, gridDim.x, lds, reinterpret_cast<uint32_t*>(lds + kLp2Bytes),
+             reinterpret_cast<uint32_t*>(lds + kLp2Bytes + 9 * 1024 * 4), tabs);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_last = atomicAdd(&p.tail[8 + kPhS], 1u) == gridDim.x - 1;
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
-  {
-    const Pipe& p = src.get();
-    const uint64_t ncov = __hip_atomic_load(&p.swctl->ncov, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t nF = tail_items((ncov + kSwWaves - 1) / kSwWaves, ncu);
-    ts.peeled(
-        p, kPhF, nF, [&](uint32_t t) __attribute__((always_inline)) { fin_item(src.get(), t, nF, reinterpret_cast<uint32_t*>(lds), tabs); },
-        [&](uint32_t) __attribute__((always_inline)) {
-          if (threadIdx.x < 64) sw_finish(src.get());
-        });
-  }
+  __syncthreads();
+  if (!s_last) return;
+  sweep_last(p, gridDim.x, lds);
 }
 
 template <bool kB>
@@ -2417,6 +2411,21 @@ __global__ __launch_bounds__(64 * kWPB) void k_region(Pipe p0, const Pipe* __res
   uint32_t* const tab = reinterpret_cast<uint32_t*>(lds);
   uint8_t* const smem = lds + kTabBytes;
   auto none = [](uint32_t) __attribute__((always_inline)) {};
+  // ---- the sweep tier's checks (phase F), when k_sweep resolved its links (SwCtl::state, reset where the
+  // pipeline starts): one lane per chain entry, then where the tier ends (sw_finish)
+  if (src.get().sweep && src.get().swctl->state == 1) {
+    const Pipe& p = src.get();
+    const uint64_t ncov = p.swctl->ncov;
+    const uint32_t nF = tail_items((ncov + kSwWaves - 1) / kSwWaves, ncu);
+    ts.peeled(
+        p, kPhF, nF,
+        [&](uint32_t t) __attribute__((always_inline)) { fin_item(src.get(), t, nF, reinterpret_cast<uint32_t*>(lds), tabs); },
+        [&](uint32_t) __attribute__((always_inline)) {
+          if (threadIdx.x < 64) sw_finish(src.get());
+        });
+    if (tail_done(p)) return;
+    tabs = kLdsNone;
+  }
   {
     const Pipe& p = src.get();
     const uint32_t nM = tail_items((p.nreg + kWPB - 1) / kWPB, ncu);
@@ -2496,7 +2505,7 @@ struct ldb_ctx {
   hipStream_t cp[kMaxCp] = {};
   std::vector<hipEvent_t> chunk_ev;
   double t_run = 0, t_sweep = 0, t_main = 0, t_total = 0;
-  double t_ph[8] = {};   // k_sweep's and k_region's phases (device clock, d_tacc), summed over the timed scans
+  double t_ph[16] = {};   // k_sweep's and k_region's phases (device clock, d_tacc), summed over the timed scans
   double rt_khz = 100000.0;   // the device's constant clock (s_memrealtime)
   uint64_t t_n = 0;
   // batched scans (enqueue_scan_batch): page-locked staging of the per-file Pipes, reused once the
@@ -2542,11 +2551,11 @@ static int resolve_timing(ldb_ctx* c) {
   }
   c->ev_used = 0;
   // the tail kernels' phase accumulators (every timed scan has completed: its e2 fired)
-  uint64_t acc[8];
+  uint64_t acc[16];
   if (hipMemcpy(acc, c->d_tacc, sizeof(acc), hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemset(c->d_tacc, 0, sizeof(acc)) != hipSuccess)
     return LDB_ERR_HIP;
-  for (int k = 0; k < 8; ++k) c->t_ph[k] += (double)acc[k] / c->rt_khz;
+  for (int k = 0; k < 16; ++k) c->t_ph[k] += (double)acc[k] / c->rt_khz;
   return LDB_OK;
 }
 
@@ -2708,7 +2717,7 @@ int timing_begin(ldb_ctx* c, hipStream_t s, const ldb_ctx::EvTriple** out) {
 // the tail kernels' control words and the sweep tier's (every path but the device path's run prefix, which sets
 // them in k_uniform's workgroup 0)
 __device__ __forceinline__ void tail_init(const Pipe& p, uint32_t t) {
-  if (t < kTailCtlBytes / 4) p.tail[t] = 0u;
+  if (t < kTailCtlBytes / 4) p.tail[t] = t >= kTailCtlBytes / 4 - 2 ? ~0u : 0u;   // (the last u64: a min stamp)
   if (t == 0) {
     p.swctl->fail = ~0ull;
     p.swctl->state = 0;
@@ -2828,7 +2837,7 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   return fence_ws(c, s);
 #endif
   // everything after the run prefix: the sweep tier (k_sweep), then the region pipeline (k_region)
-  hipLaunchKernelGGL(k_sweep<false>, dim3(sweep_grid(c, len)), dim3(64 * kWPB), 0, s, p, nullptr, (uint32_t)c->n_cu);
+  hipLaunchKernelGGL(k_sweep<false>, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p, nullptr);
   if (ev) LDB_HIP(hipEventRecord(ev->es, s));
   hipLaunchKernelGGL(k_region<false>, dim3(region_grid(c, L.nreg)), dim3(64 * kWPB), 0, s, p, nullptr, (uint32_t)c->n_cu);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
@@ -2942,8 +2951,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-  hipLaunchKernelGGL(k_sweep<true>, dim3(std::min(tg, sweep_grid(c, max_len)), n), dim3(64 * kWPB), 0, s, p0, d_pipes,
-                     (uint32_t)c->n_cu);
+  hipLaunchKernelGGL(k_sweep<true>, dim3(sweep_grid(c, max_len), n), dim3(64 * kSwWaves), 0, s, p0, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->es, s));
   hipLaunchKernelGGL(k_region<true>, dim3(std::min(tg, region_grid(c, max_nreg)), n), dim3(64 * kWPB), 0, s, p0, d_pipes,
                      (uint32_t)c->n_cu);
@@ -3043,7 +3051,7 @@ int ldb_ctx_create(int device, ldb_ctx** out) {
     ldb_ctx_destroy(c);
     return LDB_ERR_HIP;
   }
-  if (hipMalloc(&c->d_tacc, 8 * 8) != hipSuccess || hipMemset(c->d_tacc, 0, 8 * 8) != hipSuccess) {
+  if (hipMalloc(&c->d_tacc, 8 * 16) != hipSuccess || hipMemset(c->d_tacc, 0, 8 * 16) != hipSuccess) {
     ldb_ctx_destroy(c);
     return LDB_ERR_NOMEM;
   }
@@ -3404,7 +3412,7 @@ int ldb_kernel_timing_tail(ldb_ctx* c, double* avg_phase_ms, int n_phases) {
   if (hipSetDevice(c->device) != hipSuccess) return LDB_ERR_HIP;
   const int rc = resolve_timing(c);
   if (rc != LDB_OK) return rc;
-  for (int k = 0; k < n_phases; ++k) avg_phase_ms[k] = k < kNPh && c->t_n ? c->t_ph[k] / c->t_n : 0.0;
+  for (int k = 0; k < n_phases; ++k) avg_phase_ms[k] = k < 16 && c->t_n ? c->t_ph[k] / c->t_n : 0.0;
   return LDB_OK;
 }
 

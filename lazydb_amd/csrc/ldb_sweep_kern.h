@@ -198,7 +198,7 @@ __device__ uint64_t g_swstamps[16];
 #define SW_ADD(k, a, b)
 #endif
 
-// k_sweep phase S, item vb of vg (rounds 1-5 the k_sweep kernel): waves run vb kSwWaves + wave of the
+// k_sweep's phase S, item vb of vg (one per workgroup): waves run vb kSwWaves + wave of the
 // geometry of vg workgroups. LDS (k_sweep's): lp2 the LP2 block, sh shift by 64, 128, ..., 2048, then 16, 32,
 // 48 bytes (9 x 1024 words), hits each wave's candidate list (kSwWaves x kSwList words); built once per
 // workgroup (tabs).
@@ -210,12 +210,8 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
 #endif
   SW_T(ts0);
   const SwGeo g = sw_geo(p, (uint64_t)vg * kSwWaves);
-  // the lane numbers through an opaque per-item copy: what derives from them is computed in the item, not
-  // hoisted over k_sweep's claim loop and held (spilled) across it
-  uint32_t tid = threadIdx.x;
-  asm volatile("" : "+v"(tid) : "s"(vb));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t r = (uint64_t)vb * kSwWaves + wave;
   const bool mine = g.active && r < g.nrun;
   if (__syncthreads_or(mine ? 1 : 0) && tabs != kLdsSweep) {
@@ -839,12 +835,11 @@ __device__ __forceinline__ void sw_finish(const Pipe& p) {
       p.dyn[7] = res.n_sweep;
       p.dyn[3] = kUniDone;
     }
-    c->fail = ~0ull;
-    c->state = 0;
+    c->fail = ~0ull;   // (state stays 1 until the next pipeline's init: every k_region workgroup reads it)
   }
 }
 
-// k_sweep phase F, item vb of vg (rounds 1-5 the k_sweep_fin kernel): wave w takes runs vb kSwWaves + w, stepping
+// k_region phase F, item vb of vg (rounds 1-5 the k_sweep_fin kernel): wave w takes runs vb kSwWaves + w, stepping
 // by vg kSwWaves, one lane per chain entry. st: the shift by 256 and 4096 bytes, the slicing-by-16 tables and
 // the shift by 64 (kSwFinLds bytes of k_sweep's LDS), copied once per workgroup (tabs)
 constexpr uint32_t kSwFinLds = (2 * 1024 + 16 * 256 + 1024) * 4;

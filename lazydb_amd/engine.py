@@ -311,13 +311,13 @@ class Engine:
                 "timing_split")
         return u.value, a.value, b.value, n.value
 
-    def timing_tail(self):
+    def timing_tail(self, n: int = 7):
         """k_tail's per-phase averages (ms, device clock) over the timed scans: sweep stream, sweep checks,
         regions, links, repair, cross-region CRCs, compaction (ldb_kernel_timing_tail)."""
-        a = (C.c_double * 7)()
+        a = (C.c_double * n)()
         if not hasattr(N.lib(), "ldb_kernel_timing_tail"):   # an A/B build of an older revision
             return list(a)
-        N.check(N.lib().ldb_kernel_timing_tail(self.ctx, a, 7), "timing_tail")
+        N.check(N.lib().ldb_kernel_timing_tail(self.ctx, a, n), "timing_tail")
         return list(a)
 
     def timing_sweep(self):
