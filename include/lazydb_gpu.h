@@ -153,7 +153,10 @@ int ldb_scan_file(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t f
  * ldb_entry). ldb_scan_file_count scans like ldb_scan_file and keeps the tuples in the context's device
  * staging; *h_result says how many there are (n_entries). ldb_scan_copy_out then copies
  * min(n_entries, cap) of them into h_out and sets *n_copied. Synchronous. The tuples stay valid until
- * the next scan call on the same context (copy_out returns LDB_ERR_ARG after one). */
+ * the next scan call on the same context (copy_out returns LDB_ERR_ARG after one). Device memory held by
+ * the context (grow-only, until ldb_ctx_destroy): the image (len bytes, 16-B rounded) plus exactly
+ * n_entries tuples of the largest count so far (the count runs with no tuple room, then the staged image
+ * is scanned again into an array of n_entries), plus the workspace ldb_workspace_bytes(len). */
 int ldb_scan_file_count(ldb_ctx* ctx, const uint8_t* h_image, uint64_t len, uint32_t fid, int io_type,
                         int tuple_kind, ldb_scan_result* h_result);
 int ldb_scan_copy_out(ldb_ctx* ctx, void* h_out, uint64_t cap, uint64_t* n_copied);

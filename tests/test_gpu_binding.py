@@ -20,6 +20,15 @@ from oracle import coracle
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _torch_first():
+    # torch's HIP runtime must initialise before the library's own (liblazydb_gpu links the image's ROCm;
+    # torch ships another): the batched case below allocates its device images through torch
+    import torch
+    torch.cuda.init()
+    yield
+
+
 def _images():
     imgs = []
     for s in range(3):
@@ -89,3 +98,85 @@ def test_pool_count_copy_more_threads_than_contexts():
     for c in ctxs:
         N.check(L.ldb_ctx_destroy(c), "ldb_ctx_destroy")
     assert not failures, failures[:5]
+
+
+def _count_copy(L, ctx, img, io, kind):
+    res = N.ScanResult()
+    N.check(L.ldb_scan_file_count(ctx, img.ctypes.data, img.size, 3, io, kind, C.byref(res)), "count")
+    n = int(res.n_entries)
+    dt = coracle.INDEX_TUPLE if kind == 0 else coracle.ENTRY_TUPLE
+    out = np.empty(max(n, 1), dtype=dt)
+    got = C.c_uint64()
+    N.check(L.ldb_scan_copy_out(ctx, out.ctypes.data, n, C.byref(got)), "copy_out")
+    assert got.value == n
+    return res, out[:n]
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_host_and_batched_paths_take_the_sweep_tier(kind):
+    """VERDICT r5 (missing #1): the sweep tier behind every entry point. A Zipf log (config 3's value sizes)
+    and a writer-realistic log, through the binding's count + copy (the host image staged in chunks, the run
+    prefix per chunk, then the tier) and through the batched ldb_scan_files_dev (index.go:103-108's replay
+    of several files at once): bit-exact with the oracle, and the tier carrying >= 95 % of the entries (a
+    silent hand-off to the region pipeline would pass parity alone)."""
+    import torch
+    L = N.lib()
+    ctx = C.c_void_p()
+    N.check(L.ldb_ctx_create(0, C.byref(ctx)), "ldb_ctx_create")
+    try:
+        z, nz, _ = coracle.gen_log(96 << 20, 7, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)
+        w, nw, _ = coracle.gen_writer_log(80 << 20, 8)
+        for img, n in ((z, nz), (w, nw)):
+            res, out = _count_copy(L, ctx, img, 0, kind)
+            ref, rt = coracle.scan(img, io_type=0, fid=3, tuple_kind=kind)
+            assert (res.status, res.end_off, res.n_entries) == (ref.status, ref.end_off, ref.n_entries)
+            assert out.tobytes() == rt.tobytes()
+            assert res.n_entries == n and res.n_sweep >= 0.95 * n, res.as_dict()
+        # batched: both images in one pipeline (grid.y = file)
+        d = [torch.from_numpy(x).to("cuda:0") for x in (z, w)]
+        tsz = 16 if kind == 0 else 48
+        caps = [nz + 16, nw + 16]
+        outs = [torch.empty(cap * tsz, dtype=torch.uint8, device="cuda:0") for cap in caps]
+        d_res = torch.zeros(2 * C.sizeof(N.ScanResult), dtype=torch.uint8, device="cuda:0")
+        imgs = (C.c_void_p * 2)(*[x.data_ptr() for x in d])
+        lens = (C.c_uint64 * 2)(z.size, w.size)
+        fids = (C.c_uint32 * 2)(5, 6)
+        douts = (C.c_void_p * 2)(*[o.data_ptr() for o in outs])
+        dcaps = (C.c_uint64 * 2)(*caps)
+        s = torch.cuda.current_stream()
+        N.check(L.ldb_scan_files_dev(ctx, 2, imgs, lens, fids, 0, kind, douts, dcaps, C.c_void_p(d_res.data_ptr()),
+                                     C.c_void_p(s.cuda_stream)), "ldb_scan_files_dev")
+        torch.cuda.synchronize()
+        hres = d_res.cpu().numpy().tobytes()
+        sz = C.sizeof(N.ScanResult)
+        for i, (img, n, fid) in enumerate(((z, nz, 5), (w, nw, 6))):
+            ref, rt = coracle.scan(img, io_type=0, fid=fid, tuple_kind=kind)
+            r = N.ScanResult.from_buffer_copy(hres[i * sz:(i + 1) * sz])
+            assert (r.status, r.end_off, r.n_entries) == (ref.status, ref.end_off, ref.n_entries), (i, r.as_dict())
+            assert outs[i][: n * tsz].cpu().numpy().tobytes() == rt.tobytes()
+            assert r.n_sweep >= 0.95 * n, (i, r.as_dict())
+    finally:
+        N.check(L.ldb_ctx_destroy(ctx), "ldb_ctx_destroy")
+
+
+def test_count_path_stages_exact_tuples():
+    """VERDICT r5 (weak #7): the count pass stages no tuples; the copy pass exactly n_entries. The device
+    memory a context holds after count + copy is the workspace, the image and n tuples (ENTRY kind: 48 B)."""
+    import torch
+    L = N.lib()
+    ctx = C.c_void_p()
+    N.check(L.ldb_ctx_create(0, C.byref(ctx)), "ldb_ctx_create")
+    try:
+        img, n, _ = coracle.gen_log(256 << 20, 11, ksize=16, vsize=20)   # 45-B entries: n = len / 45
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info()[0]
+        res, out = _count_copy(L, ctx, img, 0, 1)
+        ref, rt = coracle.scan(img, io_type=0, fid=3, tuple_kind=1)
+        assert res.n_entries == ref.n_entries == n and out.tobytes() == rt.tobytes()
+        held = free0 - torch.cuda.mem_get_info()[0]
+        ws = int(L.ldb_workspace_bytes(C.c_uint64(img.size)))
+        bound = ws + img.size + int(1.1 * n * 48) + (64 << 20)   # (64 MiB: allocator granules, events, tables)
+        assert held <= bound, (held, ws, img.size, n * 48)
+        assert held < ws + img.size + (len(img) // 10) * 48   # round 5's len/10 + 1 entries would not fit
+    finally:
+        N.check(L.ldb_ctx_destroy(ctx), "ldb_ctx_destroy")
