@@ -10,6 +10,7 @@
 #pragma once
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/lazydb_gpu.h"
 
@@ -23,6 +24,18 @@
 #endif
 
 namespace ldb {
+
+// The library's run-time switches (A/B and test conveniences): read from the environment only when
+// LDB_DEBUG=1 is set too, so a default process never depends on its environment (VERDICT r5 hygiene).
+inline const char* ldb_knob(const char* name) {
+  const char* d = getenv("LDB_DEBUG");
+  return d && atoi(d) != 0 ? getenv(name) : nullptr;
+}
+inline int ldb_knob_int(const char* name, int dflt) {
+  const char* v = ldb_knob(name);
+  return v ? atoi(v) : dflt;
+}
+
 
 constexpr int kMaxHeader = 38;            // logfile/log_entry.go:32
 constexpr uint32_t kPoly = 0xEDB88320u;   // CRC-32/IEEE, reflected

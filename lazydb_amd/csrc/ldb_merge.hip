@@ -1233,7 +1233,7 @@ int merge_scan(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file* file
   // scan-side hash became the most expensive part of the replay: in the loop 1.64 vs 0.97 ms, as a
   // separate pass over the keys 1.84 vs 0.97 ms, against +0.46 ms of liveness when k_insert hashes the
   // key it reads anyway (config 5: 4.58 ms off, 4.74 / 4.94 ms on; gpurun_out/mg1, mg2).
-  static const bool scan_hash = getenv("LDB_MERGE_SCAN_HASH") != nullptr && atoi(getenv("LDB_MERGE_SCAN_HASH")) != 0;
+  static const bool scan_hash = ldb::ldb_knob_int("LDB_MERGE_SCAN_HASH", 0) != 0;
   // every file's replay scan in ONE batched pipeline (ldb_scan.hip enqueue_scan_batch) on the
   // caller's context and stream; a set the batch does not take (a tiny image) goes file by file
   {
@@ -1269,7 +1269,7 @@ int merge_scan_lanes(ldb_ctx* ctx, MergeWs* m, uint32_t nf, const ldb_merge_file
                      ldb_scan_result* d_res, const std::vector<uint64_t>& sbase, hipStream_t s, bool scan_hash) {
   int rc = LDB_OK;
   if (!m->fork) {
-    const char* e = getenv("LDB_MERGE_SCAN_LANES");
+    const char* e = ldb::ldb_knob("LDB_MERGE_SCAN_LANES");
     const int want = std::min(std::max(e ? atoi(e) : 4, 1), MergeWs::kMaxAux + 1) - 1;
     MHIP(hipEventCreateWithFlags(&m->fork, hipEventDisableTiming));
     for (int i = 0; i < want; ++i) {
@@ -1412,7 +1412,7 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
 
   // ---- 2. liveness
   // >= (1 + 1/tdiv) slots per record: load <= 0.8 at the default when every key is distinct
-  static const uint64_t tdiv = getenv("LDB_MERGE_TDIV") ? (uint64_t)std::max(1, atoi(getenv("LDB_MERGE_TDIV"))) : 4;
+  static const uint64_t tdiv = (uint64_t)std::max(1, ldb::ldb_knob_int("LDB_MERGE_TDIV", 4));
   uint64_t tcap = 1024;
   while (tcap < n + n / tdiv) tcap <<= 1;
   if (!ext_live && tcap > (1ull << 31)) return h_result->status = LDB_ERR_ARG;   // slot ids are 31-bit (k_insert)
@@ -1445,9 +1445,9 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
     // LDB_INSERT_CAS=1: claim by CAS without the load first. Off: slower (config 5 k_insert 1.96 ms
     // against 1.72 ms, gpurun_out/ktm_b3) -- a failed CAS costs more than the load it replaces.
     // LDB_MERGE_TAGLESS=1 (tests): no hash tag, every probe that meets a taken slot compares the keys
-    const char* tl = getenv("LDB_MERGE_TAGLESS");
+    const char* tl = ldb::ldb_knob("LDB_MERGE_TAGLESS");
     const uint64_t tagmask = tl && atoi(tl) != 0 ? 0ull : ~kGMask;
-    static const bool cas_first = getenv("LDB_INSERT_CAS") != nullptr && atoi(getenv("LDB_INSERT_CAS")) != 0;
+    static const bool cas_first = ldb::ldb_knob_int("LDB_INSERT_CAS", 0) != 0;
     if (!ext_live) {
       if (cas_first) k_insert<true><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
       else k_insert<false><<<nbk, 256, 0, s>>>(n, d_fd, nf, d_tk, tcap - 1, d_slot, now, tagmask);
@@ -1472,7 +1472,7 @@ int merge_impl(ldb_ctx* ctx, int n_files, const ldb_merge_file* files, int io_ty
   const uint32_t gate = (live_ok ? 1u : 0u) | (h_segs ? 2u : 0u);
   if (n) {   // gated on the device by the capacities (emit_fits): no host round trip in between
     const uint32_t ngrp = (uint32_t)((n + 64 * kCopyWaves - 1) / (64 * kCopyWaves));
-    static const int unroll = getenv("LDB_COPY_UNROLL") ? atoi(getenv("LDB_COPY_UNROLL")) : 1;
+    static const int unroll = ldb::ldb_knob_int("LDB_COPY_UNROLL", 1);
     if (unroll >= 4)
       k_emit_copy<4><<<ngrp, 64 * kCopyWaves, 0, s>>>(n, d_fd, nf, d_P, d_C, d_segs, d_tail, pos_cap, stream_cap,
                                                       seg_cap, gate, d_stream, d_pos);

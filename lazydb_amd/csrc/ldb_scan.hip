@@ -2618,7 +2618,7 @@ int ensure_ws(ldb_ctx* c, uint64_t bytes) {
 
 // LDB_SWEEP=0 turns the sweep tier off (A/B: the region pipeline from the run prefix's end, rounds 1-4)
 bool sweep_enabled() {
-  static const bool on = getenv("LDB_SWEEP") == nullptr || atoi(getenv("LDB_SWEEP")) != 0;
+  static const bool on = ldb_knob_int("LDB_SWEEP", 1) != 0;
   return on;
 }
 
@@ -2933,7 +2933,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
   hipLaunchKernelGGL(k_batch_init, dim3(n), dim3(64), 0, s, d_pipes);
   // the run prefixes: the whole batch gets the workgroups one file's launch would (uniform_grid, 2
   // per CU at most), dealt evenly over its files (LDB_UNI_BATCH_BPC: workgroups per CU, A/B)
-  static const int bpc = getenv("LDB_UNI_BATCH_BPC") ? std::max(1, atoi(getenv("LDB_UNI_BATCH_BPC"))) : 1;
+  static const int bpc = std::max(1, ldb_knob_int("LDB_UNI_BATCH_BPC", 1));
   for (int i0 = 0; i0 < nf; i0 += kUniBatch) {
     UniBatch ub{};
     const int m = std::min(kUniBatch, nf - i0);
@@ -2962,7 +2962,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
 
 // LDB_SCAN_BATCH=0 turns the batched multi-file path off (A/B)
 bool batch_enabled() {
-  static const bool on = getenv("LDB_SCAN_BATCH") == nullptr || atoi(getenv("LDB_SCAN_BATCH")) != 0;
+  static const bool on = ldb_knob_int("LDB_SCAN_BATCH", 1) != 0;
   return on;
 }
 
@@ -3174,7 +3174,7 @@ static int scan_file_impl(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint
   // (hipHostMalloc, torch pin_memory, another context's registration) is staged like pageable memory.
   if (cap > UINT64_MAX / tsz) return LDB_ERR_ARG;
   void* mapped = nullptr;
-  if (len && getenv("LDB_DIRECT_IMAGE") != nullptr && c->registered(h_image, len) &&
+  if (len && ldb_knob("LDB_DIRECT_IMAGE") != nullptr && c->registered(h_image, len) &&
       (hipHostGetDevicePointer(&mapped, const_cast<uint8_t*>(h_image), 0) != hipSuccess || ((uintptr_t)mapped & 15))) {
     mapped = nullptr;   // pageable (the error is expected) or not 16-B aligned: the staged copy
     (void)hipGetLastError();
@@ -3184,7 +3184,7 @@ static int scan_file_impl(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint
   // range this context registered for all cap tuples qualifies: a shorter registration would let the
   // kernels write past the mapping
   void* out_mapped = nullptr;
-  if (cap && getenv("LDB_NO_DIRECT_OUT") == nullptr && c->registered(h_out, cap * tsz) &&
+  if (cap && ldb_knob("LDB_NO_DIRECT_OUT") == nullptr && c->registered(h_out, cap * tsz) &&
       hipHostGetDevicePointer(&out_mapped, h_out, 0) != hipSuccess) {
     out_mapped = nullptr;
     (void)hipGetLastError();
@@ -3209,7 +3209,7 @@ static int scan_file_impl(ldb_ctx* c, const uint8_t* h_image, uint64_t len, uint
   if (!c->h_res && hipMalloc(&c->h_res, sizeof(ldb_scan_result)) != hipSuccess) return LDB_ERR_NOMEM;
   hipStream_t s = c->h_stream;
   if (!c->n_cp) {
-    const char* e = getenv("LDB_H2D_STREAMS");
+    const char* e = ldb_knob("LDB_H2D_STREAMS");
     const int want = std::min(std::max(e ? atoi(e) : 2, 1), (int)ldb_ctx::kMaxCp);
     for (int i = 0; i < want; ++i) {
       if (hipStreamCreateWithFlags(&c->cp[i], hipStreamNonBlocking) != hipSuccess)

@@ -365,6 +365,12 @@ def _all_to_all_varlen(chunks, dist, device):
     recv_sz = torch.empty_like(sizes_d)
     dist.all_to_all_single(recv_sz, sizes_d)
     recv_sz = [int(x) for x in recv_sz.cpu()]
+    # the bytes sent and received over all ranks must balance: a transport or caller fault in the size
+    # exchange makes every rank raise here, instead of posting inconsistent splits
+    bal = torch.tensor([int(sizes.sum()) - sum(recv_sz)], dtype=torch.int64, device=dev)
+    dist.all_reduce(bal)
+    if int(bal.item()) != 0:
+        raise RuntimeError(f"all-to-all exchange: sent and received byte totals differ by {int(bal.item())}")
     send = torch.cat(chunks) if chunks else torch.zeros(0, dtype=torch.uint8, device=dev)
     recv = torch.empty(sum(recv_sz), dtype=torch.uint8, device=dev)
     dist.all_to_all_single(recv, send, output_split_sizes=recv_sz, input_split_sizes=[int(x) for x in sizes])

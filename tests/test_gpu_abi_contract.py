@@ -173,12 +173,14 @@ def test_scan_host_chunked_run_prefix(gpu_engine):
         eng.host_register(img)
         try:
             for direct in (False, True):
-                if direct:
+                if direct:   # (the library reads its switches only under LDB_DEBUG)
+                    os.environ["LDB_DEBUG"] = "1"
                     os.environ["LDB_DIRECT_IMAGE"] = "1"
                 try:
                     res, tup = eng.scan_host(img, fid=3)
                 finally:
                     os.environ.pop("LDB_DIRECT_IMAGE", None)
+                    os.environ.pop("LDB_DEBUG", None)
                 same(res, tup, *ref)
         finally:
             eng.host_unregister(img)

@@ -60,6 +60,7 @@ def test_merge_small_cases_tagless(eng, name, monkeypatch):
     """The same cases with the liveness table's hash tag off (LDB_MERGE_TAGLESS): every probe that
     meets a taken slot compares the keys, so the key-length recovery from the bytes before a
     slot's key (key_len_before) and the byte compare decide every duplicate."""
+    monkeypatch.setenv("LDB_DEBUG", "1")   # (the library reads its switches only under LDB_DEBUG)
     monkeypatch.setenv("LDB_MERGE_TAGLESS", "1")
     files, kw = MC.small_cases()[name]
     check_case(eng, files, kw)

@@ -15,6 +15,6 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
            "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex 'k_uniform|k_scan_main|k_compact|k_combine|k_link' -d $OUT/pmc$i -o pmc -f csv -- python3 bench.py $SHORT > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $OUT/pmc$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex 'k_uniform|k_sweep|k_region' -d $OUT/pmc$i -o pmc -f csv -- python3 bench.py $SHORT > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $OUT/pmc$i.log; exit 1; }
 done
 python3 tools/prof_summary.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
