@@ -889,7 +889,6 @@ __global__ __launch_bounds__(64 * kCopyWaves) void k_emit_copy(
   // kCopyUnroll pieces per lane per round: every full piece's load is issued before the round's first
   // store, so a lane keeps that many 16-B reads in flight (one at a time left the copy latency-bound)
   typedef unsigned int v4g __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(1))) const uint8_t* gsrc_t;
   typedef __attribute__((address_space(1))) v4g* gdst_t;
   for (uint32_t t0 = 0; t0 < total; t0 += 64 * kCopyUnroll) {
     const uint8_t* ss[kCopyUnroll];

@@ -52,7 +52,7 @@ constexpr int kNB = LDB_NB;    // LDS ring depth per wavefront
 constexpr int kG = kW / 1024 + 1;  // LDS-DMA instructions per region (5 x 1 KiB + the halo)
 
 // ---------------------------------------------------------------- wave policy (SIMT)
-constexpr int kStampSlots = 18;   // phase ids of region_process / region_chained / k_scan_main (tools/stamps.py)
+[[maybe_unused]] constexpr int kStampSlots = 18;   // phase ids of region_process / region_chained / k_scan_main (tools/stamps.py)
 struct GpuWave {
   int lane;
 #ifdef LDB_STAMPS
@@ -231,7 +231,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint
   return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
-constexpr int kNt = 2;   // buffer cache-policy bit: nt (streaming)
 template <int kAux = 0>
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t x, uint32_t y, uint32_t z,
                                         uint32_t w) {
@@ -347,7 +346,7 @@ struct UniRuns {
 constexpr uint32_t kUniDirectG = 8;
 constexpr uint32_t kUniHalfTab = (kUniDirectG - 1 > kUniLevels ? kUniDirectG - 1 : kUniLevels);   // its table index
 constexpr uint64_t kUniTabWords = kUniHalfTab * 1024;
-LDB_HD inline uint32_t uni_ntab(const UniGeo& g) { return g.G <= kUniDirectG ? g.G - 1 : g.lg; }
+LDB_HD uint32_t uni_ntab(const UniGeo& g) { return g.G <= kUniDirectG ? g.G - 1 : g.lg; }
 
 // The run prefix's CRC (round 3): 2-byte slicing on LANE-PRIVATE byte tables, so a wave's table reads
 // never bank-conflict. Row i of the 64 KiB block is 256 B: dwords [0, 32) hold T16[i] = the register
@@ -1411,6 +1410,7 @@ __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_l
     if (p.swctl && threadIdx.x == 0) {   // the sweep tier's control words (k_sweep follows)
       p.swctl->fail = ~0ull;
       p.swctl->state = 0;
+      p.swctl->stop = 0;
     }
   }
   if (kMulti && LDB_FOLD_INIT && blockIdx.x == 0 && threadIdx.x < kTailCtlBytes / 4)
@@ -2254,7 +2254,7 @@ __global__ __launch_bounds__(256) void k_read_reduce(const uint4* __restrict__ p
 // register pressure spilled every phase's values to scratch, 224-272 B per lane, and a wave's first scratch
 // access costs tens of us at launch scale, tools/microbench/mb_scratch.hip: the sweep 5-7 % slower); S and F
 // in one launch (S's stream loop then held the protocol's values in SGPRs and spilled them into the loop: 3 %).
-constexpr int kPhS = 0, kPhF = 1, kPhM = 2, kPhL = 3, kPhR = 4, kPhC = 5, kPhK = 6, kNPh = 7;
+constexpr int kPhS = 0, kPhF = 1, kPhM = 2, kPhL = 3, kPhR = 4, kPhC = 5, kPhK = 6;
 constexpr uint32_t kMainLds = kWPB * (sizeof(WaveLds) + kNB * kBuf);
 constexpr uint32_t kCompactWsum = (4 * (kBlkRegions + 1) + 15) & ~15u, kCompactPart = kCompactWsum + 4 * kWPB;
 constexpr uint32_t kCompactLds = kCompactPart + 8 * kWPB;
@@ -2721,6 +2721,7 @@ __device__ __forceinline__ void tail_init(const Pipe& p, uint32_t t) {
   if (t == 0) {
     p.swctl->fail = ~0ull;
     p.swctl->state = 0;
+    p.swctl->stop = 0;
   }
 }
 __global__ __launch_bounds__(64) void k_init(Pipe p, uint64_t dyn_val) {

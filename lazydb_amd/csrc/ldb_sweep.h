@@ -80,7 +80,8 @@ struct alignas(16) SwCtl {
   uint64_t xe, ke;    // where it ends (link resolution)
   uint64_t ncov;      // runs whose chain entries are the tier's
   uint64_t fail;      // smallest tier index of an entry whose CRC failed (k_sweep_fin), ~0
-  uint64_t spare;     // (round 5: a stop word later runs polled; every run now streams to its end)
+  uint64_t stop;      // set by run 0 when the tier surely ends inside it (declined, or its chain died within
+                      // its first decode block): no other run's registers serve an entry, they stop streaming
   uint64_t done0, done1;   // workgroups finished (k_sweep, k_sweep_fin): the last one resolves
   uint64_t state;     // 1 once k_sweep resolved the links; k_sweep_fin's last workgroup clears it
   uint64_t nrun;      // runs of this scan (each run's slab: scratch_bytes / 16 / nrun records)

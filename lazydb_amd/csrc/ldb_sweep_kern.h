@@ -241,6 +241,16 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
     const __amdgpu_buffer_rsrc_t irs = rsrc_of(p.img + A, (uint32_t)(ib < 0xFFFFFFFFull ? ib : 0xFFFFFFFFull));
     uint32_t npend = 0, ncand = 0;
     bool decl = false;
+    // The stop word (SwCtl::stop): run 0 sets it when the tier surely ends inside run 0 -- it declined, or the
+    // chain from x_s died within run 0's first decode block (a position no candidate holds: a header
+    // decode_lean_w rejects, as in a log of empty keys or negative expiries) -- and the other runs, whose
+    // registers then serve no entry of the tier, stop streaming. Polled once per pair of quarters, the value
+    // used a pair later (its load completes under the next quarters' loads: no wait of its own).
+    const __amdgpu_buffer_rsrc_t krs = rsrc_of(&p.swctl->stop, 8);
+    auto stop_tier = [&] {
+      if (lane == 0) __hip_atomic_store(&p.swctl->stop, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    bool probe = r == 0;
     // decode hl[0, nf) (one candidate per lane) and append the entries decode_lean accepts to the slab
     auto flush = [&](uint32_t nf) {
       const bool v = (uint32_t)lane < nf;
@@ -260,6 +270,22 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
       store16(srs, ok && idx < cap ? idx * 16u : kDrop, (uint32_t)pos, (uint32_t)(pos >> 32), e.k, e.vv);
       ncand += (uint32_t)__builtin_popcountll(bal);
       if (ncand > cap) decl = true;
+      if (probe) {   // run 0's first block holds every candidate up to its last position: walk the chain in it
+        probe = false;
+        const uint64_t last = sw_readlane64(v ? at : 0ull, (int)nf - 1);
+        const uint32_t sz = e.hs + e.k + e.vv;
+        uint64_t x = g.xs;
+        bool dies = false;
+        for (uint32_t s = 0; s < 64u && x <= last; ++s) {   // (x rises through distinct candidates)
+          const uint64_t mt = __ballot(ok && at == x);
+          if (!mt) {
+            dies = true;
+            break;
+          }
+          x += (uint32_t)__builtin_amdgcn_readlane((int)sz, __builtin_ctzll(mt));
+        }
+        if (dies) stop_tier();
+      }
     };
     // The run in quarters of 4 KiB: lane l holds the quarter's bytes [64 l, 64 l + 64) as 4 rows (a row
     // instruction reads 4 KiB in 64-B steps; the lane's bytes stay contiguous for its CRC), lane 63 also the
@@ -466,16 +492,26 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
     // Every run streams to its end, declined or not: a declined run (too many candidates) ends the tier
     // unless an entry from an earlier run covers it whole (sw_link), and that entry's CRC is then checked
     // from this run's window and group registers, so they are always complete. (Round 5 broke out of the
-    // loop at a decline and polled a stop word per pair of quarters; an entry spanning a declined run was
-    // then verified from stale registers.)
+    // loop at a decline and polled a stop word; an entry spanning a declined run was then verified from
+    // stale registers.) The one exception is the stop word above: set only when the tier ends inside run 0.
+    uint32_t sv = 0;   // the stop word, as loaded a pair of quarters ago
     for (uint32_t i = 0; i < nq; i += 2) {
+      if (r != 0 && sv) {   // (the run's registers are not needed: run 0 ends the tier)
+        decl = true;
+        break;
+      }
       load_q(Q, (i + 1) * 4096u);
       __builtin_amdgcn_sched_barrier(0);
       if (!proc_q(P, i * 4096u)) decl = true;
+      sv = __builtin_amdgcn_raw_buffer_load_b32(krs, 0, 0, kSc1);   // (before the next rows: done by their wait)
       load_q(P, (i + 2) * 4096u);
       __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < nq && !proc_q(Q, (i + 1) * 4096u)) decl = true;
       drain();
+      if (r == 0 && decl) {   // run 0 declined: the tier ends at x_s
+        stop_tier();
+        break;
+      }
     }
     if (nq & 3u) rg_tree((nq - 1u) * 4096u);   // a final batch of fewer than four quarters
     SW_T(tl1);

@@ -16,7 +16,7 @@ def short(name: str) -> str:
                  ("k_uniform<true", "k_uniform_chunk"), ("k_uniform<false, true>", "k_uniform_hash")):
         if k in name:
             return v
-    for k in ("k_uniform", "k_scan_main", "k_link", "k_repair", "k_combine", "k_final", "k_compact", "k_serial", "k_fallback",
+    for k in ("k_uniform", "k_sweep", "k_region", "k_init", "k_batch_init", "k_serial", "k_fallback",
               "k_locate", "k_insert", "k_live", "k_scan_reduce", "k_scan_tiles", "k_scan_write", "k_pack",
               "k_emit_copy"):
         if k in name:
@@ -53,7 +53,7 @@ def main(d: str) -> None:
                 extra = f"  -> {v * 1024 / 1e6:.1f} MB"
             print(f"  {cname:24s} {v:16.1f}{extra}")
             pmc.setdefault(k, {})[cname] = v
-    for k in ("k_uniform", "k_scan_main"):
+    for k in ("k_uniform", "k_sweep", "k_region"):
         if k in pmc and "FETCH_SIZE" in pmc[k]:
             pmc[k]["hbm_read_bytes_per_launch"] = pmc[k]["FETCH_SIZE"] * 2 * 1024
     with open(os.path.join(d, "pmc.json"), "w") as f:
