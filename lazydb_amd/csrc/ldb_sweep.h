@@ -50,7 +50,10 @@ constexpr uint32_t kSwG = 16;                  // windows per group register (4 
 constexpr int kSwWaves = 16;                   // waves per k_sweep workgroup (1 per CU: LDS)
 constexpr uint32_t kSwList = 512;              // candidate positions awaiting decode, per wave (LDS)
 constexpr uint32_t kSwTrust = 4;               // a speculated chain this long is kept when it ends in its run
+constexpr uint32_t kSwTagWalk = 14;            // the walk's last start tag (it takes that chain whatever it is)
+constexpr uint32_t kSwTagRelink = 15;          // a chain the links re-walked from the true position (sw_link)
 constexpr uint32_t kSwMaxRuns = 4096;
+constexpr uint64_t kSwMinBatches = 4;          // a run's least length in batches (64 KiB)
 constexpr uint32_t kSwDead = 1u, kSwDecl = 2u;
 constexpr uint64_t kSwPosMask = (1ull << 60) - 1;   // slab records: index tuple, walk tag in pos bits 60-63
 constexpr int kSwFinWaves = 4;
@@ -85,7 +88,8 @@ struct alignas(16) SwCtl {
   uint64_t done0, done1;   // workgroups finished (k_sweep, k_sweep_fin): the last one resolves
   uint64_t state;     // 1 once k_sweep resolved the links; k_sweep_fin's last workgroup clears it
   uint64_t nrun;      // runs of this scan (each run's slab: scratch_bytes / 16 / nrun records)
-  uint64_t pad[5];
+  uint64_t relinks;   // runs the links set aside or re-walked (sw_link's extra passes)
+  uint64_t pad[4];
 };
 static_assert(sizeof(SwCtl) == 128, "sweep control block");
 

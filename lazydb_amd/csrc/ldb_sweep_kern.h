@@ -36,7 +36,10 @@ __device__ __forceinline__ uint32_t sw_dpp(uint32_t x) {
 
 // ---------------------------------------------------------------- k_sweep
 // One wave per run: rows [A, B) of the image (B - A a multiple of the batch but for the last run).
-// Geometry, identical in every wave: a0 = x_s rounded down to a batch, the rest dealt in runs of rl.
+// Geometry, identical in every wave: a0 = x_s rounded down to a batch, the rest dealt in runs of rl, at least
+// kSwMinBatches batches: a run that one entry covers whole holds no chain start, and when a false start
+// inside that entry's value makes it look active the links need a pass of their own to set it aside
+// (sw_link); 64-KiB runs keep that to entries above 64 KiB, at no cost to the stream (small files only).
 struct SwGeo {
   uint64_t xs, ks, a0, rl, nrun;
   bool active;
@@ -50,7 +53,8 @@ __device__ __forceinline__ SwGeo sw_geo(const Pipe& p, uint64_t nwaves) {
   const uint64_t total = g.active ? p.len - g.a0 : 0;
   const uint64_t nb = (total + kSwBatch - 1) / kSwBatch;   // batches
   uint64_t nr = nwaves < kSwMaxRuns ? nwaves : kSwMaxRuns;
-  const uint64_t per = nr ? (nb + nr - 1) / nr : 0;        // batches per run
+  uint64_t per = nr ? (nb + nr - 1) / nr : 0;              // batches per run
+  per = per && per < kSwMinBatches ? kSwMinBatches : per;   // (round 6: runs no entry of <= 64 KiB covers whole)
   g.rl = per * kSwBatch;
   g.nrun = per ? (nb + per - 1) / per : 0;
   return g;
@@ -95,15 +99,83 @@ __device__ __forceinline__ T sw_wg_scan(T v, T ident, Op op, T* s_wtot) {
 // active run whose chain ended inside it. Fully parallel: the last active run before each run is a
 // prefix maximum over the runs, each thread checks a contiguous share; the runs' bases a prefix sum.
 // Both scans are wave-level lane shifts plus one pass over the 16 wave totals (four barriers in all).
+// Round 6 (found by the CPU emulation of the tier, tests/emu): when the first event is a run whose own walk
+// is not the chain's -- its walk took a false start inside an entry's value, as binary values offer, or
+// found none -- it is fixed and the links resolved again, up to kSwRelink times: a run the chain passes
+// over whole (the exit entering it lies at or past its end) is made inactive (no walk, no entries:
+// k_region's checks skip it); one the chain enters at T is re-walked from T over its slab (wave 0, tag
+// kSwTagRelink), which is the serial replay's own walk through the run's candidates.
 // LDS (the caller's, kSwLinkLds bytes): X of each thread's last active run, the wave totals of both scans,
-// the first event and the tier's end
-constexpr uint32_t kSwLinkLds = 8 * 1024 + 8 * 16 + 4 * 16 + 8 + 8;
+// the first event, the tier's end, the run to fix (and how, from where) and the re-walk's result
+constexpr uint32_t kSwLinkLds = 8 * 1024 + 8 * 16 + 4 * 16 + 8 * 8;
+constexpr int kSwRelink = 64;
+
+// the chain from T through run r's slab records (ncand of them, in file order) to the run's end B or the first
+// position no record holds; its records tagged kSwTagRelink. One wave (wave 0 of the links' workgroup).
+__device__ __forceinline__ void sw_rewalk(const Pipe& p, uint64_t r, uint64_t nrun, uint64_t T, uint64_t B, uint32_t ncand,
+                                          uint64_t* Xo, uint64_t* no, bool* deado) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t cap64 = p.scratch_bytes / 16 / nrun;   // (the run's slab, as sweep_item dealt them)
+  const __amdgpu_buffer_rsrc_t srs = rsrc_of(p.scratch + r * cap64, ncand * 16u);
+  uint4 rec = make_uint4(0, 0, 0, 0);
+  uint64_t lp = ~0ull;
+  uint32_t lsz = 0, bi = 0;
+  bool dirty = false;
+  auto load_blk = [&](uint32_t blk) {
+    const uint32_t i = blk * 64u + (uint32_t)lane;
+    const v4u32 q = __builtin_amdgcn_raw_buffer_load_b128(srs, i < ncand ? i * 16u : kDrop, 0, kSc1);
+    rec = make_uint4(q[0], q[1], q[2], q[3]);
+    const uint64_t pos = ((uint64_t)rec.y << 32) | rec.x;
+    lp = i < ncand ? (pos & 0xFFFFFFFFFFull) : ~0ull;
+    lsz = (uint32_t)((pos >> 40) & 0x3Fu) + rec.z + rec.w;
+  };
+  auto write_blk = [&](uint32_t blk) {
+    const uint32_t i = blk * 64u + (uint32_t)lane;
+    store16(srs, i < ncand ? i * 16u : kDrop, rec.x, rec.y, rec.z, rec.w);
+  };
+  load_blk(0);
+  uint64_t x = T, n = 0;
+  bool dead = false;
+  while (x < B) {
+    for (;;) {   // the block holding x (or the last)
+      const uint32_t nv = ncand - bi * 64u < 64u ? ncand - bi * 64u : 64u;
+      const uint64_t lastp = nv ? sw_readlane64(lp, (int)nv - 1) : 0;
+      if (nv == 0 || lastp >= x || (bi + 1) * 64u >= ncand) break;
+      if (dirty) write_blk(bi);
+      dirty = false;
+      load_blk(++bi);
+    }
+    const uint64_t mt = __ballot(lp == x);
+    if (!mt) {
+      dead = true;
+      break;
+    }
+    const int L = __builtin_ctzll(mt);
+    if (lane == L) {
+      rec.y = (rec.y & 0x0FFFFFFFu) | (kSwTagRelink << 28);
+      dirty = true;
+    }
+    ++n;
+    x += (uint32_t)__builtin_amdgcn_readlane((int)lsz, L);
+  }
+  if (dirty) write_blk(bi);
+  *Xo = x;
+  *no = n;
+  *deado = dead;
+}
 __device__ __forceinline__ void sw_link(const Pipe& p, const SwGeo& g, uint8_t* lds) {
   uint64_t* s_x = reinterpret_cast<uint64_t*>(lds);
   uint64_t* s_wsum = s_x + 1024;
   int32_t* s_wmax = reinterpret_cast<int32_t*>(s_wsum + 16);
   unsigned long long& s_ev = *reinterpret_cast<unsigned long long*>(s_wmax + 16);
-  uint64_t& s_xe = *(reinterpret_cast<uint64_t*>(s_wmax + 16) + 1);
+  uint64_t* s_w = reinterpret_cast<uint64_t*>(s_wmax + 16);
+  uint64_t& s_xe = s_w[1];
+  uint64_t& s_fix = s_w[2];   // the run to fix (~0: none), then how (1 inactive, 2 re-walk) and from where
+  uint64_t& s_mode = s_w[3];
+  uint64_t& s_T = s_w[4];
+  uint64_t& s_rx = s_w[5];    // the re-walk's exit, entries, whether it ended inside the run
+  uint64_t& s_rn = s_w[6];
+  uint64_t& s_rd = s_w[7];
   constexpr int kPer = (kSwMaxRuns + 1023) / 1024;   // runs per thread (blockDim.x = 1024)
   static_assert(64 * kSwWaves == 1024, "sw_link: one 1024-thread workgroup");
   SwCtl* c = p.swctl;
@@ -112,7 +184,7 @@ __device__ __forceinline__ void sw_link(const Pipe& p, const SwGeo& g, uint8_t* 
   const uint64_t r0 = (uint64_t)tid * kPer;
   // this thread's runs, every load in flight together
   uint64_t E[kPer], X[kPer], hi[kPer], n[kPer];
-  uint32_t fl[kPer];
+  uint32_t fl[kPer], nc[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const bool v = r0 + k < nrun;
@@ -122,43 +194,103 @@ __device__ __forceinline__ void sw_link(const Pipe& p, const SwGeo& g, uint8_t* 
     hi[k] = q->hi;
     n[k] = q->n;
     fl[k] = v ? q->flags : kSwDecl;
+    nc[k] = q->ncand;
   }
-  int32_t la = -1;   // the last active run of this thread's share, and its exit
-  uint64_t lx = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k)
-    if (!(fl[k] & kSwDecl) && E[k] != ~0ull) {
-      la = (int32_t)(r0 + k);
-      lx = X[k];
-    }
-  s_x[tid] = lx;
-  if (tid == 0) s_ev = ~0ull;
   auto mx = [](int32_t a, int32_t b) { return a > b ? a : b; };
-  const int32_t incl = sw_wg_scan<decltype(mx), int32_t>(la, -1, mx, s_wmax);   // (its barrier publishes s_x)
-  int32_t prev0 = __shfl_up(incl, 1);   // the last active run before this share
-  if ((tid & 63u) == 0) {
-    prev0 = -1;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) prev0 = mx(prev0, s_wmax[w]);
-  }
-  uint64_t T = prev0 >= 0 ? s_x[(uint32_t)prev0 / kPer] : g.xs;   // the chain's position entering the share
-  uint64_t ev = ~0ull, xe_mine = 0;
+  uint64_t evm = ~0ull;
+  int32_t incl = -1;
+  int pass = 0;
+  for (;; ++pass) {
+    int32_t la = -1;   // the last active run of this thread's share, and its exit
+    uint64_t lx = 0;
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    if (ev != ~0ull || r0 + k >= nrun) continue;
-    const uint64_t r = r0 + k;
-    if (!(fl[k] & kSwDecl) && E[k] != ~0ull) {
-      if (E[k] != T) { ev = 2 * r; xe_mine = T; continue; }
-      if (fl[k] & kSwDead) { ev = 2 * r + 1; xe_mine = X[k]; continue; }
-      T = X[k];
-    } else if (T < hi[k]) {   // not covered: the chain has an entry in this run that no walk took
-      ev = 2 * r;
-      xe_mine = T;
+    for (int k = 0; k < kPer; ++k)
+      if (!(fl[k] & kSwDecl) && E[k] != ~0ull) {
+        la = (int32_t)(r0 + k);
+        lx = X[k];
+      }
+    s_x[tid] = lx;
+    if (tid == 0) {
+      s_ev = ~0ull;
+      s_fix = ~0ull;
     }
+    incl = sw_wg_scan<decltype(mx), int32_t>(la, -1, mx, s_wmax);   // (its barrier publishes s_x)
+    int32_t prev0 = __shfl_up(incl, 1);   // the last active run before this share
+    if ((tid & 63u) == 0) {
+      prev0 = -1;
+      for (uint32_t w = 0; w < (tid >> 6); ++w) prev0 = mx(prev0, s_wmax[w]);
+    }
+    uint64_t T = prev0 >= 0 ? s_x[(uint32_t)prev0 / kPer] : g.xs;   // the chain's position entering the share
+    uint64_t ev = ~0ull, xe_mine = 0, fix_mine = 0, T_mine = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (ev != ~0ull || r0 + k >= nrun) continue;
+      const uint64_t r = r0 + k;
+      const bool relink = pass < kSwRelink && (fl[k] >> 8) != kSwTagRelink;
+      if (!(fl[k] & kSwDecl) && E[k] != ~0ull) {
+        if (E[k] != T) {
+          ev = 2 * r;
+          xe_mine = T;
+          // passed over whole: its walk is no part of the chain; entered at T: re-walked from there
+          fix_mine = relink ? (T >= hi[k] ? 1 : (nc[k] ? 2 : 0)) : 0;
+          T_mine = T;
+          continue;
+        }
+        if (fl[k] & kSwDead) { ev = 2 * r + 1; xe_mine = X[k]; continue; }
+        T = X[k];
+      } else if (T < hi[k]) {   // not covered: the chain has an entry in this run that no walk took
+        ev = 2 * r;
+        xe_mine = T;
+        fix_mine = relink && !(fl[k] & kSwDecl) && nc[k] ? 2 : 0;
+        T_mine = T;
+      }
+    }
+    if (ev != ~0ull) atomicMin(&s_ev, (unsigned long long)ev);
+    __syncthreads();
+    evm = s_ev;
+    if (evm != ~0ull && ev == evm) {
+      s_xe = xe_mine;
+      if (fix_mine) {
+        s_fix = evm / 2;
+        s_mode = fix_mine;
+        s_T = T_mine;
+      }
+    }
+    __syncthreads();
+    const uint64_t fix = s_fix;
+    if (fix == ~0ull) break;
+    const uint64_t mode = s_mode, Tf = s_T;
+    if (mode == 2 && tid < 64) {
+      uint64_t rx, rn;
+      bool rd;
+      sw_rewalk(p, fix, nrun, Tf, p.swrun[fix].hi, p.swrun[fix].ncand, &rx, &rn, &rd);
+      if (tid == 0) {
+        s_rx = rx;
+        s_rn = rn;
+        s_rd = rd ? 1u : 0u;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (r0 + k == fix) {
+        if (mode == 1) {   // no walk, no entries, no tag (k_region's checks skip a run with tag 0)
+          E[k] = ~0ull;
+          n[k] = 0;
+          fl[k] &= kSwDecl;
+        } else {           // the chain from T
+          E[k] = Tf;
+          X[k] = s_rx;
+          n[k] = s_rn;
+          fl[k] = (s_rd ? kSwDead : 0u) | (kSwTagRelink << 8);
+        }
+        p.swrun[fix].E = E[k];
+        p.swrun[fix].X = X[k];
+        p.swrun[fix].n = n[k];
+        p.swrun[fix].flags = fl[k];
+      }
+    __syncthreads();   // (every thread has read s_fix, s_ev and the re-walk before the next pass resets them)
   }
-  if (ev != ~0ull) atomicMin(&s_ev, (unsigned long long)ev);
-  __syncthreads();
-  const uint64_t evm = s_ev;
-  if (evm != ~0ull && ev == evm) s_xe = xe_mine;
   if (evm == ~0ull && tid == nt - 1) s_xe = incl >= 0 ? s_x[(uint32_t)incl / kPer] : g.xs;
   // bases: an exclusive prefix of the runs' entry counts (inactive runs count 0)
   const uint64_t ncov = evm == ~0ull ? nrun : ((evm & 1) ? evm / 2 + 1 : evm / 2);
@@ -180,6 +312,7 @@ __device__ __forceinline__ void sw_link(const Pipe& p, const SwGeo& g, uint8_t* 
     c->ke = g.ks + tot;
     c->ncov = ncov;
     c->nrun = nrun;
+    c->relinks = (uint64_t)pass;
     c->state = 1;
   }
 }
@@ -471,16 +604,16 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
     };
     auto drain = [&] {   // decode while 64 or more candidates wait
       SW_T(td0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the hit list's stores, before other lanes read them
+      LDB_WAVE_XCHG_LDS();   // the hit list's stores, before other lanes read them
       while (npend >= 64 && !decl) {
         flush(64);
         npend -= 64;
         for (uint32_t i = (uint32_t)lane; i < npend; i += 64) {   // (npend < kSwList - 64: one or few rounds)
           const uint32_t t = hl[64 + i];
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          LDB_WAIT_LGKM0();
           hl[i] = t;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        LDB_WAVE_XCHG_LDS();
       }
       SW_T(td1);
       SW_ADD(4, td0, td1);
@@ -517,7 +650,7 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
     SW_T(tl1);
     SW_ADD(5, tl0, tl1);
     if (!decl && npend) flush(npend);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slab's stores, before the walk reads them
+    LDB_WAVE_XCHG_VM();   // the slab's stores, before the walk reads them (other lanes' records)
     // ---- the walk: from the run's first entry, each entry's end is the next candidate
     uint64_t E = ~0ull, X = 0, cnt = 0;
     uint32_t fl = decl ? kSwDecl : 0u, tag = 1, si = 0;
@@ -559,12 +692,17 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
       // inside a value can claim a size past the run's end) or ends in it (the file's last run). Later
       // starts are tried, and the first weak chain is taken back (re-walked, so its records carry its tag
       // again) only if none of them holds; the links then check it like any other.
+      // Round 6 (found by the CPU emulation of the tier, tests/emu): of several weak chains the one taken back
+      // leaves the run if any does, and has the most entries among those (the first of equals). In a run
+      // that an entry's binary value fills up to a few short true entries, the value's false starts end
+      // inside or claim one huge entry, while the true chain leaves with more; in the file's last run no
+      // chain can leave (the decode bounds every entry by the file).
       uint64_t wE = ~0ull;
-      uint32_t wtag = 0;
+      uint32_t wtag = 0, wrank = 0;
       while (E != ~0ull) {
         if (x >= B) {
-          if (r == 0 || cnt >= kSwTrust || tag == 15) { X = x; break; }
-          if (wE == ~0ull) { wE = E; wtag = tag; }
+          if (r == 0 || cnt >= kSwTrust || tag == kSwTagWalk) { X = x; break; }
+          if (wE == ~0ull || 64u + (uint32_t)cnt > wrank) { wE = E; wtag = tag; wrank = 64u + (uint32_t)cnt; }
         } else {
           seek(x);
           const uint64_t mt = __ballot(lp == x);
@@ -581,8 +719,8 @@ __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t 
           // x is no candidate: the chain ends here (run 0's is the true chain from x_s; a speculated one
           // that held kSwTrust entries is kept and its end checked by the links), or the speculated first
           // entry was false and the next candidate is tried
-          if (r == 0 || cnt >= kSwTrust || tag == 15) { fl |= kSwDead; X = x; break; }
-          if (wE == ~0ull) { wE = E; wtag = tag; }   // weak too: a short chain that ends (the file's last run)
+          if (r == 0 || cnt >= kSwTrust || tag == kSwTagWalk) { fl |= kSwDead; X = x; break; }
+          if (wE == ~0ull || (uint32_t)cnt > wrank) { wE = E; wtag = tag; wrank = (uint32_t)cnt; }   // weak too: a short chain that ends (the file's last run)
         }
         ++si;
         ++tag;

@@ -243,10 +243,17 @@ static void emu_uniform(const Emu& emu, const uint8_t* img, uint64_t len, int io
   dyn[0] = k;
 }
 
+#ifdef LDB_EMU_SWEEP
+int emu_sweep_phase(Pipe& p, uint32_t vg, uint32_t vgf);   // tests/emu/sweep_emu.cpp
+#endif
+
 // run_len: regions per wavefront run (k_scan_main gives each wave a contiguous run); 0 = every
-// region speculative (the pre-chain pipeline). use_run: the run prefix (k_uniform) first.
-extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
-                           ldb_scan_result* res, uint32_t* stats, uint64_t run_len, int use_run) {
+// region speculative (the pre-chain pipeline). use_run: the run prefix (k_uniform) first. sweep_vg > 0
+// (libldb_emu_sweep.so): the sweep tier after the run prefix (k_sweep of sweep_vg workgroups, phase F of
+// at most sweep_vgf items), as the GPU pipeline orders it; the region pipeline continues where it ends.
+static int scan_impl(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                     ldb_scan_result* res, uint32_t* stats, uint64_t run_len, int use_run, uint32_t sweep_vg,
+                     uint32_t sweep_vgf) {
   Emu emu;
   const uint64_t nreg = std::max<uint64_t>(1, (len + kW - 1) / kW);
   const uint64_t nblk = (nreg + kBlkRegions - 1) / kBlkRegions;
@@ -271,6 +278,49 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
     return 0;
   }
   if (use_run) emu_uniform(emu, img, len, io, out, cap, dyn.data());
+  // the sweep tier's buffers, sized as the GPU workspace (WsLayout), and the image with a garbage tail (the
+  // GPU's staging buffer holds whatever lies past len; no result may depend on it)
+  std::vector<uint8_t> padded;
+  std::vector<uint32_t> swrw, swrg, swpl, swt;
+  std::vector<SwRun> swrun;
+  SwCtl swctl{};
+  (void)sweep_vg;
+  (void)sweep_vgf;
+#ifdef LDB_EMU_SWEEP
+  if (sweep_vg && first_region(p) < nreg) {
+    padded.resize(len + 65536);
+    std::copy(img, img + len, padded.begin());
+    uint64_t g = 0x9E3779B97F4A7C15ull ^ len;
+    for (size_t i = len; i < padded.size(); ++i) {
+      g = g * 6364136223846793005ull + 1442695040888963407ull;
+      padded[i] = (uint8_t)(g >> 56);
+    }
+    p.img = padded.data();
+    swrw.assign((len + kSwBatch) / kSwW + 1, 0u);
+    swrg.assign((len + kSwBatch) / (kSwW * kSwG) + 1, 0u);
+    swpl.assign((len + kSwBatch) / 64 + 1, 0u);
+    swrun.assign(kSwMaxRuns, SwRun{});
+    swt.assign(kSwTabWords, 0u);
+    build_swtab(swt.data());
+    p.swrw = swrw.data();
+    p.swrg = swrg.data();
+    p.swpl = swpl.data();
+    p.swrun = swrun.data();
+    p.swctl = &swctl;
+    p.swt = swt.data();
+    p.scratch_bytes = sizeof(ldb_index_tuple) * scratch.size();
+    p.tail = nullptr;
+    p.tacc = nullptr;
+    p.sweep = 1;
+    const int rc = emu_sweep_phase(p, sweep_vg, sweep_vgf);
+    if (rc < 0) return rc - 200;
+    if (stats) stats[3] = (uint32_t)swctl.relinks;   // the links' extra passes (sw_link)
+    if (rc == 1) {   // sw_finish wrote *p.result
+      if (stats) { stats[0] = 0; stats[1] = 0; stats[2] = 0; }
+      return 0;
+    }
+  }
+#endif
   const uint64_t rf = first_region(p), K = run_k(p), x0 = chain_x0(p);
   res->n_run = K;
   res->n_sweep = 0;
@@ -436,9 +486,23 @@ extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fi
   res->end_off = tp;
   res->n_repairs = ctr[2];
   res->n_regions = (uint32_t)(nreg - rf);
+  res->n_sweep = sweep_vg ? dyn[7] : 0;
   if (stats) { stats[0] = nfail; stats[1] = ctr[2]; stats[2] = n_fast; }
   return 0;
 }
+
+extern "C" int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                           ldb_scan_result* res, uint32_t* stats, uint64_t run_len, int use_run) {
+  return scan_impl(img, len, io, fid, out, cap, res, stats, run_len, use_run, 0, 0);
+}
+
+#ifdef LDB_EMU_SWEEP
+extern "C" int emu_scan_sweep(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                              ldb_scan_result* res, uint32_t* stats, uint64_t run_len, uint32_t sweep_vg,
+                              uint32_t sweep_vgf) {
+  return scan_impl(img, len, io, fid, out, cap, res, stats, run_len, 1, sweep_vg, sweep_vgf);
+}
+#endif
 
 extern "C" int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
                              ldb_scan_result* res, uint32_t* stats, uint64_t run_len) {

@@ -4,7 +4,7 @@ The tier takes a log from the run prefix's end when its entries vary in length (
 one streaming pass of CRC window registers and entry-start candidates, a per-run walk, link resolution,
 then per-entry CRC checks from the registers (logfile/log_entry.go:110-121 getEntryCrc, log_file.go:141-143
 the comparison). These cases put corrupt bytes where that algebra changes form: the first and last byte of
-an entry's CRC span, both sides of a 256-B window edge, a 4-KiB group edge and a run edge (16 KiB at 64 MiB),
+an entry's CRC span, both sides of a 256-B window edge, a 4-KiB group edge and a run edge (64 KiB, the least run length),
 and check the tier's share on clean logs so a silent hand-off to the region pipeline cannot pass unseen.
 """
 import random
@@ -77,7 +77,7 @@ def test_sweep_corruption(eng, mixed_log, where):
         i = int(rng.integers(n // 4, n - 2))
         at = int(pos[i]) + 4 if where == "first" else int(pos[i] + sz[i]) - 1
     else:
-        step = {"win_lo": 256, "win_hi": 256, "group": 4096, "run_lo": 16384, "run_hi": 16384}[where]
+        step = {"win_lo": 256, "win_hi": 256, "group": 4096, "run_lo": 65536, "run_hi": 65536}[where]
         for _ in range(1000):
             b = int(rng.integers(len(c) // 8, int(pos[-1]))) // step * step
             if _entry_over(pos, sz, b) >= 0:
@@ -130,8 +130,12 @@ def test_sweep_dense_candidates(eng):
 
 
 def test_sweep_writer_mix(eng):
+    """Binary values up to 64 KiB: runs a value fills but for a few short true entries, whose false starts
+    end inside or claim one huge entry (round 6, found by tests/emu: the weak-chain ranking, the links'
+    re-walk from the true position, 64-KiB least runs; the tier took 920 of 4,969 entries before them)."""
     w, nw, _ = coracle.gen_writer_log(32 << 20, 17, vmax=65536)
-    check(eng, w)
+    res = check(eng, w)
+    assert res.n_sweep >= 0.95 * nw, (res.n_sweep, nw)
 
 
 def _text_fill(rng, G, upto):
@@ -154,19 +158,19 @@ def _text_fill(rng, G, upto):
     return parts
 
 
-@pytest.mark.parametrize("vlen,d", [(40000, 8), (33000, 0), (64000, 300), (50000, -60)])
+@pytest.mark.parametrize("vlen,d", [(140000, 8), (133000, 0), (200000, 300), (150000, -60)])
 def test_sweep_entry_spanning_declined_runs(eng, vlen, d):
     """an entry whose 0x02-byte value covers whole runs that decline (every position a
     candidate). Its CRC is checked from those runs' window and group registers, so a declined run must
     still compute them; round 5 stopped streaming at the decline and verified the entry from stale ones.
-    The header sits in the run before (its value starts d bytes into a 16-KiB run of a 1 MiB file)."""
+    The header sits in the run before (its value starts d bytes into a 64-KiB run of a 1 MiB file)."""
     from tests.golden import make_golden as G
     rng = random.Random(vlen + d)
     size = 1 << 20
     # another log of the same size first, so the workspace's registers hold someone else's values
     w, _, _ = coracle.gen_writer_log(size, 3)
     check(eng, w, kinds=(0,), ios=(0,))
-    R = 8 * 16384
+    R = 2 * 65536
     big = G.ent(key=G.alpha(rng, 16), value=bytes([2]) * vlen)
     hs_k = len(big) - vlen
     h = R + d - hs_k
