@@ -56,9 +56,21 @@ struct WaveSync {
 };
 struct Fiber {
   ucontext_t uc;
-  std::unique_ptr<char[]> stack;
+  char* stack = nullptr;
   bool done = false;
 };
+// fiber stacks, kept across workgroups (a workgroup is 1,024 fibers; allocating their stacks per workgroup
+// dominated the sanitizer build's time)
+inline char* stack_at(uint32_t i, size_t bytes) {
+  static std::vector<std::unique_ptr<char[]>> pool;
+  static size_t pool_bytes = 0;
+  if (pool_bytes != bytes) {
+    pool.clear();
+    pool_bytes = bytes;
+  }
+  while (pool.size() <= i) pool.emplace_back(new char[bytes]);
+  return pool[i].get();
+}
 struct Block {
   uint32_t n = 0;
   Dim3 bidx{}, bdim{}, gdim{};
@@ -111,9 +123,9 @@ inline void run_block(Dim3 bidx, Dim3 gdim, uint32_t n, std::function<void()> bo
   blk() = &b;
   for (uint32_t i = 0; i < n; ++i) {
     Fiber& f = b.f[i];
-    f.stack.reset(new char[stack_bytes]);
+    f.stack = stack_at(i, stack_bytes);
     getcontext(&f.uc);
-    f.uc.uc_stack.ss_sp = f.stack.get();
+    f.uc.uc_stack.ss_sp = f.stack;
     f.uc.uc_stack.ss_size = stack_bytes;
     f.uc.uc_link = nullptr;
     makecontext(&f.uc, fiber_entry, 0);
@@ -125,10 +137,7 @@ inline void run_block(Dim3 bidx, Dim3 gdim, uint32_t n, std::function<void()> bo
       if (b.f[i].done) continue;
       b.cur = (int)i;
       swapcontext(&b.sched, &b.f[i].uc);
-      if (b.f[i].done) {
-        --left;
-        b.f[i].stack.reset();
-      }
+      if (b.f[i].done) --left;
     }
     if (left && b.progress == before) die("deadlock: lanes wait at a collective or barrier others never reach");
   }

@@ -18,7 +18,19 @@ int emu_scan_runs(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_in
                   ldb_scan_result* res, uint32_t* st, uint64_t run_len);
 int emu_scan_ex(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
                 ldb_scan_result* res, uint32_t* st, uint64_t run_len, int run_prefix);
+#ifdef LDB_EMU_SWEEP
+int emu_scan_sweep(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb_index_tuple* out, uint64_t cap,
+                   ldb_scan_result* res, uint32_t* st, uint64_t run_len, uint32_t vg, uint32_t vgf);
+#endif
 }
+
+// modes: 0-2 the region pipeline alone (every region speculative; runs of 3 and 64 regions), 3 the run prefix
+// first, 4 (the sweep build, san_sweep) the run prefix, then the sweep tier's kernel code under tests/emu/simt.h
+#ifdef LDB_EMU_SWEEP
+static const int kMode0 = 4, kModes = 5;   // (san_sweep: the sweep mode only; san_main runs the others)
+#else
+static const int kMode0 = 0, kModes = 4;
+#endif
 
 static int g_fail = 0, g_cases = 0;
 
@@ -31,13 +43,16 @@ static void check(const char* name, const std::vector<uint8_t>& img) {
     std::vector<ldb_index_tuple> rt(ref.n_entries + 1);
     ldbo_scan(p, len, io, 0, 0, rt.data(), ref.n_entries, &ref);
     const uint64_t cap = len / 5 + 8;
-    for (int mode = 0; mode < 4; ++mode) {
+    for (int mode = kMode0; mode < kModes; ++mode) {
       std::vector<ldb_index_tuple> out(cap);
       ldb_scan_result res{};
       uint32_t st[4] = {0, 0, 0, 0};
       int rc;
       if (mode < 3) rc = emu_scan_runs(p, len, io, 0, out.data(), cap, &res, st, mode == 0 ? 0 : (mode == 1 ? 3 : 64));
-      else rc = emu_scan_ex(p, len, io, 0, out.data(), cap, &res, st, 64, 1);
+      else if (mode == 3) rc = emu_scan_ex(p, len, io, 0, out.data(), cap, &res, st, 64, 1);
+#ifdef LDB_EMU_SWEEP
+      else rc = emu_scan_sweep(p, len, io, 0, out.data(), cap, &res, st, 64, 3, 4);
+#endif
       ++g_cases;
       bool ok = rc == 0 && res.status == ref.status && res.end_off == ref.end_off && res.n_entries == ref.n_entries;
       for (uint64_t i = 0; ok && i < ref.n_entries && i < cap; ++i)
@@ -69,8 +84,8 @@ int main(int argc, char** argv) {
   for (int i = 1; i < argc; ++i) {
     std::vector<uint8_t> img = read_file(argv[i]);
     check(argv[i], img);
-    // the fixture cut at every length mod 16 near its end (ragged tails, both IO rules)
-    for (uint64_t d = 1; d < 16 && d < img.size(); d += 5) {
+    // the fixture cut at every length mod 16 near its end (ragged tails, both IO rules; san_sweep: one cut)
+    for (uint64_t d = 1; d < (kMode0 ? 2u : 16u) && d < img.size(); d += 5) {
       std::vector<uint8_t> cut(img.begin(), img.end() - (long)d);
       check((std::string(argv[i]) + "-cut").c_str(), cut);
     }
