@@ -136,6 +136,35 @@ def case_prefix_keys():
         dict(active_fid=43, active_off=int(files[3].size), max_file_size=1 << 16, now=NOW)
 
 
+def case_long_and_hot_keys():
+    """Keys over 64 B that agree in their first 64 bytes (and more) and differ after them, keys of 63-65 B,
+    and one key rewritten ~2,000 times across the files, among distinct keys (round 6)."""
+    import random
+    rnd = random.Random(77)
+    longk = [b"L" * 64 + b"x" * j + b"%d" % i for i in range(6) for j in (0, 1, 40)]
+    edge = [bytes([65 + i]) * n for i in range(3) for n in (63, 64, 65)]
+    hot = b"hot-key"
+    files = []
+    for f in range(5):
+        recs = []
+        for r in range(900):
+            u = rnd.random()
+            if u < 0.45:
+                k = hot
+            elif u < 0.75:
+                k = rnd.choice(longk + edge)
+            else:
+                k = b"k-%d-%d" % (f, r)
+            if rnd.random() < 0.08:
+                recs.append(dict(stat=1, key=k))
+            else:
+                recs.append(dict(key=k, value=bytes(rnd.getrandbits(8) for _ in range(rnd.choice([0, 9, 40]))),
+                                 expired_at=rnd.choice([0, 0, 0, NOW - 1, NOW + 1])))
+        files.append(_log(recs))
+    return [(img, 10 + f, f != 4) for f, img in enumerate(files)], \
+        dict(active_fid=14, active_off=int(files[4].size), max_file_size=1 << 16, now=NOW)
+
+
 def case_crc_corrupt():
     return [(golden_img("mixed_64k"), 1, True), (golden_img("crc_corrupt"), 2, True),
             (np.zeros(64, np.uint8), 3, False)], dict(active_fid=3, active_off=0, max_file_size=1 << 20, now=NOW)
@@ -153,4 +182,5 @@ def small_cases():
         out[f"hot_keys{s}"] = case_hot_keys(s)
     out["tiny_entries"] = case_tiny_entries()
     out["prefix_keys"] = case_prefix_keys()
+    out["long_and_hot_keys"] = case_long_and_hot_keys()
     return out
