@@ -1297,6 +1297,18 @@ __device__ __forceinline__ void uni_run(const Pipe& p, const UniRun& q, uint64_t
   }
 }
 
+// The run prefix's LDS: the combine tables first, then the LP2 block at a byte offset below 64 KiB, so every
+// table read carries its base in the DS instruction's 16-bit offset (round 6: with the LP2 block first, the
+// combine tables sat above 64 KiB and the kernel kept ~20 table bases in VGPRs, at the 128-VGPR cap of a
+// 1024-thread workgroup: 7 VGPRs spilled to scratch). The LP2 base stays a multiple of 128 B (its lanes'
+// dwords map to 32 distinct banks).
+constexpr uint32_t kUniLp2Off = (4 * (uint32_t)kUniTabWords + 255u) & ~255u;
+static_assert(kUniLp2Off + 256 < 65536, "the LP2 block's base must fit a DS offset");
+#define LDB_UNI_LDS                                                                 \
+  __shared__ __attribute__((aligned(256))) uint8_t uni_lds[kUniLp2Off + kLp2Bytes]; \
+  uint32_t* const comb = reinterpret_cast<uint32_t*>(uni_lds);                     \
+  uint8_t* const lp2 = uni_lds + kUniLp2Off
+
 // kChunk: a_lo, a_hi: image bytes [0, a_hi) are in place; candidates not already taken by a launch
 // with a_hi = a_lo are this launch's (a_hi >= len: every remaining candidate). !kChunk: the whole image.
 // LDS: the 64 KiB LP2 block, the combine tables and the setup (~90 KiB): one workgroup of 16 waves per
@@ -1305,8 +1317,7 @@ __device__ __forceinline__ void uni_run(const Pipe& p, const UniRun& q, uint64_t
 // PCIe) and the merge's hashed scans take the first run only.
 template <bool kChunk, bool kHash>
 __global__ __launch_bounds__(64 * kUniWaves) void k_uniform(Pipe p, uint64_t a_lo, uint64_t a_hi) {
-  __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
-  __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];   // combine tables (shift by 2^i P bytes)
+  LDB_UNI_LDS;   // comb: the combine tables (shift by 2^i P bytes), lp2: the LP2 block
   __shared__ UniSetup su;
   __shared__ UniRuns ru;
   constexpr bool kMulti = !kChunk && !kHash;
@@ -1473,8 +1484,7 @@ __global__ __launch_bounds__(kFillThreads) void k_uniform_fill_batch(UniBatch b)
 template <bool kHash>
 __global__ __launch_bounds__(64 * kUniWaves) void k_uniform_batch(UniBatch b) {
   const Pipe p = b.p[blockIdx.y];
-  __shared__ __attribute__((aligned(256))) uint8_t lp2[kLp2Bytes];
-  __shared__ __attribute__((aligned(16))) uint32_t comb[kUniTabWords];
+  LDB_UNI_LDS;
   __shared__ UniSetup su;
   __shared__ UniRuns ru;
   lp2_build(lp2, p.gtab);
@@ -2277,8 +2287,10 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p0, const Pipe* __
   LDB_PIPE_SELECT;
   if (!p.sweep || scan_done(p)) return;   // (uni_finish ended the scan)
   int tabs = kLdsNone;
-  sweep_item(p, blockIdx.x, gridDim.x, lds, reinterpret_cast<uint32_t*>(lds + kLp2Bytes),
-             reinterpret_cast<uint32_t*>(lds + kLp2Bytes + 9 * 1024 * 4), tabs);
+  // the shift tables first, then the LP2 block below 64 KiB, then the hit lists (kSwLds: every table base
+  // in the DS instructions' 16-bit offsets, as k_uniform's LDB_UNI_LDS)
+  sweep_item(p, blockIdx.x, gridDim.x, lds + kSwShBytes, reinterpret_cast<uint32_t*>(lds),
+             reinterpret_cast<uint32_t*>(lds + kSwShBytes + kLp2Bytes), tabs);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -335,7 +335,9 @@ __device__ uint64_t g_swstamps[16];
 // geometry of vg workgroups. LDS (k_sweep's): lp2 the LP2 block, sh shift by 64, 128, ..., 2048, then 16, 32,
 // 48 bytes (9 x 1024 words), hits each wave's candidate list (kSwWaves x kSwList words); built once per
 // workgroup (tabs).
-constexpr uint32_t kSwLds = kLp2Bytes + 9 * 1024 * 4 + kSwWaves * kSwList * 4;
+constexpr uint32_t kSwShBytes = 9 * 1024 * 4;
+constexpr uint32_t kSwLds = kSwShBytes + kLp2Bytes + kSwWaves * kSwList * 4;
+static_assert(kSwShBytes + 256 < 65536 && kSwShBytes % 128 == 0, "k_sweep: the LP2 base in a DS offset, bank-aligned");
 __device__ __forceinline__ void sweep_item(const Pipe& p, uint32_t vb, uint32_t vg, uint8_t* lp2, uint32_t* sh,
                                            uint32_t* hits, int& tabs) {
 #ifdef LDB_STAMPS

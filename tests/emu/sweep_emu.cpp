@@ -40,8 +40,8 @@ int emu_sweep_phase(Pipe& p, uint32_t vg, uint32_t vgf) {
   for (uint32_t b = 0; b < vg; ++b)
     simt::run_block(simt::Dim3{b, 0, 0}, simt::Dim3{vg, 1, 1}, 64 * kSwWaves, [&] {
       int tabs = kLdsNone;
-      sweep_item(p, b, vg, lds, reinterpret_cast<uint32_t*>(lds + kLp2Bytes),
-                 reinterpret_cast<uint32_t*>(lds + kLp2Bytes + 9 * 1024 * 4), tabs);
+      sweep_item(p, b, vg, lds + kSwShBytes, reinterpret_cast<uint32_t*>(lds),
+                 reinterpret_cast<uint32_t*>(lds + kSwShBytes + kLp2Bytes), tabs);   // (k_sweep's layout)
     });
   simt::run_block(simt::Dim3{vg - 1, 0, 0}, simt::Dim3{vg, 1, 1}, 64 * kSwWaves, [&] { sweep_last(p, vg, lds); });
   if (c->state != 1) return -2;
