@@ -88,6 +88,9 @@ def gather_tuples(tuple_bytes: torch.Tensor, dst: int = 0, device=None):
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
+    # self-check: every rank sees its own count come back; a transport or caller fault makes
+    # every rank raise instead of posting mismatched sends and receives
+    agree(counts[rank] == tuple_bytes.numel(), "gather_tuples: byte counts", dev)
     gather_tuples.last_bytes = sum(c for r, c in enumerate(counts) if r != dst)
     if rank == dst:
         bufs = [tuple_bytes if r == dst else torch.empty(counts[r], dtype=torch.uint8, device=dev)
