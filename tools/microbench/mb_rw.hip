@@ -21,11 +21,14 @@
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// kMode 0: reads only; 1: reads, then the workgroup's slice of writes; 2: writes interleaved every kEvery rounds
+// kMode 0: reads only; 1: reads, then the workgroup's slice of writes; 2: writes interleaved every kEvery rounds;
+// 3: writes first, then reads; 4: odd workgroups write first, even ones last; 5: as 1 with plain stores;
+// 6: the writes alone
 template <int kMode, int kEvery>
 __global__ __launch_bounds__(1024) void k_rw(const uint4* __restrict__ in, uint64_t n16, uint4* out, uint64_t m16,
                                              uint32_t* sink) {
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool first = kMode == 3 || (kMode == 4 && (blockIdx.x & 1));
   const uint64_t nw = (uint64_t)gridDim.x * 16, gw = (uint64_t)blockIdx.x * 16 + wave;
   // reads: wave gw takes rounds of 8 KiB (8 loads of 1 KiB per wave), rounds interleaved over the waves
   const uint64_t rounds = n16 / 512;
@@ -34,7 +37,16 @@ __global__ __launch_bounds__(1024) void k_rw(const uint4* __restrict__ in, uint6
   const uint64_t w_lo = (uint64_t)blockIdx.x * per_wg, w_hi = w_lo + per_wg < m16 ? w_lo + per_wg : m16;
   uint64_t wc = w_lo + (uint64_t)wave * 64;   // this wave's next chunk
   uint32_t acc = 0, it = 0;
-  for (uint64_t r = gw; r < rounds; r += nw) {
+  if (first) {
+    for (; wc < w_hi; wc += 16 * 64) {
+      const uint64_t i = wc + lane;
+      if (i < w_hi) {
+        const u32x4 t = {(uint32_t)i, 1u, 2u, 3u};
+        __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(out + i));
+      }
+    }
+  }
+  for (uint64_t r = gw; kMode != 6 && r < rounds; r += nw) {
     u32x4 x[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + r * 512 + k * 64 + lane));
@@ -52,12 +64,13 @@ __global__ __launch_bounds__(1024) void k_rw(const uint4* __restrict__ in, uint6
       }
     }
   }
-  if (kMode >= 1) {
+  if (kMode >= 1 && !first) {
     for (; wc < w_hi; wc += 16 * 64) {
       const uint64_t i = wc + lane;
       if (i < w_hi) {
         const u32x4 t = {(uint32_t)i, 1u, 2u, 3u};
-        __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(out + i));
+        if (kMode == 5) *reinterpret_cast<u32x4*>(out + i) = t;   // plain store (write-back L2)
+        else __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(out + i));
       }
     }
   }
@@ -96,6 +109,15 @@ int main() {
   std::printf("reads only          %.4f ms (%.0f GB/s)\n", r0, nb / r0 / 1e6);
   const double r1 = run<1, 1>(in, n16, out, m16, sink, ncu);
   std::printf("reads then writes   %.4f ms\n", r1);
+  std::printf("reads then plain writes %.4f ms\n", run<5, 1>(in, n16, out, m16, sink, ncu));
+  const double w6 = run<6, 1>(in, n16, out, m16, sink, ncu);
+  std::printf("writes alone        %.4f ms (%.0f GB/s)\n", w6, mb / w6 / 1e6);
+  const double w6b = run<6, 1>(in, n16, out, m16, sink, 4 * ncu);
+  std::printf("writes alone, 4 workgroups per CU %.4f ms (%.0f GB/s)\n", w6b, mb / w6b / 1e6);
+  std::printf("writes then reads   %.4f ms\n", run<3, 1>(in, n16, out, m16, sink, ncu));
+  std::printf("half first, half last %.4f ms\n", run<4, 1>(in, n16, out, m16, sink, ncu));
+  std::printf("reads only (again) %.4f ms, reads then writes (again) %.4f ms\n", run<0, 1>(in, n16, out, m16, sink, ncu),
+              run<1, 1>(in, n16, out, m16, sink, ncu));
   std::printf("interleaved every 1 %.4f ms\n", run<2, 1>(in, n16, out, m16, sink, ncu));
   std::printf("interleaved every 2 %.4f ms\n", run<2, 2>(in, n16, out, m16, sink, ncu));
   std::printf("interleaved every 3 %.4f ms\n", run<2, 3>(in, n16, out, m16, sink, ncu));
