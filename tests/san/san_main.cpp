@@ -82,6 +82,7 @@ static std::vector<uint8_t> read_file(const char* path) {
 
 int main(int argc, char** argv) {
   for (int i = 1; i < argc; ++i) {
+    if (kMode0 && (i & 1) == 0) continue;   // (san_sweep: every other fixture, to keep the CPU suite short)
     std::vector<uint8_t> img = read_file(argv[i]);
     check(argv[i], img);
     // the fixture cut at every length mod 16 near its end (ragged tails, both IO rules; san_sweep: one cut)
