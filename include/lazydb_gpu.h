@@ -102,7 +102,7 @@ typedef struct ldb_scan_result {
   uint32_t n_repairs;    /* diagnostics: speculative-walk repairs performed (0 on well-formed logs) */
   uint32_t n_regions;    /* diagnostics: regions the region pipeline replayed (after the run prefix) */
   uint32_t n_fast;       /* diagnostics: of those, regions verified by the chained fast path (ldb_chain.h) */
-  uint32_t n_broken;     /* diagnostics: links still broken after k_repair's parallel walkers (the serial
+  uint32_t n_broken;     /* diagnostics: links still broken after the repair's parallel walkers (the serial
                             repair's sources; 0 on well-formed logs) */
   uint64_t n_run;        /* diagnostics: leading entries verified as one run of equal-sized entries
                             (k_uniform); they are tuples [0, n_run) */

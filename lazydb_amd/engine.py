@@ -305,15 +305,16 @@ class Engine:
         return a.value, b.value, n.value
 
     def timing_split(self, enable: int = -1):
-        """(avg k_uniform ms, avg k_scan_main ms, avg pipeline ms, launches) since the last reset."""
+        """(avg k_uniform ms, avg k_region ms, avg pipeline ms, launches) since the last reset."""
         u, a, b, n = C.c_double(), C.c_double(), C.c_double(), C.c_uint64()
         N.check(N.lib().ldb_kernel_timing_split(self.ctx, enable, C.byref(u), C.byref(a), C.byref(b), C.byref(n)),
                 "timing_split")
         return u.value, a.value, b.value, n.value
 
     def timing_tail(self, n: int = 7):
-        """k_tail's per-phase averages (ms, device clock) over the timed scans: sweep stream, sweep checks,
-        regions, links, repair, cross-region CRCs, compaction (ldb_kernel_timing_tail)."""
+        """Per-phase averages (ms, device clock) over the timed scans (ldb_kernel_timing_tail): [0] unused, [1] the
+        sweep checks (k_region phase F), [2..6] regions, links, repair, cross-region CRCs, compaction (phases
+        M, L, R, C, K)."""
         a = (C.c_double * n)()
         if not hasattr(N.lib(), "ldb_kernel_timing_tail"):   # an A/B build of an older revision
             return list(a)
@@ -321,7 +322,7 @@ class Engine:
         return list(a)
 
     def timing_sweep(self):
-        """(avg k_sweep ms, avg k_sweep_fin ms) over the timed launches: the sweep tier (query)."""
+        """(avg k_sweep ms, avg phase-F ms) over the timed launches: the sweep tier's stream and its checks (query)."""
         a, b = C.c_double(), C.c_double()
         N.check(N.lib().ldb_kernel_timing_sweep(self.ctx, C.byref(a), C.byref(b)), "timing_sweep")
         return a.value, b.value
