@@ -137,6 +137,25 @@ def test_emulated_sweep_golden_generators(lib, seed):
         check(lib, img)
 
 
+def test_emulated_sweep_txlog(lib):
+    """Tx.Commit writes (tx.go:156-206): snowflake TxIDs as 10-byte varints, TxStat 1, 1-16 entries per
+    transaction, some with a TTL -- headers of 15-21 bytes the lean decode takes; the tier carries them all."""
+    from tests.golden import make_golden as G
+    rng = random.Random(25)
+    parts, used, ms = [], 0, 1_700_000_000_000
+    while used < (2 << 20) - 8192:
+        ms += rng.randrange(1, 50)
+        tx = (ms << 22) | (rng.randrange(1023) << 12) | rng.randrange(4096)
+        for _ in range(rng.randrange(1, 17)):
+            e = G.ent(key=G.alpha(rng, rng.randrange(16, 65)), value=G.alpha(rng, rng.randrange(32, 513)), tx_id=tx,
+                      tx_stat=1, expired_at=rng.choice([0] * 9 + [1_700_000_000 + rng.randrange(10**6)]))
+            parts.append(e)
+            used += len(e)
+    img = np.frombuffer(G.image(parts, used + 4096), np.uint8).copy()
+    res = check(lib, img, vgs=(None, 2))
+    assert res.status == 2 and res.n_sweep == len(parts), (res.n_sweep, len(parts))
+
+
 def test_emulated_sweep_dense_candidates(lib):
     """Values of 0x02 bytes: every position passes the candidate filter, runs decline (run 0 too: the stop
     word), the region pipeline replays them."""
