@@ -280,13 +280,13 @@ static int scan_impl(const uint8_t* img, uint64_t len, int io, uint32_t fid, ldb
   if (use_run) emu_uniform(emu, img, len, io, out, cap, dyn.data());
   // the sweep tier's buffers, sized as the GPU workspace (WsLayout), and the image with a garbage tail (the
   // GPU's staging buffer holds whatever lies past len; no result may depend on it)
+  (void)sweep_vg;
+  (void)sweep_vgf;
+#ifdef LDB_EMU_SWEEP
   std::vector<uint8_t> padded;
   std::vector<uint32_t> swrw, swrg, swpl, swt;
   std::vector<SwRun> swrun;
   SwCtl swctl{};
-  (void)sweep_vg;
-  (void)sweep_vgf;
-#ifdef LDB_EMU_SWEEP
   if (sweep_vg && first_region(p) < nreg) {
     padded.resize(len + 65536);
     std::copy(img, img + len, padded.begin());
