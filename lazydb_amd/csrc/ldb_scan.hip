@@ -326,7 +326,14 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // Workgroup 0 publishes K = 0 or the entry size for the pipeline. Returns false when there is no run.
 // Every pipeline kernel serves one scan (its Pipe by value, p0) or, with kB, one file of a batched
 // scan: grid.y = file, its Pipe from the device array pb (enqueue_scan_batch).
-#define LDB_PIPE_SELECT const Pipe p = kB ? pb[blockIdx.y] : p0
+typedef __attribute__((address_space(4))) const Pipe* CPipe;
+// (a batched launch's pipe through the constant address space: the host wrote the array before the launch and
+// nothing changes it during one, so its fields can be re-read where a copy in global memory would spill SGPRs --
+// round 6: k_sweep<true> 38 SGPRs spilled into its stream loop)
+#define LDB_PIPE_SELECT                                                                              \
+  const Pipe& p = *(kB ? (const Pipe*)(CPipe)(pb + blockIdx.y)                                       \
+                       : (const Pipe*)(CPipe)__builtin_amdgcn_kernarg_segment_ptr());                \
+  (void)p0
 
 // Header probes of a one-run launch (chunked, batched or hashed scans; every workgroup probes, 64 probes
 // in round 0: the device path's several runs use uni_search below, one workgroup). The first header
@@ -1986,7 +1993,7 @@ __device__ void serial_walk(const Pipe& p) {
 }
 template <bool kB>
 __global__ __launch_bounds__(64) void k_serial(Pipe p0, int only_on_overflow, const Pipe* __restrict__ pb) {
-  LDB_PIPE_SELECT;
+  const Pipe p = kB ? pb[blockIdx.y] : p0;  // (a copy: a reference into the kernel arguments costs 28 VGPRs here)
   if (threadIdx.x != 0) return;
   if (only_on_overflow && !p.ctr[1]) return;
   serial_walk(p);
@@ -2175,7 +2182,6 @@ __device__ __forceinline__ uint32_t tail_items(uint64_t want, uint32_t ncu) {
 // argument itself, p0 at the kernarg segment's offset 0; a batched launch's device array), so no phase holds
 // another's Pipe fields in registers. Made in the kernel's own body (the kernarg segment pointer exists only
 // there), every use inlined.
-typedef __attribute__((address_space(4))) const Pipe* CPipe;
 template <bool kB>
 struct PipeSrc {
   const Pipe* pb;
