@@ -2785,7 +2785,12 @@ __global__ __launch_bounds__(64) void k_batch_init(const Pipe* __restrict__ pb) 
   tail_init(p, threadIdx.x);
 }
 
-int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s) {
+// split_sweep: one k_sweep launch per file (its pipe by value) instead of one over (vg, n) -- round 6: the 5 x
+// 512 MiB writer-mix batch 2.39 -> 2.19 ms (the sweep 1.87 -> ~1.67 ms), the Zipf batch unchanged, while the
+// merge's 16 mostly-uniform files lost 0.3 ms replay to 16 launches that return at once
+// (profiles/r06_sweep_split_ab.txt); the public batch API splits up to kSweepSplitMax files, the merge never
+constexpr int kSweepSplitMax = 8;
+int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s, bool split_sweep) {
   if (!c || nf < 0 || (io != LDB_IO_FILEIO && io != LDB_IO_MMAP) ||
       (kind != LDB_TUPLE_INDEX && kind != LDB_TUPLE_ENTRY))
     return LDB_ERR_ARG;
@@ -2861,7 +2866,13 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-  hipLaunchKernelGGL(k_sweep<true>, dim3(sweep_grid(c, max_len), n), dim3(64 * kSwWaves), 0, s, p0, d_pipes);
+  static const int split_knob = ldb_knob_int("LDB_SWEEP_SPLIT", -1);   // (A/B: 0 never, 1 always)
+  if (split_knob == 1 || (split_knob < 0 && split_sweep))
+    for (unsigned i = 0; i < n; ++i)
+      hipLaunchKernelGGL(k_sweep<false>, dim3(sweep_grid(c, c->h_pipes[i].len)), dim3(64 * kSwWaves), 0, s,
+                         c->h_pipes[i], nullptr);
+  else
+    hipLaunchKernelGGL(k_sweep<true>, dim3(sweep_grid(c, max_len), n), dim3(64 * kSwWaves), 0, s, p0, d_pipes);
   if (ev) LDB_HIP(hipEventRecord(ev->es, s));
   hipLaunchKernelGGL(k_region<true>, dim3(std::min(tg, region_grid(c, max_nreg)), n), dim3(64 * kWPB), 0, s, p0, d_pipes,
                      (uint32_t)c->n_cu);
@@ -2911,7 +2922,7 @@ __attribute__((visibility("hidden"))) int ldb_scan_files_dev_batched(ldb_ctx* c,
     if (!batch_eligible(d_images[i], lens[i])) return LDB_ERR_ARG;
     bf[i] = BatchFile{d_images[i], lens[i], fids[i], d_outs[i], caps[i], d_results + i, d_hash ? d_hash[i] : nullptr};
   }
-  return enqueue_scan_batch(c, n_files, bf.data(), io_type, LDB_TUPLE_INDEX, (hipStream_t)stream);
+  return enqueue_scan_batch(c, n_files, bf.data(), io_type, LDB_TUPLE_INDEX, (hipStream_t)stream, false);
 }
 
 const char* ldb_status_str(int s) {
@@ -3033,7 +3044,8 @@ int ldb_scan_files_dev(ldb_ctx* c, int n_files, const uint8_t* const* d_images, 
     std::vector<BatchFile> bf(n_files);
     for (int i = 0; i < n_files; ++i)
       bf[i] = BatchFile{d_images[i], lens[i], fids[i], d_outs[i], caps[i], d_results + i, nullptr};
-    return enqueue_scan_batch(c, n_files, bf.data(), io_type, tuple_kind, (hipStream_t)stream);
+    return enqueue_scan_batch(c, n_files, bf.data(), io_type, tuple_kind, (hipStream_t)stream,
+                              n_files <= kSweepSplitMax);
   }
   uint64_t mx = 0;
   for (int i = 0; i < n_files; ++i) mx = std::max(mx, lens[i]);

@@ -1,7 +1,7 @@
 """The batched replay (ldb_scan_files_dev: index.go:103-108's five value types at once) through the sweep
 tier: five Zipf-value logs (config 3's shape) and five writer-mix logs, each batch checked against the oracle
 (status, end, count, every tuple, the tier's share), then timed beside the same files scanned one by one
-(ldb_scan_file_dev). usage: python tools/batch_tier.py [MiB per file]"""
+(ldb_scan_file_dev). usage: python tools/batch_tier.py [MiB per file] [files per batch] [w: the writer mix only]"""
 import ctypes as C
 import os
 import sys
@@ -66,10 +66,12 @@ def run(eng, name, imgs, reps=10):
 
 def main():
     mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    nf = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     eng = Engine(0)
-    run(eng, "Zipf values (config 3 shape)",
-        [coracle.gen_log(mib << 20, 30 + i, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)[0] for i in range(5)])
-    run(eng, "writer mix", [coracle.gen_writer_log(mib << 20, 50 + i)[0] for i in range(5)])
+    if sys.argv[3:4] != ["w"]:
+        run(eng, "Zipf values (config 3 shape)",
+            [coracle.gen_log(mib << 20, 30 + i, ksize=64, value_mode=1, zipf_s=1.1, zipf_max=4096)[0] for i in range(nf)])
+    run(eng, "writer mix", [coracle.gen_writer_log(mib << 20, 50 + i)[0] for i in range(nf)])
     eng.close()
 
 
