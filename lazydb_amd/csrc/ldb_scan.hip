@@ -325,15 +325,15 @@ static_assert(sizeof(UniSetup) <= kUniSetupBytes, "run-prefix setup block");
 // offset 0 -- the same scan, without a run of one). Shifts come from the x^(8n) table (n <= kW).
 // Workgroup 0 publishes K = 0 or the entry size for the pipeline. Returns false when there is no run.
 // Every pipeline kernel serves one scan (its Pipe by value, p0) or, with kB, one file of a batched
-// scan: grid.y = file, its Pipe from the device array pb (enqueue_scan_batch).
+// scan: grid.y = file. k_sweep and k_region take a batch's pipes by value too (PipeArg: up to kUniBatch
+// of them in the kernel arguments), each read through the kernarg segment: pointers loaded from there are
+// known to be global, where pointers loaded from a device array of pipes left every access of the batched
+// kernels a FLAT one (round 6: k_region<true> 1088 flat instructions, k_sweep<true> 59; its workgroups ran
+// ~15 % slower than k_sweep<false>'s, tools/sw_trace.py)
 typedef __attribute__((address_space(4))) const Pipe* CPipe;
-// (a batched launch's pipe through the constant address space: the host wrote the array before the launch and
-// nothing changes it during one, so its fields can be re-read where a copy in global memory would spill SGPRs --
-// round 6: k_sweep<true> 38 SGPRs spilled into its stream loop)
 #define LDB_PIPE_SELECT                                                                              \
-  const Pipe& p = *(kB ? (const Pipe*)(CPipe)(pb + blockIdx.y)                                       \
-                       : (const Pipe*)(CPipe)__builtin_amdgcn_kernarg_segment_ptr());                \
-  (void)p0
+  const Pipe& p = *(const Pipe*)((CPipe)__builtin_amdgcn_kernarg_segment_ptr() + (kB ? blockIdx.y : 0u)); \
+  (void)a0
 
 // Header probes of a one-run launch (chunked, batched or hashed scans; every workgroup probes, 64 probes
 // in round 0: the device path's several runs use uni_search below, one workgroup). The first header
@@ -1455,6 +1455,8 @@ constexpr int kUniBatch = 16;
 struct UniBatch {
   Pipe p[kUniBatch];
 };
+template <bool kB>
+using PipeArg = typename std::conditional<kB, UniBatch, Pipe>::type;
 // the batched scan's fill: grid.y = file. With hashes (merge mode) the same pass also emits each run
 // entry's key hash (ldb::key_hash_w): one thread per entry reads its key as dword-aligned 16-B pieces.
 // In the verify loop the hash was serial work on one lane in G plus key loads issued after the CRC and
@@ -2184,21 +2186,14 @@ __device__ __forceinline__ uint32_t tail_items(uint64_t want, uint32_t ncu) {
 // there), every use inlined.
 template <bool kB>
 struct PipeSrc {
-  const Pipe* pb;
   CPipe ka;
   __device__ __forceinline__ const Pipe& get() const {
-    if constexpr (kB) {
-      const Pipe* q = pb + blockIdx.y;
-      asm volatile("" : "+s"(q));
-      return *q;
-    } else {
-      CPipe q = ka;
-      asm volatile("" : "+s"(q));
-      return *(const Pipe*)q;
-    }
+    CPipe q = kB ? ka + blockIdx.y : ka;
+    asm volatile("" : "+s"(q));
+    return *(const Pipe*)q;
   }
 };
-#define LDB_PIPE_SRC(kB) const PipeSrc<kB> src{pb, (CPipe)__builtin_amdgcn_kernarg_segment_ptr()}
+#define LDB_PIPE_SRC(kB) const PipeSrc<kB> src{(CPipe)__builtin_amdgcn_kernarg_segment_ptr()}
 
 // The phase protocol over Pipe::tail: [0, 8) tickets, [8, 16) items done, [16, 24) published, then the phases'
 // start stamps (u64 [16, 24)). s_tail_tk / s_tail_fl: the workgroup's broadcast words.
@@ -2286,12 +2281,28 @@ __device__ __forceinline__ bool tail_done(const Pipe& p) {   // after a wait: th
 // whose code it keeps: no phase protocol inside, so nothing is held across its stream loop -- the same body
 // behind k_region's tickets spilled SGPRs into that loop, 3 % slower), then the links by the last workgroup to
 // finish (a done counter, no waiting).
+#ifdef LDB_SW_TRACE
+// (trace builds: per workgroup of k_sweep, [file fid - 1][blockIdx.x] -> start, stream end, end, CU id; real-time
+// clock, 100 MHz; tools/sw_trace.py)
+constexpr int kSwTraceWgs = 8 * 1024;
+__device__ uint64_t g_swtrace[kSwTraceWgs * 4];
+#define LDB_SW_STAMP(k, v)                                                                            \
+  do {                                                                                                \
+    const uint64_t slot_ = (uint64_t)(p.fid - 1) * gridDim.x + blockIdx.x;                            \
+    if (threadIdx.x == 0 && slot_ < (uint64_t)kSwTraceWgs) g_swtrace[slot_ * 4 + (k)] = (v);            \
+  } while (0)
+#else
+#define LDB_SW_STAMP(k, v) do {} while (0)
+#endif
+
 template <bool kB>
-__global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p0, const Pipe* __restrict__ pb) {
+__global__ __launch_bounds__(64 * kSwWaves) void k_sweep(PipeArg<kB> a0) {
   __shared__ __attribute__((aligned(256))) uint8_t lds[cmax(kSwLds, kSwLinkLds)];
   __shared__ int s_last;
   LDB_PIPE_SELECT;
   if (!p.sweep || scan_done(p)) return;   // (uni_finish ended the scan)
+  LDB_SW_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  LDB_SW_STAMP(3, (uint64_t)__smid());
   int tabs = kLdsNone;
   // the shift tables first, then the LP2 block below 64 KiB, then the hit lists (kSwLds: every table base
   // in the DS instructions' 16-bit offsets, as k_uniform's LDB_UNI_LDS)
@@ -2299,6 +2310,7 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p0, const Pipe* __
              reinterpret_cast<uint32_t*>(lds + kSwShBytes + kLp2Bytes), tabs);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  LDB_SW_STAMP(1, __builtin_amdgcn_s_memrealtime());
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     s_last = atomicAdd(&p.tail[8 + kPhS], 1u) == gridDim.x - 1;
@@ -2307,12 +2319,13 @@ __global__ __launch_bounds__(64 * kSwWaves) void k_sweep(Pipe p0, const Pipe* __
   __syncthreads();
   if (!s_last) return;
   sweep_last(p, gridDim.x, lds);
+  LDB_SW_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
 
 template <bool kB>
-__global__ __launch_bounds__(64 * kWPB) void k_region(Pipe p0, const Pipe* __restrict__ pb, uint32_t ncu) {
+__global__ __launch_bounds__(64 * kWPB) void k_region(PipeArg<kB> a0, uint32_t ncu) {
   __shared__ __attribute__((aligned(256))) uint8_t lds[kRegionLds];
-  (void)p0;   // (read through src)
+  (void)a0;   // (read through src)
   LDB_PIPE_SRC(kB);
   if (scan_done(src.get())) return;   // the run prefix or the sweep tier ended the scan
   const TailSync ts;
@@ -2747,9 +2760,9 @@ int enqueue_scan(ldb_ctx* c, const uint8_t* d_img, uint64_t len, uint32_t fid, i
   return fence_ws(c, s);
 #endif
   // everything after the run prefix: the sweep tier (k_sweep), then the region pipeline (k_region)
-  hipLaunchKernelGGL(k_sweep<false>, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p, nullptr);
+  hipLaunchKernelGGL(k_sweep<false>, dim3(sweep_grid(c, len)), dim3(64 * kSwWaves), 0, s, p);
   if (ev) LDB_HIP(hipEventRecord(ev->es, s));
-  hipLaunchKernelGGL(k_region<false>, dim3(region_grid(c, L.nreg)), dim3(64 * kWPB), 0, s, p, nullptr, (uint32_t)c->n_cu);
+  hipLaunchKernelGGL(k_region<false>, dim3(region_grid(c, L.nreg)), dim3(64 * kWPB), 0, s, p, (uint32_t)c->n_cu);
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
@@ -2785,12 +2798,7 @@ __global__ __launch_bounds__(64) void k_batch_init(const Pipe* __restrict__ pb) 
   tail_init(p, threadIdx.x);
 }
 
-// split_sweep: one k_sweep launch per file (its pipe by value) instead of one over (vg, n) -- round 6: the 5 x
-// 512 MiB writer-mix batch 2.39 -> 2.19 ms (the sweep 1.87 -> ~1.67 ms), the Zipf batch unchanged, while the
-// merge's 16 mostly-uniform files lost 0.3 ms replay to 16 launches that return at once
-// (profiles/r06_sweep_split_ab.txt); the public batch API splits up to kSweepSplitMax files, the merge never
-constexpr int kSweepSplitMax = 8;
-int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s, bool split_sweep) {
+int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind, hipStream_t s) {
   if (!c || nf < 0 || (io != LDB_IO_FILEIO && io != LDB_IO_MMAP) ||
       (kind != LDB_TUPLE_INDEX && kind != LDB_TUPLE_ENTRY))
     return LDB_ERR_ARG;
@@ -2831,7 +2839,7 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     c->h_pipes[i].hash_out = f[i].hash_out;
   }
   const Pipe* d_pipes = reinterpret_cast<const Pipe*>(c->ws);
-  const Pipe p0{};   // unused by the kB instances
+  UniBatch ub{};   // a launch's pipes, by value (k_sweep<true>, k_region<true>)
   // k_sweep, k_region: the chip's workgroups dealt over the files, not one file's grid per file (round 3: 16 files of
   // 256 MiB launched 16 x 256 k_scan_main workgroups that queued behind each other even when every run
   // prefix covered its file; profiles/r03_s35_merge_spread_ab.json, r04_batch_spread_writer_mix_ab.txt)
@@ -2866,16 +2874,28 @@ int enqueue_scan_batch(ldb_ctx* c, int nf, const BatchFile* f, int io, int kind,
     }
   }
   if (ev) LDB_HIP(hipEventRecord(ev->eu, s));
-  static const int split_knob = ldb_knob_int("LDB_SWEEP_SPLIT", -1);   // (A/B: 0 never, 1 always)
-  if (split_knob == 1 || (split_knob < 0 && split_sweep))
+  // LDB_SWEEP_SPLIT=1 (A/B): one k_sweep launch per file instead of one over (vg, n). While the batch's pipes came
+  // from a device array (flat accesses) that won for the writer mix (2.39 -> 2.19 ms); with the pipes in the
+  // kernel arguments the one launch is level there and faster for Zipf values and the merge
+  // (profiles/r06_sweep_split_ab.txt, r06_batch_kernarg_ab.txt)
+  static const bool split = ldb_knob_int("LDB_SWEEP_SPLIT", 0) == 1;
+  if (split)
     for (unsigned i = 0; i < n; ++i)
       hipLaunchKernelGGL(k_sweep<false>, dim3(sweep_grid(c, c->h_pipes[i].len)), dim3(64 * kSwWaves), 0, s,
-                         c->h_pipes[i], nullptr);
+                         c->h_pipes[i]);
   else
-    hipLaunchKernelGGL(k_sweep<true>, dim3(sweep_grid(c, max_len), n), dim3(64 * kSwWaves), 0, s, p0, d_pipes);
+    for (int i0 = 0; i0 < nf; i0 += kUniBatch) {   // (the pipes by value: kUniBatch files per launch)
+      const int m = std::min(kUniBatch, nf - i0);
+      for (int i = 0; i < m; ++i) ub.p[i] = c->h_pipes[i0 + i];
+      hipLaunchKernelGGL(k_sweep<true>, dim3(sweep_grid(c, max_len), (unsigned)m), dim3(64 * kSwWaves), 0, s, ub);
+    }
   if (ev) LDB_HIP(hipEventRecord(ev->es, s));
-  hipLaunchKernelGGL(k_region<true>, dim3(std::min(tg, region_grid(c, max_nreg)), n), dim3(64 * kWPB), 0, s, p0, d_pipes,
-                     (uint32_t)c->n_cu);
+  for (int i0 = 0; i0 < nf; i0 += kUniBatch) {
+    const int m = std::min(kUniBatch, nf - i0);
+    for (int i = 0; i < m; ++i) ub.p[i] = c->h_pipes[i0 + i];
+    hipLaunchKernelGGL(k_region<true>, dim3(std::min(tg, region_grid(c, max_nreg)), (unsigned)m), dim3(64 * kWPB), 0, s,
+                       ub, (uint32_t)c->n_cu);
+  }
   if (ev) LDB_HIP(hipEventRecord(ev->e2, s));
   LDB_HIP(hipGetLastError());
   return fence_ws(c, s);
@@ -2922,7 +2942,7 @@ __attribute__((visibility("hidden"))) int ldb_scan_files_dev_batched(ldb_ctx* c,
     if (!batch_eligible(d_images[i], lens[i])) return LDB_ERR_ARG;
     bf[i] = BatchFile{d_images[i], lens[i], fids[i], d_outs[i], caps[i], d_results + i, d_hash ? d_hash[i] : nullptr};
   }
-  return enqueue_scan_batch(c, n_files, bf.data(), io_type, LDB_TUPLE_INDEX, (hipStream_t)stream, false);
+  return enqueue_scan_batch(c, n_files, bf.data(), io_type, LDB_TUPLE_INDEX, (hipStream_t)stream);
 }
 
 const char* ldb_status_str(int s) {
@@ -3044,8 +3064,7 @@ int ldb_scan_files_dev(ldb_ctx* c, int n_files, const uint8_t* const* d_images, 
     std::vector<BatchFile> bf(n_files);
     for (int i = 0; i < n_files; ++i)
       bf[i] = BatchFile{d_images[i], lens[i], fids[i], d_outs[i], caps[i], d_results + i, nullptr};
-    return enqueue_scan_batch(c, n_files, bf.data(), io_type, tuple_kind, (hipStream_t)stream,
-                              n_files <= kSweepSplitMax);
+    return enqueue_scan_batch(c, n_files, bf.data(), io_type, tuple_kind, (hipStream_t)stream);
   }
   uint64_t mx = 0;
   for (int i = 0; i < n_files; ++i) mx = std::max(mx, lens[i]);
@@ -3257,6 +3276,16 @@ int ldb_scan_copy_out(ldb_ctx* c, void* h_out, uint64_t cap, uint64_t* n_copied)
   return LDB_OK;
 }
 
+#ifdef LDB_SW_TRACE
+int ldb_debug_swtrace(uint64_t* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_swtrace), sizeof(g_swtrace)) != hipSuccess) return LDB_ERR_HIP;
+  if (reset) {
+    static uint64_t z[kSwTraceWgs * 4];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_swtrace), z, sizeof(z)) != hipSuccess) return LDB_ERR_HIP;
+  }
+  return LDB_OK;
+}
+#endif
 #ifdef LDB_STAMPS
 int ldb_debug_stamps(uint64_t* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 8 * kStampSlots) != hipSuccess) return LDB_ERR_HIP;
